@@ -1,0 +1,148 @@
+/*
+ * libbpe355 -- MI355X (gfx950) byte-level BPE trainer and encoder, C ABI.
+ *
+ * The drop-in boundary for gashon/transformer-lm's tokenizer path.  The reference has no
+ * FFI (it is pure Python); these entry points are what its two Python APIs bind to through
+ * ctypes (binding: transformer-lm_amd/bpe_amd/_lib.py):
+ *
+ *   bpe_train_file / bpe_train_buffer   <- train_bpe(input_path, vocab_size, special_tokens)
+ *                                          reference models/tokenizer/train.py:142-231
+ *   bpe_tok_create                      <- Tokenizer.__init__(vocab, merges, special_tokens)
+ *                                          reference models/tokenizer/tokenizer.py:12-38
+ *   bpe_tok_encode                      <- Tokenizer.encode(text)
+ *                                          reference models/tokenizer/tokenizer.py:111-138
+ *
+ * Conventions
+ *  - Every function returns 0 (BPE_OK) or a negative BPE_E_* code; bpe_last_error() gives the
+ *    message of the calling thread's last failure.  The Python binding maps BPE_E_IO to
+ *    OSError/FileNotFoundError, BPE_E_UTF8 to UnicodeDecodeError and BPE_E_KEY to KeyError,
+ *    the exception types the reference raises (train.py:22, tokenizer.py:135).
+ *  - Plain pointers and sizes only.  The library owns result objects until *_free().
+ *  - Byte-string lists cross the boundary as blobs: a sequence of (u32 little-endian length,
+ *    bytes) records.  Merges: (len a, a, len b, b) per merge, in creation order.  Vocab:
+ *    (len, bytes) per id, ids 0..n-1 in order (reference Vocab ids are dense, vocab.py:32).
+ *  - There is no CPU fallback: without a usable gfx950 device every compute call fails with
+ *    BPE_E_HIP.
+ */
+#ifndef BPE355_H
+#define BPE355_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BPE355_ABI_VERSION 1
+
+enum {
+    BPE_OK = 0,
+    BPE_E_IO = -1,       /* file could not be read (errno in bpe_last_errno()) */
+    BPE_E_UTF8 = -2,     /* input is not valid UTF-8 (reference: UnicodeDecodeError) */
+    BPE_E_KEY = -3,      /* a merged token is missing from the vocab (reference: KeyError) */
+    BPE_E_HIP = -4,      /* HIP runtime / device failure, or no gfx950 device */
+    BPE_E_ARG = -5,      /* invalid argument */
+    BPE_E_NOMEM = -6,    /* device or host allocation failed */
+    BPE_E_RCCL = -7,     /* collective failure */
+    BPE_E_LIMIT = -8     /* input exceeds a documented limit (pretoken > 16 MiB, corpus > 1 TiB) */
+};
+
+typedef struct bpe_result bpe_result;
+typedef struct bpe_tokenizer bpe_tokenizer;
+typedef struct bpe_comm bpe_comm;
+
+int bpe_abi_version(void);
+const char* bpe_last_error(void);
+int bpe_last_errno(void);
+/* number of visible gfx950 devices (0 if none); never fails */
+int bpe_device_count(void);
+
+/* ---------------------------------------------------------------- multi-GPU (RCCL) */
+/* One process per GPU.  Rank 0 creates the id, the caller broadcasts its 128 bytes (e.g. with
+ * torch.distributed), every rank calls bpe_comm_init.  A NULL comm means single GPU. */
+int bpe_comm_unique_id(uint8_t id_out[128]);
+int bpe_comm_init(const uint8_t id[128], int nranks, int rank, int device, bpe_comm** out);
+/* A host-staged communicator for testing the sharded path without RCCL: the library calls
+ * fn(ctx, buf, count) to all-reduce `count` int64 values in place (sum) on the host. */
+typedef int (*bpe_host_allreduce_fn)(void* ctx, int64_t* buf, size_t count);
+int bpe_comm_init_host(bpe_host_allreduce_fn fn, void* ctx, int nranks, int rank, int device,
+                       bpe_comm** out);
+void bpe_comm_free(bpe_comm* comm);
+
+/* ---------------------------------------------------------------- training */
+/* train_bpe(input_path, vocab_size, special_tokens): reads the file like the reference's
+ * open(path, "r", encoding="utf-8").read() (strict UTF-8, universal newlines).  With a comm,
+ * each rank passes ITS slab of the corpus (slabs must be cut at pre-token boundaries, see
+ * bpe_safe_split) and all ranks obtain the identical, global result. */
+int bpe_train_file(const char* path, int vocab_size, const char* const* specials, int n_specials,
+                   bpe_comm* comm, bpe_result** out);
+/* same, raw file bytes in host memory */
+int bpe_train_buffer(const uint8_t* data, size_t n, int vocab_size, const char* const* specials,
+                     int n_specials, bpe_comm* comm, bpe_result** out);
+/* same, raw bytes already resident in device memory (d_data on the current device; it is not
+ * modified).  stream may be NULL (the library's own stream). */
+int bpe_train_device(const uint8_t* d_data, size_t n, int vocab_size, const char* const* specials,
+                     int n_specials, bpe_comm* comm, void* hip_stream, bpe_result** out);
+
+int64_t bpe_result_n_merges(const bpe_result* r);
+int64_t bpe_result_n_vocab(const bpe_result* r);
+/* blob views owned by the result */
+size_t bpe_result_merges_blob(const bpe_result* r, const uint8_t** data);
+size_t bpe_result_vocab_blob(const bpe_result* r, const uint8_t** data);
+
+typedef struct {
+    double t_total_ms;        /* whole call, host wall clock */
+    double t_prepare_ms;      /* UTF-8 check + newline translation */
+    double t_count_ms;        /* pre-tokenize + unique-word count */
+    double t_words_ms;        /* word table + initial pair histogram */
+    double t_merge_ms;        /* merge loop */
+    double merge_kernel_ms;   /* summed device time of the merge-apply kernel (event-timed) */
+    int64_t merge_kernel_launches;
+    double merge_kernel_bytes; /* algorithmic bytes moved by those launches */
+    double count_kernel_ms;   /* device time of the pre-tokenize/count kernel */
+    double count_kernel_bytes;
+    int64_t n_bytes;          /* corpus bytes after newline translation (this rank) */
+    int64_t n_pretokens;      /* pre-tokens counted (this rank, excl. 1-byte and specials) */
+    int64_t n_words;          /* unique multi-byte words (this rank) */
+    int64_t n_word_tokens;    /* initial token slots over those words */
+    int64_t n_pairs_final;    /* pair-table keys at the end */
+    int64_t n_rebuilds;       /* candidate-set rebuilds */
+    int64_t n_rounds_device;  /* merges decided on the device */
+    int64_t n_rounds_host;    /* zero-count merges emitted after exhaustion */
+} bpe_train_stats;
+int bpe_result_stats(const bpe_result* r, bpe_train_stats* out);
+void bpe_result_free(bpe_result* r);
+
+/* Enable per-launch event timing of the hot kernels (bench / profiling); default off. */
+void bpe_set_timing(int enable);
+
+/* ---------------------------------------------------------------- tokenizer */
+/* Tokenizer(vocab, merges, special_tokens).  vocab blob: u32 count, then per entry
+ * (i64 id, u32 len, bytes) in the caller's dict order (the reverse map keeps the LAST id of a
+ * duplicated byte string, tokenizer.py:19).  merges blob: u32 count + merge records.
+ * specials: NULL/0 for none.  Missing specials are appended with ids len(vocab), ...
+ * (tokenizer.py:35-38); their ids are reported by bpe_tok_special_id. */
+int bpe_tok_create(const uint8_t* vocab_blob, size_t vocab_n, const uint8_t* merges_blob,
+                   size_t merges_n, const char* const* specials, int n_specials,
+                   bpe_tokenizer** out);
+int64_t bpe_tok_special_id(const bpe_tokenizer* tok, int i);
+/* encode(text): UTF-8 bytes in host memory -> ids.  cap >= n always suffices. */
+int bpe_tok_encode(bpe_tokenizer* tok, const uint8_t* utf8, size_t n, uint32_t* ids_out,
+                   size_t cap, size_t* n_out);
+/* same, device-resident text and output (d_out holds >= n ids) */
+int bpe_tok_encode_device(bpe_tokenizer* tok, const uint8_t* d_utf8, size_t n, uint32_t* d_out,
+                          size_t* n_out, void* hip_stream);
+void bpe_tok_free(bpe_tokenizer* tok);
+
+/* ---------------------------------------------------------------- helpers */
+/* Largest p <= pos such that splitting the text at p does not change its pre-tokenization
+ * (a U+0020 between two ASCII non-space bytes), or 0. Used to shard a corpus into slabs. */
+size_t bpe_safe_split(const uint8_t* data, size_t n, size_t pos);
+/* Deterministic synthetic corpus (bench/tests): n bytes of UTF-8 text into device memory. */
+int bpe_synth_corpus_device(uint8_t* d_out, size_t n, uint64_t seed, int flavour, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BPE355_H */

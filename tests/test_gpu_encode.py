@@ -1,0 +1,46 @@
+"""GPU parity: Tokenizer.encode (HIP) against the reference's encode goldens and the oracle."""
+import pytest
+
+import golden_cases as G
+import gpt2_files
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+bpe_amd = pytest.importorskip("bpe_amd")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    from bpe_amd import _lib
+    _lib.require_device()
+
+
+@pytest.mark.parametrize("name", G.names("encode"))
+def test_encode_matches_reference_golden(name):
+    o = G.load("encode", name)
+    vocab, merges = G.tokenizer_inputs(o)
+    tok = bpe_amd.Tokenizer(dict(vocab), list(merges), o["special_tokens"])
+    text = G.encode_text(o)
+    ids = tok.encode(text)
+    assert ids == o["ids"]
+    assert tok.decode(ids) == text.encode("utf-8").decode("utf-8", "replace")
+
+
+def test_encode_roundtrip_and_iterable():
+    vocab, merges = gpt2_files.load_gpt2(["<|endoftext|>"])
+    tok = bpe_amd.Tokenizer(vocab, merges, ["<|endoftext|>"])
+    with open(gpt2_files.FIXTURES / "tinystories_sample.txt", encoding="utf-8") as f:
+        ids_iter = list(tok.encode_iterable(f))
+    text = (gpt2_files.FIXTURES / "tinystories_sample.txt").read_text(encoding="utf-8")
+    assert ids_iter == tok.encode(text)
+    assert tok.decode(ids_iter) == text
+
+
+@pytest.mark.parametrize("seed,n_chars,flavour", [(21, 2_000_000, "mixed"), (22, 1_000_000, "space")])
+def test_encode_matches_oracle_synthetic(seed, n_chars, flavour):
+    import synth_text
+    vocab, merges = gpt2_files.load_gpt2(["<|endoftext|>"])
+    text = synth_text.generate(seed, n_chars, flavour)
+    tok = bpe_amd.Tokenizer(dict(vocab), list(merges), ["<|endoftext|>"])
+    assert tok.encode(text) == oracle.encode(vocab, merges, ["<|endoftext|>"], text)

@@ -1,0 +1,71 @@
+"""GPU parity: libbpe355's train_bpe (HIP, gfx950) against the reference goldens and the oracle.
+
+Bit-exact: ordered merges and the exact id -> bytes vocab must equal the reference's.
+"""
+import json
+import os
+
+import pytest
+
+import golden_cases as G
+import gpt2_files
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+bpe_amd = pytest.importorskip("bpe_amd")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    from bpe_amd import _lib
+    _lib.require_device()
+
+
+def test_reference_fixture_corpus_en_500():
+    """reference tests/test_train_bpe.py:28-65, through the drop-in train_bpe."""
+    vocab, merges = bpe_amd.train_bpe(gpt2_files.FIXTURES / "corpus.en", 500, ["<|endoftext|>"])
+    ref_vocab, ref_merges = gpt2_files.load_reference_train_golden()
+    assert merges == ref_merges
+    assert set(vocab.keys()) == set(ref_vocab.keys())
+    assert set(vocab.values()) == set(ref_vocab.values())
+
+
+@pytest.mark.parametrize("name", G.names("train"))
+def test_train_matches_reference_golden(name):
+    o, vocab, merges = G.train_expect(name)
+    data = G.input_bytes(o["input"])
+    got_vocab, got_merges = bpe_amd.train_bpe_bytes(data, o["vocab_size"], o["special_tokens"])
+    assert got_merges == merges
+    assert got_vocab == vocab
+
+
+def test_train_file_path_and_errors(tmp_path):
+    with pytest.raises(FileNotFoundError):
+        bpe_amd.train_bpe(tmp_path / "missing.txt", 300, [])
+    err = json.loads((G.GOLDEN / "error_train_bad_utf8.json").read_text())
+    p = tmp_path / "bad.txt"
+    p.write_bytes(bytes.fromhex(err["input_hex"]))
+    with pytest.raises(UnicodeDecodeError):
+        bpe_amd.train_bpe(p, 300, [])
+
+
+@pytest.mark.parametrize("seed,n_chars,flavour,vocab", [
+    (11, 3_000_000, "mixed", 4000),
+    (12, 2_000_000, "space", 3000),
+    (13, 8_000_000, "ascii", 6000),
+])
+def test_train_matches_oracle_synthetic(seed, n_chars, flavour, vocab):
+    import synth_text
+    data = synth_text.generate(seed, n_chars, flavour).encode("utf-8")
+    want = oracle.train_raw(data, vocab, ["<|endoftext|>"])
+    got = bpe_amd.train_bpe_bytes(data, vocab, ["<|endoftext|>"])
+    assert got[1] == want[1]
+    assert got[0] == want[0]
+
+
+def test_deterministic_repeat():
+    data = (gpt2_files.FIXTURES / "corpus.en").read_bytes()
+    r1 = bpe_amd.train_bpe_bytes(data, 1500, ["<|endoftext|>"])
+    r2 = bpe_amd.train_bpe_bytes(data, 1500, ["<|endoftext|>"])
+    assert r1 == r2

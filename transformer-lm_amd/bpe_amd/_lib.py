@@ -1,0 +1,172 @@
+"""ctypes binding of libbpe355 (include/bpe355.h).
+
+This is the whole host<->device boundary: plain pointers and sizes, the library owns result
+objects until *_free.  There is deliberately no CPU fallback: if the shared library is missing
+or no gfx950 device is visible, every compute call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import errno as _errno
+import os
+import pathlib
+import struct
+
+LIB_PATH = pathlib.Path(__file__).resolve().parent.parent / "lib" / "libbpe355.so"
+
+BPE_OK, BPE_E_IO, BPE_E_UTF8, BPE_E_KEY, BPE_E_HIP, BPE_E_ARG, BPE_E_NOMEM, BPE_E_RCCL, \
+    BPE_E_LIMIT = 0, -1, -2, -3, -4, -5, -6, -7, -8
+
+
+class LibraryMissing(RuntimeError):
+    pass
+
+
+class TrainStats(ctypes.Structure):
+    _fields_ = [
+        ("t_total_ms", ctypes.c_double), ("t_prepare_ms", ctypes.c_double),
+        ("t_count_ms", ctypes.c_double), ("t_words_ms", ctypes.c_double),
+        ("t_merge_ms", ctypes.c_double), ("merge_kernel_ms", ctypes.c_double),
+        ("merge_kernel_launches", ctypes.c_int64), ("merge_kernel_bytes", ctypes.c_double),
+        ("count_kernel_ms", ctypes.c_double), ("count_kernel_bytes", ctypes.c_double),
+        ("n_bytes", ctypes.c_int64), ("n_pretokens", ctypes.c_int64), ("n_words", ctypes.c_int64),
+        ("n_word_tokens", ctypes.c_int64), ("n_pairs_final", ctypes.c_int64),
+        ("n_rebuilds", ctypes.c_int64), ("n_rounds_device", ctypes.c_int64),
+        ("n_rounds_host", ctypes.c_int64),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+HOST_ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p,
+                                     ctypes.POINTER(ctypes.c_int64), ctypes.c_size_t)
+
+_lib = None
+
+# (name, restype, argtypes) for every symbol declared in include/bpe355.h
+_P = ctypes.c_void_p
+_U8P = ctypes.c_char_p
+_SZ = ctypes.c_size_t
+_SIGS = [
+    ("bpe_abi_version", ctypes.c_int, []),
+    ("bpe_last_error", ctypes.c_char_p, []),
+    ("bpe_last_errno", ctypes.c_int, []),
+    ("bpe_device_count", ctypes.c_int, []),
+    ("bpe_comm_unique_id", ctypes.c_int, [ctypes.c_char_p]),
+    ("bpe_comm_init", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.POINTER(_P)]),
+    ("bpe_comm_init_host", ctypes.c_int, [HOST_ALLREDUCE_FN, _P, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.POINTER(_P)]),
+    ("bpe_comm_free", None, [_P]),
+    ("bpe_train_file", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                      ctypes.c_int, _P, ctypes.POINTER(_P)]),
+    ("bpe_train_buffer", ctypes.c_int, [_U8P, _SZ, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                        ctypes.c_int, _P, ctypes.POINTER(_P)]),
+    ("bpe_train_device", ctypes.c_int, [_P, _SZ, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                        ctypes.c_int, _P, _P, ctypes.POINTER(_P)]),
+    ("bpe_result_n_merges", ctypes.c_int64, [_P]),
+    ("bpe_result_n_vocab", ctypes.c_int64, [_P]),
+    ("bpe_result_merges_blob", _SZ, [_P, ctypes.POINTER(_P)]),
+    ("bpe_result_vocab_blob", _SZ, [_P, ctypes.POINTER(_P)]),
+    ("bpe_result_stats", ctypes.c_int, [_P, ctypes.POINTER(TrainStats)]),
+    ("bpe_result_free", None, [_P]),
+    ("bpe_set_timing", None, [ctypes.c_int]),
+    ("bpe_tok_create", ctypes.c_int, [_U8P, _SZ, _U8P, _SZ, ctypes.POINTER(ctypes.c_char_p),
+                                      ctypes.c_int, ctypes.POINTER(_P)]),
+    ("bpe_tok_special_id", ctypes.c_int64, [_P, ctypes.c_int]),
+    ("bpe_tok_encode", ctypes.c_int, [_P, _U8P, _SZ, _P, _SZ, ctypes.POINTER(_SZ)]),
+    ("bpe_tok_encode_device", ctypes.c_int, [_P, _P, _SZ, _P, ctypes.POINTER(_SZ), _P]),
+    ("bpe_tok_free", None, [_P]),
+    ("bpe_safe_split", _SZ, [_U8P, _SZ, _SZ]),
+    ("bpe_synth_corpus_device", ctypes.c_int, [_P, _SZ, ctypes.c_uint64, ctypes.c_int, _P]),
+]
+SYMBOLS = [s[0] for s in _SIGS]
+
+
+def lib():
+    """Load libbpe355.so (built in-tree by __graft_entry__.build()).  Raises if missing."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise LibraryMissing(f"{LIB_PATH} not built; run `python -c 'import __graft_entry__ as g; "
+                                 "g.build()'` (hipcc --offload-arch=gfx950)")
+        L = ctypes.CDLL(str(LIB_PATH))
+        for name, res, args in _SIGS:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = ""):
+    if rc == BPE_OK:
+        return
+    msg = (lib().bpe_last_error() or b"").decode("utf-8", "replace")
+    if rc == BPE_E_IO:
+        en = lib().bpe_last_errno() or _errno.EIO
+        raise OSError(en, os.strerror(en), what or msg)
+    if rc == BPE_E_UTF8:
+        raise UnicodeDecodeError("utf-8", b"", 0, 1, msg)
+    if rc == BPE_E_KEY:
+        raise KeyError(msg)
+    raise RuntimeError(f"libbpe355 {what} failed ({rc}): {msg}")
+
+
+def require_device():
+    if lib().bpe_device_count() < 1:
+        raise RuntimeError("libbpe355 needs an MI355X (gfx950) GPU; none is visible")
+
+
+def c_strings(items):
+    items = list(items or [])
+    arr = (ctypes.c_char_p * max(1, len(items)))()
+    keep = [s.encode("utf-8") for s in items]
+    for i, b in enumerate(keep):
+        arr[i] = b
+    return arr, len(items), keep
+
+
+def iter_records(blob: bytes):
+    off, n = 0, len(blob)
+    while off < n:
+        ln = struct.unpack_from("<I", blob, off)[0]
+        off += 4
+        yield blob[off:off + ln]
+        off += ln
+
+
+def take_result(res: ctypes.c_void_p):
+    """-> (vocab dict[int, bytes], merges list[tuple[bytes, bytes]], stats dict); frees res."""
+    L = lib()
+    try:
+        p = ctypes.c_void_p()
+        n = L.bpe_result_merges_blob(res, ctypes.byref(p))
+        mb = ctypes.string_at(p, n) if n else b""
+        n = L.bpe_result_vocab_blob(res, ctypes.byref(p))
+        vb = ctypes.string_at(p, n) if n else b""
+        st = TrainStats()
+        check(L.bpe_result_stats(res, ctypes.byref(st)), "stats")
+    finally:
+        L.bpe_result_free(res)
+    it = iter_records(mb)
+    merges = [(a, next(it)) for a in it]
+    vocab = {i: b for i, b in enumerate(iter_records(vb))}
+    return vocab, merges, st.as_dict()
+
+
+def vocab_blob(vocab: dict) -> bytes:
+    parts = [struct.pack("<I", len(vocab))]
+    for i, b in vocab.items():
+        b = bytes(b)
+        parts.append(struct.pack("<qI", int(i), len(b)) + b)
+    return b"".join(parts)
+
+
+def merges_blob(merges) -> bytes:
+    parts = [struct.pack("<I", len(merges))]
+    for a, b in merges:
+        a, b = bytes(a), bytes(b)
+        parts.append(struct.pack("<I", len(a)) + a + struct.pack("<I", len(b)) + b)
+    return b"".join(parts)

@@ -1,0 +1,127 @@
+"""Tokenizer -- drop-in for reference models/tokenizer/tokenizer.py:11-167.
+
+Construction rules, special-token handling and the encode result follow the reference
+exactly; encode() runs on the GPU through libbpe355 (segmentation on special tokens,
+GPT-2 pre-tokenization, per-word rank-ordered merges, id lookup).  decode(), save() and
+from_files() are host-side byte/pickle plumbing, as in the reference.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import pickle
+from typing import Iterable, Iterator, List, Tuple
+
+from . import _lib
+from .train import train_bpe
+
+
+class Tokenizer:
+    def __init__(self, vocab: dict[int, bytes], merges: List[Tuple[bytes, bytes]],
+                 special_tokens: List[str] | None = []):
+        # tokenizer.py:18-38, including its bookkeeping quirks: vocab_inv keeps the LAST id of
+        # a repeated byte string, and a missing special is appended as
+        # self.vocab[bytes] = len(self.vocab) with vocab_inv[bytes] = len(self.vocab) - 1.
+        self.vocab = vocab
+        self.vocab_inv = {v: k for k, v in vocab.items()}
+        self.merges = merges
+        seen = set()
+        specials = []
+        for t in special_tokens or []:
+            if t not in seen:
+                seen.add(t)
+                specials.append(t)
+        # longest first; equal lengths keep first-occurrence order (the reference uses set
+        # iteration order there, which only matters for the ids of equal-length missing specials)
+        specials.sort(key=len, reverse=True)
+        self.special_tokens = specials
+        for token in self.special_tokens:
+            b = token.encode("utf-8")
+            if b not in self.vocab_inv:
+                self.vocab[b] = len(self.vocab)
+                self.vocab_inv[b] = len(self.vocab) - 1
+        self._handle = None
+
+    # ------------------------------------------------------------------ constructors
+    @classmethod
+    def train_from_file(cls, filepath: str, vocab_size: int, special_tokens: List[str]):
+        vocab, merges = train_bpe(filepath, vocab_size, special_tokens)
+        return cls(vocab, merges, special_tokens)
+
+    @classmethod
+    def fit(cls, input_path: str, vocab_size: int, special_tokens: List[str]):
+        vocab, merges = train_bpe(input_path, vocab_size, special_tokens)
+        return cls(vocab, merges, special_tokens)
+
+    @classmethod
+    def from_files(cls, vocab_filepath: str, merges_filepath: str,
+                   special_tokens: List[str] = []) -> "Tokenizer":
+        # files written by Tokenizer.save (the caller's own artifacts), as in tokenizer.py:50-61
+        with open(vocab_filepath, "rb") as f:
+            vocab = pickle.load(f)
+        with open(merges_filepath, "rb") as f:
+            merges = pickle.load(f)
+        return cls(vocab, merges, special_tokens=special_tokens)
+
+    # ------------------------------------------------------------------ device handle
+    def _device(self):
+        if self._handle is None:
+            L = _lib.lib()
+            inv = [(i, b) for b, i in self.vocab_inv.items()]
+            vb = _lib.vocab_blob(dict(inv) if len({i for i, _ in inv}) == len(inv) else {})
+            if len({i for i, _ in inv}) != len(inv):
+                # several byte strings share an id: pass the pairs as they are
+                import struct
+                vb = struct.pack("<I", len(inv)) + b"".join(
+                    struct.pack("<qI", int(i), len(b)) + bytes(b) for i, b in inv)
+            mb = _lib.merges_blob(self.merges)
+            arr, n, _keep = _lib.c_strings(self.special_tokens)
+            h = ctypes.c_void_p()
+            _lib.check(L.bpe_tok_create(vb, len(vb), mb, len(mb), arr, n, ctypes.byref(h)),
+                       "Tokenizer")
+            self._handle = h
+        return self._handle
+
+    def __del__(self):
+        h = getattr(self, "_handle", None)
+        if h is not None and _lib._lib is not None:
+            try:
+                _lib._lib.bpe_tok_free(h)
+            except Exception:  # noqa: BLE001
+                pass
+
+    # ------------------------------------------------------------------ encode / decode
+    def encode(self, text: str) -> List[int]:
+        """tokenizer.py:111-138 on the GPU."""
+        data = text.encode("utf-8")
+        h = self._device()
+        cap = max(1, len(data))
+        out = (ctypes.c_uint32 * cap)()
+        n_out = ctypes.c_size_t(0)
+        _lib.check(_lib.lib().bpe_tok_encode(h, data, len(data), out, cap, ctypes.byref(n_out)),
+                   "encode")
+        return list(out[: n_out.value])
+
+    def encode_iterable(self, iterable: Iterable[str]) -> Iterator[int]:
+        """tokenizer.py:140-150: concatenate items until >= 2 MiB characters, encode each chunk."""
+        it = iter(iterable)
+        while True:
+            text = ""
+            for line in it:
+                text += line
+                if len(text) >= 1024 * 1024 * 2:
+                    break
+            if not text:
+                break
+            yield from self.encode(text)
+
+    def decode(self, ids: List[int]) -> str:
+        raw = b"".join([self.vocab[i] for i in ids])
+        return raw.decode("utf-8", errors="replace")
+
+    def save(self, path: str, prefix: str = ""):
+        os.makedirs(path, exist_ok=True)
+        with open(os.path.join(path, prefix + "-vocab.pkl"), "wb+") as f:
+            pickle.dump(self.vocab, f)
+        with open(os.path.join(path, prefix + "-merges.pkl"), "wb+") as f:
+            pickle.dump(self.merges, f)

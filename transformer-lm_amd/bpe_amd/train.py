@@ -1,0 +1,69 @@
+"""train_bpe -- drop-in for reference models/tokenizer/train.py:142 (train_bpe).
+
+Same signature, same return value (vocab: dict[int, bytes], merges: list[tuple[bytes, bytes]]),
+same exceptions (FileNotFoundError / OSError, UnicodeDecodeError), bit-identical output.
+The work runs in libbpe355 on an MI355X: pre-tokenization, word counting, the pair histogram
+and the merge loop are HIP kernels (transformer-lm_amd/csrc).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List
+
+from . import _lib
+
+__all__ = ["train_bpe", "train_bpe_bytes", "last_train_stats"]
+
+_last_stats: dict = {}
+
+
+def last_train_stats() -> dict:
+    """Timings and counters of the most recent train_bpe call on this process."""
+    return dict(_last_stats)
+
+
+def _finish(rc, res, what):
+    global _last_stats
+    _lib.check(rc, what)
+    vocab, merges, stats = _lib.take_result(res)
+    _last_stats = stats
+    return vocab, merges
+
+
+def train_bpe(input_path: str | os.PathLike, vocab_size: int, special_tokens: List[str] = [],
+              comm=None):
+    """Train a byte-level BPE on the file at input_path (reference train.py:142-231).
+
+    comm: optional bpe_amd.dist.Communicator when each rank passes its own corpus slab.
+    """
+    L = _lib.lib()
+    arr, n, _keep = _lib.c_strings(special_tokens)
+    res = ctypes.c_void_p()
+    path = os.fsencode(os.fspath(input_path))
+    rc = L.bpe_train_file(path, int(vocab_size), arr, n, comm.handle if comm else None,
+                          ctypes.byref(res))
+    return _finish(rc, res, f"train_bpe({os.fspath(input_path)!r})")
+
+
+def train_bpe_bytes(data: bytes, vocab_size: int, special_tokens: List[str] = [], comm=None):
+    """train_bpe on the raw bytes of a file (decoded exactly like the file would be)."""
+    L = _lib.lib()
+    arr, n, _keep = _lib.c_strings(special_tokens)
+    res = ctypes.c_void_p()
+    rc = L.bpe_train_buffer(data, len(data), int(vocab_size), arr, n,
+                            comm.handle if comm else None, ctypes.byref(res))
+    return _finish(rc, res, "train_bpe_bytes")
+
+
+def train_bpe_device(d_ptr: int, n: int, vocab_size: int, special_tokens: List[str] = [],
+                     comm=None, stream: int = 0):
+    """train_bpe on raw bytes already resident in device memory (e.g. a torch uint8 CUDA
+    tensor's data_ptr()); used by bench.py so the timed region starts with data in HBM."""
+    L = _lib.lib()
+    arr, k, _keep = _lib.c_strings(special_tokens)
+    res = ctypes.c_void_p()
+    rc = L.bpe_train_device(ctypes.c_void_p(d_ptr), n, int(vocab_size), arr, k,
+                            comm.handle if comm else None, ctypes.c_void_p(stream or None),
+                            ctypes.byref(res))
+    return _finish(rc, res, "train_bpe_device")

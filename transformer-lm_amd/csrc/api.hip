@@ -1,0 +1,253 @@
+// C ABI of libbpe355 (include/bpe355.h): argument checking, error codes, result objects.
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <unordered_set>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+
+namespace bpe {
+
+namespace {
+thread_local std::string g_err;
+thread_local int g_errno = 0;
+bool g_timing = false;
+
+struct DeviceGuard {
+    // make sure a gfx950 device is present; there is no CPU fallback
+    static void require() {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+            throw Error{BPE_E_HIP, "no HIP device visible (libbpe355 needs an MI355X / gfx950 GPU)"};
+    }
+};
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        f();
+        g_err.clear();
+        return BPE_OK;
+    } catch (const Error& e) {
+        g_err = e.msg;
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        g_err = "host allocation failed";
+        return BPE_E_NOMEM;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return BPE_E_ARG;
+    }
+}
+
+std::vector<std::string> to_specials(const char* const* specials, int n) {
+    BPE_REQUIRE(n >= 0 && (n == 0 || specials), BPE_E_ARG, "bad special token list");
+    std::vector<std::string> v;
+    for (int i = 0; i < n; ++i) {
+        BPE_REQUIRE(specials[i], BPE_E_ARG, "null special token");
+        v.emplace_back(specials[i]);
+    }
+    return v;
+}
+
+struct StreamHolder {
+    hipStream_t s = nullptr;
+    bool own = false;
+    explicit StreamHolder(void* user) {
+        if (user) {
+            s = (hipStream_t)user;
+        } else {
+            BPE_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+            own = true;
+        }
+    }
+    ~StreamHolder() {
+        if (own && s) (void)hipStreamDestroy(s);
+    }
+};
+
+void put_u32(std::string& b, uint32_t v) { b.append(reinterpret_cast<const char*>(&v), 4); }
+
+}  // namespace
+
+void set_error(int, const std::string& msg) { g_err = msg; }
+bool timing_enabled() { return g_timing; }
+
+}  // namespace bpe
+
+struct bpe_result {
+    std::string merges_blob, vocab_blob;
+    int64_t n_merges = 0, n_vocab = 0;
+    bpe_train_stats stats{};
+};
+
+struct bpe_comm {
+    std::unique_ptr<bpe::Comm> impl;
+};
+
+namespace bpe {
+std::unique_ptr<Comm> make_rccl_comm(const uint8_t id[128], int nranks, int rank, int device);
+std::unique_ptr<Comm> make_host_comm(bpe_host_allreduce_fn fn, void* ctx, int nranks, int rank,
+                                     int device);
+}  // namespace bpe
+
+namespace {
+
+// Vocab(special_tokens) + add_token per merge (reference models/tokenizer/vocab.py:2-34)
+void finish_result(bpe::TrainOutput& out, const std::vector<std::string>& specials, bpe_result* r) {
+    std::vector<const std::string*> ids;
+    std::unordered_set<std::string> seen;
+    std::vector<std::string> extra;
+    extra.reserve(out.merges.size());
+    auto add = [&](const std::string& s) {
+        if (seen.insert(s).second) ids.push_back(&*seen.find(s));
+    };
+    for (const auto& s : specials) add(s);
+    for (int b = 0; b < 256; ++b) add(std::string(1, (char)b));
+    for (const auto& m : out.merges) add(m.first + m.second);
+    r->n_merges = (int64_t)out.merges.size();
+    r->n_vocab = (int64_t)ids.size();
+    for (const auto& m : out.merges) {
+        bpe::put_u32(r->merges_blob, (uint32_t)m.first.size());
+        r->merges_blob += m.first;
+        bpe::put_u32(r->merges_blob, (uint32_t)m.second.size());
+        r->merges_blob += m.second;
+    }
+    for (const auto* s : ids) {
+        bpe::put_u32(r->vocab_blob, (uint32_t)s->size());
+        r->vocab_blob += *s;
+    }
+    r->stats = out.stats;
+}
+
+int train_common(const uint8_t* d_data, size_t n, int vocab_size, const char* const* specials,
+                 int n_specials, bpe_comm* comm, void* stream, bpe_result** out) {
+    return bpe::guarded([&] {
+        BPE_REQUIRE(out, BPE_E_ARG, "out is NULL");
+        *out = nullptr;
+        bpe::DeviceGuard::require();
+        auto sp = bpe::to_specials(specials, n_specials);
+        bpe::StreamHolder sh(stream);
+        bpe::TrainOutput to;
+        bpe::train_on_device(d_data, n, vocab_size, sp, comm ? comm->impl.get() : nullptr, sh.s, to);
+        auto r = std::make_unique<bpe_result>();
+        finish_result(to, sp, r.get());
+        *out = r.release();
+    });
+}
+
+}  // namespace
+
+extern "C" {
+
+int bpe_abi_version(void) { return BPE355_ABI_VERSION; }
+const char* bpe_last_error(void) { return bpe::g_err.c_str(); }
+int bpe_last_errno(void) { return bpe::g_errno; }
+void bpe_set_timing(int enable) { bpe::g_timing = enable != 0; }
+
+int bpe_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    int k = 0;
+    for (int i = 0; i < n; ++i) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, i) == hipSuccess && std::strncmp(p.gcnArchName, "gfx950", 6) == 0) ++k;
+    }
+    return k;
+}
+
+int bpe_train_device(const uint8_t* d_data, size_t n, int vocab_size, const char* const* specials,
+                     int n_specials, bpe_comm* comm, void* hip_stream, bpe_result** out) {
+    if (n && !d_data) return bpe::guarded([] { throw bpe::Error{BPE_E_ARG, "data is NULL"}; });
+    return train_common(d_data, n, vocab_size, specials, n_specials, comm, hip_stream, out);
+}
+
+int bpe_train_buffer(const uint8_t* data, size_t n, int vocab_size, const char* const* specials,
+                     int n_specials, bpe_comm* comm, bpe_result** out) {
+    bpe::DevBuf<uint8_t> d;
+    int rc = bpe::guarded([&] {
+        BPE_REQUIRE(!n || data, BPE_E_ARG, "data is NULL");
+        bpe::DeviceGuard::require();
+        d.alloc(std::max<size_t>(n, 1));
+        if (n) BPE_HIP(hipMemcpy(d.p, data, n, hipMemcpyHostToDevice));
+    });
+    if (rc) return rc;
+    return train_common(d.p, n, vocab_size, specials, n_specials, comm, nullptr, out);
+}
+
+int bpe_train_file(const char* path, int vocab_size, const char* const* specials, int n_specials,
+                   bpe_comm* comm, bpe_result** out) {
+    std::string data;
+    int rc = bpe::guarded([&] {
+        BPE_REQUIRE(path, BPE_E_ARG, "path is NULL");
+        FILE* f = std::fopen(path, "rb");
+        if (!f) {
+            bpe::g_errno = errno;
+            throw bpe::Error{BPE_E_IO, std::string("cannot open ") + path + ": " + std::strerror(errno)};
+        }
+        std::fseek(f, 0, SEEK_END);
+        const long sz = std::ftell(f);
+        std::fseek(f, 0, SEEK_SET);
+        data.resize(sz > 0 ? (size_t)sz : 0);
+        const size_t got = data.empty() ? 0 : std::fread(&data[0], 1, data.size(), f);
+        std::fclose(f);
+        BPE_REQUIRE(got == data.size(), BPE_E_IO, std::string("short read on ") + path);
+    });
+    if (rc) return rc;
+    return bpe_train_buffer(reinterpret_cast<const uint8_t*>(data.data()), data.size(), vocab_size,
+                            specials, n_specials, comm, out);
+}
+
+int64_t bpe_result_n_merges(const bpe_result* r) { return r ? r->n_merges : -1; }
+int64_t bpe_result_n_vocab(const bpe_result* r) { return r ? r->n_vocab : -1; }
+size_t bpe_result_merges_blob(const bpe_result* r, const uint8_t** data) {
+    if (!r || !data) return 0;
+    *data = reinterpret_cast<const uint8_t*>(r->merges_blob.data());
+    return r->merges_blob.size();
+}
+size_t bpe_result_vocab_blob(const bpe_result* r, const uint8_t** data) {
+    if (!r || !data) return 0;
+    *data = reinterpret_cast<const uint8_t*>(r->vocab_blob.data());
+    return r->vocab_blob.size();
+}
+int bpe_result_stats(const bpe_result* r, bpe_train_stats* out) {
+    if (!r || !out) return BPE_E_ARG;
+    *out = r->stats;
+    return BPE_OK;
+}
+void bpe_result_free(bpe_result* r) { delete r; }
+
+int bpe_comm_unique_id(uint8_t id_out[128]);
+int bpe_comm_init(const uint8_t id[128], int nranks, int rank, int device, bpe_comm** out) {
+    return bpe::guarded([&] {
+        BPE_REQUIRE(out && id && nranks >= 1 && rank >= 0 && rank < nranks, BPE_E_ARG, "bad comm args");
+        auto c = std::make_unique<bpe_comm>();
+        c->impl = bpe::make_rccl_comm(id, nranks, rank, device);
+        *out = c.release();
+    });
+}
+int bpe_comm_init_host(bpe_host_allreduce_fn fn, void* ctx, int nranks, int rank, int device,
+                       bpe_comm** out) {
+    return bpe::guarded([&] {
+        BPE_REQUIRE(out && fn && nranks >= 1 && rank >= 0 && rank < nranks, BPE_E_ARG, "bad comm args");
+        auto c = std::make_unique<bpe_comm>();
+        c->impl = bpe::make_host_comm(fn, ctx, nranks, rank, device);
+        *out = c.release();
+    });
+}
+void bpe_comm_free(bpe_comm* comm) { delete comm; }
+
+size_t bpe_safe_split(const uint8_t* data, size_t n, size_t pos) {
+    auto ascii_nonspace = [](uint8_t b) { return b < 0x80 && b != 0x20 && (b < 0x09 || b > 0x0D); };
+    if (!data || n < 3) return 0;
+    if (pos > n - 2) pos = n - 2;
+    for (size_t p = pos; p >= 1; --p)
+        if (data[p] == 0x20 && ascii_nonspace(data[p - 1]) && ascii_nonspace(data[p + 1])) return p;
+    return 0;
+}
+
+}  // extern "C"

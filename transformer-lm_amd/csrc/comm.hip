@@ -1,0 +1,87 @@
+// Communicators for the sharded trainer: one process per GPU, corpus slabs per rank, one
+// sum all-reduce of the per-round pair deltas (and once of the initial byte-pair
+// histogram).  RCCL over xGMI in production; a host-staged variant lets the sharded path be
+// exercised by several processes that share one GPU (tests).
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "internal.h"
+
+namespace bpe {
+
+namespace {
+
+#define BPE_NCCL(expr)                                                                       \
+    do {                                                                                     \
+        ncclResult_t r_ = (expr);                                                            \
+        if (r_ != ncclSuccess)                                                               \
+            throw Error{BPE_E_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)};     \
+    } while (0)
+
+struct RcclComm final : Comm {
+    ncclComm_t comm = nullptr;
+    RcclComm(const uint8_t id[128], int n, int r, int dev) {
+        nranks = n;
+        rank = r;
+        device = dev;
+        BPE_HIP(hipSetDevice(dev));
+        ncclUniqueId uid;
+        static_assert(sizeof(uid.internal) == 128, "ncclUniqueId size");
+        std::memcpy(uid.internal, id, 128);
+        BPE_NCCL(ncclCommInitRank(&comm, n, uid, r));
+    }
+    ~RcclComm() override {
+        if (comm) (void)ncclCommDestroy(comm);
+    }
+    void allreduce_i64(int64_t* d_buf, size_t count, hipStream_t stream) override {
+        if (nranks == 1 || count == 0) return;
+        BPE_NCCL(ncclAllReduce(d_buf, d_buf, count, ncclInt64, ncclSum, comm, stream));
+    }
+};
+
+struct HostComm final : Comm {
+    bpe_host_allreduce_fn fn;
+    void* ctx;
+    std::vector<int64_t> buf;
+    HostComm(bpe_host_allreduce_fn f, void* c, int n, int r, int dev) : fn(f), ctx(c) {
+        nranks = n;
+        rank = r;
+        device = dev;
+    }
+    void allreduce_i64(int64_t* d_buf, size_t count, hipStream_t stream) override {
+        if (nranks == 1 || count == 0) return;
+        buf.resize(count);
+        BPE_HIP(hipMemcpyAsync(buf.data(), d_buf, count * 8, hipMemcpyDeviceToHost, stream));
+        BPE_HIP(hipStreamSynchronize(stream));
+        BPE_REQUIRE(fn(ctx, buf.data(), count) == 0, BPE_E_RCCL, "host all-reduce callback failed");
+        BPE_HIP(hipMemcpyAsync(d_buf, buf.data(), count * 8, hipMemcpyHostToDevice, stream));
+        BPE_HIP(hipStreamSynchronize(stream));
+    }
+};
+
+}  // namespace
+
+std::unique_ptr<Comm> make_rccl_comm(const uint8_t id[128], int nranks, int rank, int device) {
+    return std::make_unique<RcclComm>(id, nranks, rank, device);
+}
+std::unique_ptr<Comm> make_host_comm(bpe_host_allreduce_fn fn, void* ctx, int nranks, int rank,
+                                     int device) {
+    return std::make_unique<HostComm>(fn, ctx, nranks, rank, device);
+}
+
+}  // namespace bpe
+
+extern "C" int bpe_comm_unique_id(uint8_t id_out[128]) {
+    if (!id_out) return BPE_E_ARG;
+    ncclUniqueId uid;
+    const ncclResult_t r = ncclGetUniqueId(&uid);
+    if (r != ncclSuccess) {
+        bpe::set_error(BPE_E_RCCL, ncclGetErrorString(r));
+        return BPE_E_RCCL;
+    }
+    std::memcpy(id_out, uid.internal, 128);
+    return BPE_OK;
+}

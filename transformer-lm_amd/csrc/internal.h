@@ -1,0 +1,55 @@
+// Host-side interfaces shared by the libbpe355 translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "bpe_common.h"
+
+namespace bpe {
+
+// ---------------------------------------------------------------- communicator
+// Sum-all-reduce of int64 buffers across the ranks that each own one corpus slab.
+struct Comm {
+    int nranks = 1, rank = 0, device = 0;
+    virtual ~Comm() = default;
+    // in-place sum over ranks of d_buf[0..count) (device memory), ordered on `stream`
+    virtual void allreduce_i64(int64_t* d_buf, size_t count, hipStream_t stream) = 0;
+};
+
+// ---------------------------------------------------------------- text preparation
+// Validates strict UTF-8 and applies universal newlines (reference train.py:22 text-mode
+// read).  Returns the device pointer to use (d_in itself when no \r is present, else
+// `scratch`) and the resulting length.  Throws Error{BPE_E_UTF8} on bad input.
+const uint8_t* prepare_text(const uint8_t* d_in, size_t n, DevBuf<uint8_t>& scratch,
+                            size_t* n_out, hipStream_t stream);
+
+// ---------------------------------------------------------------- unique-word count
+struct WordCounts {
+    DevBuf<unsigned long long> key;   // (len << 40) | (offset + 1); 0 = empty
+    DevBuf<unsigned long long> cnt;
+    size_t cap = 0;
+    uint64_t n_pretokens = 0;         // multi-byte pre-tokens seen
+};
+// Pre-tokenize text[0..n) with the GPT-2 pattern and count the multi-byte words.
+// (Single-byte words carry no pairs and cannot affect training.)
+void count_words(const uint8_t* d_text, size_t n, WordCounts& wc, hipStream_t stream,
+                 float* kernel_ms);
+
+// ---------------------------------------------------------------- training driver
+struct TrainOutput {
+    std::vector<std::pair<uint32_t, uint32_t>> merges_internal;  // (a, b) internal ids
+    std::vector<std::string> tok_bytes;                          // internal id -> bytes
+    std::vector<std::pair<std::string, std::string>> merges;     // byte pairs, in order
+    bpe_train_stats stats{};
+};
+void train_on_device(const uint8_t* d_raw, size_t n, int vocab_size,
+                     const std::vector<std::string>& specials, Comm* comm, hipStream_t stream,
+                     TrainOutput& out);
+
+bool timing_enabled();
+
+}  // namespace bpe

@@ -1,0 +1,234 @@
+// Text preparation and unique-word counting on the device.
+//
+//   prepare_text : reference models/tokenizer/train.py:22, open(path, "r", encoding="utf-8")
+//                  .read() -- strict UTF-8 (UnicodeDecodeError) + universal newlines.
+//   count_words  : reference models/tokenizer/train.py:16-28 extract_subword_frequencies,
+//                  GPT-2 pattern of train.py:143-146 (pretok.h).
+//
+// HBM layout: the corpus is read once, coalesced; the word-count table is two flat u64
+// arrays (key, count) of power-of-two capacity.  A key packs (length << 40 | offset + 1):
+// the offset of the first occurrence that claimed the slot IS the word's identity, so a
+// single 64-bit CAS publishes a slot completely and a later thread verifies a match by
+// comparing bytes against the corpus itself -- exact counting with no spin-waits.
+#include <hipcub/hipcub.hpp>
+
+#include "internal.h"
+#include "pretok.h"
+
+namespace bpe {
+
+// ------------------------------------------------------------------ UTF-8 validation
+__device__ __forceinline__ int utf8_len_valid(const uint8_t* __restrict__ s, size_t n, size_t i) {
+    const uint32_t b0 = s[i];
+    uint32_t need, lo = 0x80, hi = 0xBF;
+    if (b0 < 0x80u) return 1;
+    if (b0 >= 0xC2u && b0 <= 0xDFu) need = 2;
+    else if (b0 == 0xE0u) { need = 3; lo = 0xA0; }
+    else if (b0 >= 0xE1u && b0 <= 0xECu) need = 3;
+    else if (b0 == 0xEDu) { need = 3; hi = 0x9F; }
+    else if (b0 >= 0xEEu && b0 <= 0xEFu) need = 3;
+    else if (b0 == 0xF0u) { need = 4; lo = 0x90; }
+    else if (b0 >= 0xF1u && b0 <= 0xF3u) need = 4;
+    else if (b0 == 0xF4u) { need = 4; hi = 0x8F; }
+    else return 0;
+    if (i + need > n) return 0;
+    const uint32_t b1 = s[i + 1];
+    if (b1 < lo || b1 > hi) return 0;
+    for (uint32_t k = 2; k < need; ++k)
+        if ((s[i + k] & 0xC0u) != 0x80u) return 0;
+    return (int)need;
+}
+
+// byte i is well-formed iff it is ASCII, a lead byte of a valid sequence, or a continuation
+// byte covered by the nearest lead byte within 3 positions before it.
+__device__ __forceinline__ bool byte_ok(const uint8_t* __restrict__ s, size_t n, size_t i) {
+    const uint32_t b = s[i];
+    if (b < 0x80u) return true;
+    if ((b & 0xC0u) != 0x80u) return utf8_len_valid(s, n, i) > 0;
+    size_t q = i;
+    for (int k = 0; k < 3 && q > 0; ++k) {
+        --q;
+        if ((s[q] & 0xC0u) != 0x80u) {
+            const int l = utf8_len_valid(s, n, q);
+            return l > 0 && i < q + (size_t)l;
+        }
+    }
+    return false;
+}
+
+constexpr int kValidateBytes = 16;
+
+__global__ void k_validate(const uint8_t* __restrict__ s, size_t n,
+                           unsigned long long* __restrict__ err_pos, unsigned* __restrict__ has_cr) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t lo = t * kValidateBytes;
+    if (lo >= n) return;
+    bool cr = false;
+    if (lo + kValidateBytes <= n && (((uintptr_t)(s + lo)) & 15) == 0) {
+        const uint4 v = *reinterpret_cast<const uint4*>(s + lo);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        uint32_t hi_bits = 0, cr_bits = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            hi_bits |= w[k] & 0x80808080u;
+            const uint32_t x = w[k] ^ 0x0D0D0D0Du;                 // zero byte <=> '\r'
+            cr_bits |= (x - 0x01010101u) & ~x & 0x80808080u;
+        }
+        if (cr_bits) atomicOr(has_cr, 1u);
+        if (!hi_bits) return;                                       // all ASCII: done
+    }
+    const size_t hi = lo + kValidateBytes < n ? lo + kValidateBytes : n;
+    for (size_t i = lo; i < hi; ++i) {
+        if (s[i] == 0x0D) cr = true;
+        if (!byte_ok(s, n, i)) {
+            atomicMin(err_pos, (unsigned long long)i);
+            break;
+        }
+    }
+    if (cr) atomicOr(has_cr, 1u);
+}
+
+// universal newlines: "\r\n" -> "\n", lone "\r" -> "\n"
+__global__ void k_newline_map(const uint8_t* __restrict__ s, size_t n, uint8_t* __restrict__ out,
+                              uint8_t* __restrict__ keep) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t b = s[i];
+    out[i] = (b == 0x0D) ? 0x0A : b;
+    keep[i] = !(b == 0x0D && i + 1 < n && s[i + 1] == 0x0A);
+}
+
+const uint8_t* prepare_text(const uint8_t* d_in, size_t n, DevBuf<uint8_t>& scratch,
+                            size_t* n_out, hipStream_t stream) {
+    *n_out = n;
+    if (n == 0) return d_in;
+    DevBuf<unsigned long long> flags(2);
+    unsigned long long h_init[2] = {~0ULL, 0ULL};
+    BPE_HIP(hipMemcpyAsync(flags.p, h_init, sizeof(h_init), hipMemcpyHostToDevice, stream));
+    const size_t threads = (n + kValidateBytes - 1) / kValidateBytes;
+    hipLaunchKernelGGL(k_validate, dim3(ceil_div(threads, 256)), dim3(256), 0, stream, d_in, n,
+                       flags.p, reinterpret_cast<unsigned*>(flags.p + 1));
+    BPE_HIP(hipGetLastError());
+    unsigned long long h[2];
+    BPE_HIP(hipMemcpyAsync(h, flags.p, sizeof(h), hipMemcpyDeviceToHost, stream));
+    BPE_HIP(hipStreamSynchronize(stream));
+    if (h[0] != ~0ULL)
+        throw Error{BPE_E_UTF8, "'utf-8' codec can't decode byte at position " + std::to_string(h[0])};
+    if ((unsigned)h[1] == 0) return d_in;
+
+    DevBuf<uint8_t> mapped(n), keep(n);
+    scratch.alloc(n);
+    hipLaunchKernelGGL(k_newline_map, dim3(ceil_div(n, 256)), dim3(256), 0, stream, d_in, n,
+                       mapped.p, keep.p);
+    DevBuf<unsigned long long> d_nsel(1);
+    size_t tmp_bytes = 0;
+    BPE_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmp_bytes, mapped.p, keep.p, scratch.p,
+                                          d_nsel.p, (int64_t)n, stream));
+    DevBuf<uint8_t> tmp(tmp_bytes);
+    BPE_HIP(hipcub::DeviceSelect::Flagged(tmp.p, tmp_bytes, mapped.p, keep.p, scratch.p, d_nsel.p,
+                                          (int64_t)n, stream));
+    unsigned long long nsel = 0;
+    BPE_HIP(hipMemcpyAsync(&nsel, d_nsel.p, 8, hipMemcpyDeviceToHost, stream));
+    BPE_HIP(hipStreamSynchronize(stream));
+    *n_out = (size_t)nsel;
+    return scratch.p;
+}
+
+// ------------------------------------------------------------------ word counting
+constexpr unsigned long long kOffMask = (1ULL << 40) - 1;
+constexpr int kMaxProbe = 1 << 16;
+
+__device__ __forceinline__ bool bytes_equal(const uint8_t* __restrict__ x,
+                                            const uint8_t* __restrict__ y, size_t len) {
+    for (size_t i = 0; i < len; ++i)
+        if (x[i] != y[i]) return false;
+    return true;
+}
+
+// Each thread owns a nominal span [t*span, (t+1)*span): it starts at the first safe point
+// at or after the span start and stops at the first safe point at or after the span end,
+// so the spans tile the text exactly along token boundaries.
+__global__ void __launch_bounds__(256) k_count_words(const uint8_t* __restrict__ s, size_t n,
+                                                     size_t span,
+                                                     unsigned long long* __restrict__ key,
+                                                     unsigned long long* __restrict__ cnt,
+                                                     size_t mask, unsigned* __restrict__ status,
+                                                     unsigned long long* __restrict__ n_tok) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t lo = t * span;
+    if (lo >= n) return;
+    const size_t hi = lo + span;
+    size_t p = (t == 0) ? 0 : next_safe_point(s, n, lo);
+    unsigned long long ntok = 0;
+    while (p < n) {
+        if (p >= hi && is_safe_point(s, n, p)) break;
+        const size_t e = token_end(s, n, p);
+        const size_t len = e - p;
+        if (len >= 2) {
+            ++ntok;
+            if (len >= (1ULL << 24)) { atomicOr(status, 2u); p = e; continue; }
+            const unsigned long long mine = ((unsigned long long)len << 40) | (p + 1);
+            size_t slot = hash_word(s + p, len) & mask;
+            int probe = 0;
+            for (; probe < kMaxProbe; ++probe) {
+                unsigned long long k = key[slot];
+                if (k == 0) {
+                    k = atomicCAS(&key[slot], 0ULL, mine);
+                    if (k == 0) { atomicAdd(&cnt[slot], 1ULL); break; }
+                }
+                if ((k >> 40) == len && bytes_equal(s + ((k & kOffMask) - 1), s + p, len)) {
+                    atomicAdd(&cnt[slot], 1ULL);
+                    break;
+                }
+                slot = (slot + 1) & mask;
+            }
+            if (probe == kMaxProbe) atomicOr(status, 1u);
+        }
+        p = e;
+    }
+    if (ntok) atomicAdd(n_tok, ntok);
+}
+
+void count_words(const uint8_t* d_text, size_t n, WordCounts& wc, hipStream_t stream,
+                 float* kernel_ms) {
+    BPE_REQUIRE(n < (1ULL << 40) - 1, BPE_E_LIMIT, "corpus slab larger than 1 TiB");
+    size_t cap = next_pow2(std::max<size_t>(1 << 16, n / 96));
+    constexpr size_t kSpan = 256;
+    DevBuf<unsigned> status(1);
+    DevBuf<unsigned long long> ntok(1);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (kernel_ms) {
+        BPE_HIP(hipEventCreate(&e0));
+        BPE_HIP(hipEventCreate(&e1));
+    }
+    for (int attempt = 0;; ++attempt) {
+        wc.key.alloc(cap);
+        wc.cnt.alloc(cap);
+        wc.cap = cap;
+        BPE_HIP(hipMemsetAsync(wc.key.p, 0, wc.key.bytes(), stream));
+        BPE_HIP(hipMemsetAsync(wc.cnt.p, 0, wc.cnt.bytes(), stream));
+        BPE_HIP(hipMemsetAsync(status.p, 0, 4, stream));
+        BPE_HIP(hipMemsetAsync(ntok.p, 0, 8, stream));
+        if (n) {
+            const size_t threads = (n + kSpan - 1) / kSpan;
+            if (kernel_ms) BPE_HIP(hipEventRecord(e0, stream));
+            hipLaunchKernelGGL(k_count_words, dim3(ceil_div(threads, 256)), dim3(256), 0, stream,
+                               d_text, n, kSpan, wc.key.p, wc.cnt.p, cap - 1, status.p, ntok.p);
+            BPE_HIP(hipGetLastError());
+            if (kernel_ms) BPE_HIP(hipEventRecord(e1, stream));
+        }
+        unsigned st = 0;
+        BPE_HIP(hipMemcpyAsync(&st, status.p, 4, hipMemcpyDeviceToHost, stream));
+        BPE_HIP(hipMemcpyAsync(&wc.n_pretokens, ntok.p, 8, hipMemcpyDeviceToHost, stream));
+        BPE_HIP(hipStreamSynchronize(stream));
+        if (st & 2u) throw Error{BPE_E_LIMIT, "a pre-token is longer than 16 MiB"};
+        if (kernel_ms && n) BPE_HIP(hipEventElapsedTime(kernel_ms, e0, e1));
+        if (!(st & 1u)) break;
+        BPE_REQUIRE(attempt < 4, BPE_E_NOMEM, "word table overflow");
+        cap *= 4;  // the table filled up: grow and recount
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+}
+
+}  // namespace bpe

@@ -1,0 +1,1083 @@
+// BPE merge loop on the device.
+//
+// Reference semantics (models/tokenizer/train.py):
+//   31-49    words -> byte ids, pair histogram weighted by word count
+//   183-189  rounds = vocab_size - len(vocab); best = max(pairs, key=(count, (bytes a, bytes b)))
+//            over every key still in the dict (count 0 included); stop early only if empty
+//   190-224  new = a + b; rewrite every word left to right, non-overlapping; per occurrence
+//            (x, a) -= c, (x, new) += c for the rewritten left neighbour x, and
+//            (b, y) -= c, (new, y) += c for the original right neighbour y
+//   226-228  pop best; append (a, b) to merges
+// Tokens are identified by their bytes (vocab.py:29): a merge whose bytes already exist
+// reuses that token's id (token dedupe below).
+//
+// Device design (one HIP stream, three kernels per round, batched host checks):
+//   K1 k_merge  : every workgroup reduces K3's per-block partials to the round's best pair,
+//                 resolves the new token id (hash map over token bytes), counts its rank
+//                 among all tokens (for the lexicographic tie-break); block 0 records the
+//                 merge and the new token.  Then all workgroups rewrite the active words
+//                 that contain (a, b) in place and accumulate, per neighbour token, the
+//                 left/right deltas L[x], R[y] (int64).
+//   [allreduce of L/R over ranks when sharded]
+//   K2 k_apply  : for every token x with L[x] / R[y] != 0 apply the four pair updates to the
+//                 pair hash table, mark touched keys present, add keys that cross the
+//                 candidate threshold T to the candidate list C; update lexicographic ranks.
+//   K3 k_argmax : argmax over C of (count, rank(a), rank(b)) -> per-block partials.
+// Every key with count >= T is in C (they only rise by crossing T inside K2), so the max of
+// C is the global max whenever it is >= T; otherwise the host rebuilds C with a lower T.
+// Zero-count keys that are still "present" (touched and never popped) are exactly the
+// reference's leftover dict keys; once no positive count remains (every word is a single
+// token) the reference pops them in descending byte order, which the host reproduces.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cstring>
+#include <map>
+#include <set>
+#include <unordered_map>
+
+#include "internal.h"
+
+namespace bpe {
+
+namespace {
+
+constexpr unsigned kPresent = 1u, kInC = 2u;
+enum : int { HALT_NONE = 0, HALT_REBUILD = 1, HALT_DONE = 2 };
+enum : unsigned { ERR_PAIRS_FULL = 1u, ERR_C_FULL = 2u, ERR_POOL = 4u };
+constexpr unsigned long long kPolyP = 0x100000001B3ULL * 0x9E3779B97F4A7C15ULL | 1ULL;
+
+struct RoundState {
+    int halt;
+    int round;
+    int n_rounds;
+    int ntok;
+    long long T;
+    unsigned nC, capC;
+    unsigned cur_a, cur_b, cur_new, cur_slot;
+    long long cur_cnt;
+    int new_is_new;
+    unsigned new_rank[2];
+    unsigned err;
+    unsigned n_act;
+    unsigned n_single;
+    unsigned pool_used, pool_cap;
+    unsigned long long pair_used;
+    unsigned long long scan_slots;
+};
+
+struct Partial {
+    long long cnt;
+    unsigned long long tb;
+    unsigned slot, pad;
+};
+
+struct PairsDev {
+    unsigned long long* key;  // ((a << 32) | b) + 1, 0 = empty
+    long long* cnt;
+    unsigned* flag;           // kPresent | kInC
+    size_t mask;
+    unsigned* C;
+};
+
+struct ToksDev {
+    uint8_t* pool;
+    uint32_t* off;
+    uint32_t* len;
+    unsigned long long* hash;  // polynomial hash of the bytes
+    unsigned long long* pw;    // P^len
+    unsigned long long* key8;  // first 8 bytes, big-endian, zero padded
+    uint32_t* rank;            // lexicographic rank among live tokens
+    uint32_t* map;             // hash -> id + 1
+    uint32_t map_mask;
+};
+
+template <class TokT>
+struct WordsDev {
+    TokT* tok;
+    const uint32_t* wbeg;
+    uint32_t* wlen;
+    const unsigned long long* wcnt;
+    const uint32_t* act;
+};
+
+template <class TokT> struct Chunk;
+template <> struct Chunk<uint16_t> { static constexpr int N = 8; };
+template <> struct Chunk<uint32_t> { static constexpr int N = 4; };
+
+__device__ __forceinline__ bool cand_better(long long c1, unsigned long long t1, long long c2,
+                                            unsigned long long t2) {
+    return c1 > c2 || (c1 == c2 && t1 > t2);
+}
+
+template <class T>
+__device__ __forceinline__ T wave_sum(T v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// ------------------------------------------------------------------ pair table
+__device__ __forceinline__ size_t pair_slot(const PairsDev& P, unsigned long long key,
+                                            RoundState* st) {
+    size_t s = mix64(key) & P.mask;
+    for (size_t probe = 0; probe <= P.mask; ++probe) {
+        unsigned long long k = P.key[s];
+        if (k == key) return s;
+        if (k == 0) {
+            k = atomicCAS(&P.key[s], 0ULL, key);
+            if (k == 0) {
+                atomicAdd(&st->pair_used, 1ULL);
+                return s;
+            }
+            if (k == key) return s;
+        }
+        s = (s + 1) & P.mask;
+    }
+    atomicOr(&st->err, ERR_PAIRS_FULL);
+    return ~(size_t)0;
+}
+
+// frequencies[(p, q)] += d with the reference's defaultdict semantics (the key becomes
+// present); increments that lift a key across T enter the candidate list.
+__device__ __forceinline__ void pair_update(const PairsDev& P, RoundState* st, unsigned p,
+                                            unsigned q, long long d, long long T) {
+    const unsigned long long key = ((((unsigned long long)p) << 32) | q) + 1ULL;
+    const size_t s = pair_slot(P, key, st);
+    if (s == ~(size_t)0) return;
+    const long long old = (long long)atomicAdd((unsigned long long*)&P.cnt[s], (unsigned long long)d);
+    const bool cross = d > 0 && old < T && old + d >= T;
+    unsigned f = kPresent | (cross ? kInC : 0u);
+    if (!cross && (P.flag[s] & kPresent)) return;
+    const unsigned prev = atomicOr(&P.flag[s], f);
+    if (cross && !(prev & kInC)) {
+        const unsigned idx = atomicAdd(&st->nC, 1u);
+        if (idx < st->capC) P.C[idx] = (unsigned)s;
+        else atomicOr(&st->err, ERR_C_FULL);
+    }
+}
+
+// ------------------------------------------------------------------ token helpers
+__device__ __forceinline__ unsigned long long concat_key8(const ToksDev& K, unsigned a, unsigned b) {
+    const unsigned la = K.len[a];
+    const unsigned long long ka = K.key8[a];
+    if (la >= 8) return ka;
+    return ka | (K.key8[b] >> (8 * la));
+}
+
+__device__ __forceinline__ uint8_t concat_byte(const ToksDev& K, unsigned a, unsigned la,
+                                               unsigned b, unsigned i) {
+    return i < la ? K.pool[K.off[a] + i] : K.pool[K.off[b] + (i - la)];
+}
+
+// -1 / 0 / +1: bytes(x) vs bytes(a) + bytes(b)
+__device__ int cmp_with_concat(const ToksDev& K, unsigned x, unsigned a, unsigned b,
+                               unsigned long long k8new) {
+    const unsigned long long kx = K.key8[x];
+    if (kx != k8new) return kx < k8new ? -1 : 1;
+    const unsigned lx = K.len[x], la = K.len[a], ln = la + K.len[b];
+    const unsigned m = lx < ln ? lx : ln;
+    const uint8_t* px = K.pool + K.off[x];
+    for (unsigned i = 8; i < m; ++i) {
+        const uint8_t bx = px[i], bn = concat_byte(K, a, la, b, i);
+        if (bx != bn) return bx < bn ? -1 : 1;
+    }
+    return lx < ln ? -1 : (lx > ln ? 1 : 0);
+}
+
+__device__ bool equals_concat(const ToksDev& K, unsigned x, unsigned a, unsigned b) {
+    const unsigned la = K.len[a], ln = la + K.len[b];
+    if (K.len[x] != ln) return false;
+    const uint8_t* px = K.pool + K.off[x];
+    for (unsigned i = 0; i < ln; ++i)
+        if (px[i] != concat_byte(K, a, la, b, i)) return false;
+    return true;
+}
+
+// ------------------------------------------------------------------ K1: merge
+struct BestShared {
+    int stop;
+    unsigned a, b, nw, slot, isnew;
+    long long cnt;
+    unsigned long long hash, k8;
+    int round, ntok;
+};
+
+template <class TokT>
+__global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
+                                               const Partial* __restrict__ part, int nparts,
+                                               PairsDev P, ToksDev K, WordsDev<TokT> W,
+                                               unsigned long long* __restrict__ LR,
+                                               uint32_t* __restrict__ m_a, uint32_t* __restrict__ m_b,
+                                               uint32_t* __restrict__ m_new) {
+    __shared__ BestShared sb;
+    __shared__ unsigned long long s_red[4];
+    const int tid = threadIdx.x;
+    if (tid < 64) {
+        // every workgroup redundantly decides the round: no extra launch, no grid sync
+        int stop = HALT_NONE;
+        const int halt = st->halt, round = st->round;
+        if (halt) stop = -1;
+        else if (round >= st->n_rounds) stop = HALT_DONE;
+        long long bc = LLONG_MIN;
+        unsigned long long bt = 0;
+        unsigned bs = 0;
+        if (!stop) {
+            for (int i = tid; i < nparts; i += 64) {
+                const Partial pp = part[i];
+                if (cand_better(pp.cnt, pp.tb, bc, bt)) { bc = pp.cnt; bt = pp.tb; bs = pp.slot; }
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+                const long long oc = __shfl_xor(bc, o);
+                const unsigned long long ot = __shfl_xor(bt, o);
+                const unsigned os = __shfl_xor(bs, o);
+                if (cand_better(oc, ot, bc, bt)) { bc = oc; bt = ot; bs = os; }
+            }
+            if (bc < st->T) stop = HALT_REBUILD;
+        }
+        if (tid == 0) {
+            sb.stop = stop;
+            if (!stop) {
+                const unsigned long long key = P.key[bs] - 1ULL;
+                const unsigned a = (unsigned)(key >> 32), b = (unsigned)(key & 0xffffffffu);
+                const int ntok = st->ntok;
+                // token dedupe: does bytes(a) + bytes(b) already exist?
+                const unsigned long long h = K.hash[a] * K.pw[b] + K.hash[b];
+                const unsigned ln = K.len[a] + K.len[b];
+                unsigned nw = (unsigned)ntok;
+                unsigned s = (unsigned)mix64(h) & K.map_mask;
+                for (unsigned m; (m = K.map[s]) != 0; s = (s + 1) & K.map_mask) {
+                    const unsigned id = m - 1;
+                    if (K.hash[id] == h && K.len[id] == ln && equals_concat(K, id, a, b)) {
+                        nw = id;
+                        break;
+                    }
+                }
+                sb.a = a; sb.b = b; sb.nw = nw; sb.slot = bs; sb.cnt = bc;
+                sb.isnew = (nw == (unsigned)ntok);
+                sb.hash = h; sb.k8 = concat_key8(K, a, b);
+                sb.round = round; sb.ntok = ntok;
+            }
+        }
+    }
+    __syncthreads();
+    if (sb.stop) {
+        if (blockIdx.x == 0 && tid == 0 && sb.stop > 0) st->halt = sb.stop;
+        return;
+    }
+    const unsigned a = sb.a, b = sb.b, nw = sb.nw;
+    const int ntok = sb.ntok;
+
+    if (blockIdx.x == 0) {  // record the merge and register a new token
+        if (tid == 0) {
+            st->cur_a = a; st->cur_b = b; st->cur_new = nw; st->cur_slot = sb.slot;
+            st->cur_cnt = sb.cnt; st->new_is_new = (int)sb.isnew;
+            m_a[sb.round] = a; m_b[sb.round] = b; m_new[sb.round] = nw;
+        }
+        if (sb.isnew) {
+            const unsigned la = K.len[a], ln = la + K.len[b];
+            const unsigned base = st->pool_used;
+            if (base + ln <= st->pool_cap) {
+                for (unsigned i = tid; i < ln; i += blockDim.x)
+                    K.pool[base + i] = concat_byte(K, a, la, b, i);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                if (base + ln > st->pool_cap) atomicOr(&st->err, ERR_POOL);
+                K.off[nw] = base; K.len[nw] = ln;
+                K.hash[nw] = sb.hash; K.pw[nw] = K.pw[a] * K.pw[b]; K.key8[nw] = sb.k8;
+                st->pool_used = base + ln;
+            }
+        }
+    }
+
+    // rank of the new token = number of live tokens with smaller bytes (a slice per block)
+    if (sb.isnew) {
+        const unsigned per = (ntok + gridDim.x - 1) / gridDim.x;
+        const unsigned lo = blockIdx.x * per;
+        unsigned less = 0;
+        for (unsigned x = lo + tid; x < lo + per && x < (unsigned)ntok; x += blockDim.x)
+            less += cmp_with_concat(K, x, a, b, sb.k8) < 0;
+        less = wave_sum(less);
+        if ((tid & 63) == 0 && less) atomicAdd(&st->new_rank[sb.round & 1], less);
+    }
+
+    // rewrite every active word containing (a, b)
+    constexpr int CH = Chunk<TokT>::N;
+    const unsigned n_act = st->n_act;
+    unsigned long long scanned = 0;
+    unsigned singles = 0;
+    for (unsigned i = blockIdx.x * blockDim.x + tid; i < n_act; i += gridDim.x * blockDim.x) {
+        const uint32_t w = W.act[i];
+        const uint32_t len = W.wlen[w];
+        if (len < 2) continue;
+        scanned += len;
+        TokT* t = W.tok + W.wbeg[w];
+        bool hit = false;
+        TokT prev = 0;
+        for (uint32_t base = 0; base < len && !hit; base += CH) {
+            TokT v[CH];
+            *reinterpret_cast<uint4*>(v) = *reinterpret_cast<const uint4*>(t + base);
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                const uint32_t idx = base + k;
+                if (idx < len) {
+                    if (idx > 0 && prev == (TokT)a && v[k] == (TokT)b) hit = true;
+                    prev = v[k];
+                }
+            }
+        }
+        if (!hit) continue;
+        const unsigned long long c = W.wcnt[w];
+        uint32_t j = 0, r = 0;
+        while (r < len) {
+            const TokT x = t[r];
+            if (x == (TokT)a && r + 1 < len && t[r + 1] == (TokT)b) {
+                if (j > 0) atomicAdd(&LR[2 * (size_t)t[j - 1]], c);          // (x,a)-=c (x,new)+=c
+                if (r + 2 < len) atomicAdd(&LR[2 * (size_t)t[r + 2] + 1], c); // (b,y)-=c (new,y)+=c
+                t[j++] = (TokT)nw;
+                r += 2;
+            } else {
+                t[j++] = x;
+                ++r;
+            }
+        }
+        W.wlen[w] = j;
+        singles += (j < 2);
+    }
+    scanned = wave_sum(scanned);
+    singles = wave_sum(singles);
+    if ((tid & 63) == 0) {
+        if (scanned) atomicAdd(&st->scan_slots, scanned);
+        if (singles) atomicAdd(&st->n_single, singles);
+    }
+    (void)s_red;
+}
+
+// ------------------------------------------------------------------ K2: apply deltas
+__global__ void __launch_bounds__(256) k_apply(RoundState* __restrict__ st, PairsDev P, ToksDev K,
+                                               unsigned long long* __restrict__ LR) {
+    if (st->halt) return;
+    const unsigned x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int isnew = st->new_is_new;
+    const unsigned ntok = (unsigned)st->ntok + (unsigned)isnew;
+    const unsigned a = st->cur_a, b = st->cur_b, nw = st->cur_new;
+    const int round = st->round;
+    const long long T = st->T;
+    if (x == 0) {
+        const unsigned bs = st->cur_slot;  // pop(best_pair)
+        P.cnt[bs] = 0;
+        atomicAnd(&P.flag[bs], ~kPresent);
+        st->new_rank[(round + 1) & 1] = 0;
+        if (isnew) {
+            unsigned s = (unsigned)mix64(K.hash[nw]) & K.map_mask;
+            while (K.map[s] != 0) s = (s + 1) & K.map_mask;
+            K.map[s] = nw + 1;
+        }
+    }
+    if (x >= ntok) return;
+    if (isnew) {
+        const unsigned rnew = st->new_rank[round & 1];
+        if (x == nw) K.rank[x] = rnew;
+        else {
+            const unsigned r = K.rank[x];
+            K.rank[x] = r + (r >= rnew);
+        }
+    }
+    const long long l = (long long)LR[2 * (size_t)x];
+    const long long r = (long long)LR[2 * (size_t)x + 1];
+    if (l) {
+        LR[2 * (size_t)x] = 0;
+        if (!(x == a && a == b)) pair_update(P, st, x, a, -l, T);
+        pair_update(P, st, x, nw, l, T);
+    }
+    if (r) {
+        LR[2 * (size_t)x + 1] = 0;
+        if (!(x == b && a == b)) pair_update(P, st, b, x, -r, T);
+        pair_update(P, st, nw, x, r, T);
+    }
+}
+
+// ------------------------------------------------------------------ K3: argmax over C
+__global__ void __launch_bounds__(256) k_argmax(RoundState* __restrict__ st, PairsDev P,
+                                                const uint32_t* __restrict__ rank,
+                                                Partial* __restrict__ part, int advance) {
+    __shared__ long long sc[4];
+    __shared__ unsigned long long stb[4];
+    __shared__ unsigned ss[4];
+    if (st->halt) return;
+    const unsigned nC = st->nC;
+    long long bc = LLONG_MIN;
+    unsigned long long bt = 0;
+    unsigned bs = 0;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < nC; i += gridDim.x * blockDim.x) {
+        const unsigned s = P.C[i];
+        if (!(P.flag[s] & kPresent)) continue;
+        const long long c = P.cnt[s];
+        const unsigned long long key = P.key[s] - 1ULL;
+        const unsigned long long tb =
+            ((unsigned long long)rank[key >> 32] << 32) | rank[key & 0xffffffffu];
+        if (cand_better(c, tb, bc, bt)) { bc = c; bt = tb; bs = s; }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const long long oc = __shfl_xor(bc, o);
+        const unsigned long long ot = __shfl_xor(bt, o);
+        const unsigned os = __shfl_xor(bs, o);
+        if (cand_better(oc, ot, bc, bt)) { bc = oc; bt = ot; bs = os; }
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sc[w] = bc; stb[w] = bt; ss[w] = bs; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
+            if (cand_better(sc[k], stb[k], bc, bt)) { bc = sc[k]; bt = stb[k]; bs = ss[k]; }
+        part[blockIdx.x] = Partial{bc, bt, bs, 0};
+        if (advance && blockIdx.x == 0) {
+            st->round += 1;
+            st->ntok += st->new_is_new;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ word table build
+__global__ void k_collect_words(const unsigned long long* __restrict__ key,
+                                const unsigned long long* __restrict__ cnt, size_t cap,
+                                const uint8_t* __restrict__ text, const uint8_t* __restrict__ sp_bytes,
+                                const uint32_t* __restrict__ sp_off, const uint32_t* __restrict__ sp_len,
+                                int n_sp, unsigned long long* __restrict__ w_off,
+                                uint32_t* __restrict__ w_len, unsigned long long* __restrict__ w_cnt,
+                                unsigned* __restrict__ n_words, unsigned* __restrict__ max_len) {
+    const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= cap) return;
+    const unsigned long long k = key[s];
+    if (!k) return;
+    const unsigned len = (unsigned)(k >> 40);
+    const unsigned long long off = (k & ((1ULL << 40) - 1)) - 1;
+    for (int i = 0; i < n_sp; ++i) {  // train.py:25 skips matches equal to a special token
+        if (sp_len[i] != len) continue;
+        bool eq = true;
+        for (unsigned j = 0; j < len && eq; ++j) eq = text[off + j] == sp_bytes[sp_off[i] + j];
+        if (eq) return;
+    }
+    const unsigned idx = atomicAdd(n_words, 1u);
+    w_off[idx] = off; w_len[idx] = len; w_cnt[idx] = cnt[s];
+    atomicMax(max_len, len);
+}
+
+__global__ void k_chunks(const uint32_t* __restrict__ w_len, unsigned n, int ch,
+                         uint32_t* __restrict__ nch) {
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) nch[i] = (w_len[i] + ch - 1) / ch;
+}
+
+template <class TokT>
+__global__ void k_fill_words(const uint8_t* __restrict__ text, const unsigned long long* __restrict__ w_off,
+                             const uint32_t* __restrict__ w_len, const unsigned long long* __restrict__ w_cnt,
+                             const uint32_t* __restrict__ chunk_beg, unsigned n, int ch,
+                             TokT* __restrict__ tok, uint32_t* __restrict__ wbeg,
+                             uint32_t* __restrict__ act, unsigned long long* __restrict__ hist) {
+    const unsigned w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= n) return;
+    const uint32_t beg = chunk_beg[w] * ch, len = w_len[w];
+    const uint8_t* src = text + w_off[w];
+    const unsigned long long c = w_cnt[w];
+    wbeg[w] = beg;
+    act[w] = w;
+    unsigned prev = src[0];
+    tok[beg] = (TokT)prev;
+    for (uint32_t i = 1; i < len; ++i) {
+        const unsigned cur = src[i];
+        tok[beg + i] = (TokT)cur;
+        atomicAdd(&hist[prev * 256 + cur], c);   // train.py:45-46
+        prev = cur;
+    }
+}
+
+__global__ void k_init_pairs(const unsigned long long* __restrict__ hist, PairsDev P,
+                             RoundState* st) {
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 65536) return;
+    const long long c = (long long)hist[i];
+    if (c <= 0) return;
+    const unsigned long long key = ((((unsigned long long)(i >> 8)) << 32) | (i & 255u)) + 1ULL;
+    const size_t s = pair_slot(P, key, st);
+    if (s == ~(size_t)0) return;
+    P.cnt[s] = c;
+    P.flag[s] = kPresent;
+}
+
+__global__ void k_init_tokens(ToksDev K) {
+    const unsigned i = threadIdx.x;  // 256 threads
+    K.pool[i] = (uint8_t)i;
+    K.off[i] = i;
+    K.len[i] = 1;
+    K.hash[i] = i;
+    K.pw[i] = kPolyP;
+    K.key8[i] = (unsigned long long)i << 56;
+    K.rank[i] = i;
+    __syncthreads();
+    if (i == 0) {
+        for (unsigned t = 0; t < 256; ++t) {
+            unsigned s = (unsigned)mix64(t) & K.map_mask;
+            while (K.map[s] != 0) s = (s + 1) & K.map_mask;
+            K.map[s] = t + 1;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ rebuild helpers
+struct RebuildStats {
+    unsigned long long bins[64];
+    unsigned long long ghosts;
+    unsigned long long sub[1024];
+};
+
+__global__ void k_rebuild_hist(PairsDev P, size_t cap, RebuildStats* rs) {
+    __shared__ unsigned long long sh[64];
+    if (threadIdx.x < 64) sh[threadIdx.x] = 0;
+    __syncthreads();
+    unsigned long long ghosts = 0;
+    for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap;
+         s += (size_t)gridDim.x * blockDim.x) {
+        if (!(P.flag[s] & kPresent)) continue;
+        const long long c = P.cnt[s];
+        if (c <= 0) { ghosts += (c == 0); continue; }
+        atomicAdd(&sh[63 - __clzll((unsigned long long)c)], 1ULL);
+    }
+    ghosts = wave_sum(ghosts);
+    if ((threadIdx.x & 63) == 0 && ghosts) atomicAdd(&rs->ghosts, ghosts);
+    __syncthreads();
+    if (threadIdx.x < 64 && sh[threadIdx.x]) atomicAdd(&rs->bins[threadIdx.x], sh[threadIdx.x]);
+}
+
+__global__ void k_rebuild_sub(PairsDev P, size_t cap, long long lo, long long width,
+                              RebuildStats* rs) {
+    for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap;
+         s += (size_t)gridDim.x * blockDim.x) {
+        if (!(P.flag[s] & kPresent)) continue;
+        const long long c = P.cnt[s];
+        if (c < lo || c >= lo + width * 1024) continue;
+        atomicAdd(&rs->sub[(c - lo) / width], 1ULL);
+    }
+}
+
+__global__ void k_build_C(PairsDev P, size_t cap, long long T, RoundState* st) {
+    for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap;
+         s += (size_t)gridDim.x * blockDim.x) {
+        const unsigned f = P.flag[s];
+        const bool in = (f & kPresent) && P.cnt[s] >= T;
+        if (in) {
+            const unsigned idx = atomicAdd(&st->nC, 1u);
+            if (idx < st->capC) P.C[idx] = (unsigned)s;
+            else atomicOr(&st->err, ERR_C_FULL);
+            if (!(f & kInC)) P.flag[s] = f | kInC;
+        } else if (f & kInC) {
+            P.flag[s] = f & ~kInC;
+        }
+    }
+}
+
+__global__ void k_collect_present(PairsDev P, size_t cap, unsigned long long* out,
+                                  unsigned* n_out) {
+    for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap;
+         s += (size_t)gridDim.x * blockDim.x) {
+        if (P.flag[s] & kPresent) out[atomicAdd(n_out, 1u)] = P.key[s] - 1ULL;
+    }
+}
+
+__global__ void k_rehash(const unsigned long long* __restrict__ okey, const long long* __restrict__ ocnt,
+                         const unsigned* __restrict__ oflag, size_t ocap, PairsDev P, RoundState* st) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ocap) return;
+    const unsigned long long k = okey[i];
+    if (!k) return;
+    const size_t s = pair_slot(P, k, st);
+    if (s == ~(size_t)0) return;
+    P.cnt[s] = ocnt[i];
+    P.flag[s] = oflag[i] & kPresent;
+}
+
+__global__ void k_flag_active(const uint32_t* __restrict__ act, unsigned n,
+                              const uint32_t* __restrict__ wlen, uint8_t* __restrict__ keep) {
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) keep[i] = wlen[act[i]] >= 2;
+}
+
+// ------------------------------------------------------------------ host driver
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+struct Timer {
+    hipEvent_t a = nullptr, b = nullptr;
+};
+
+template <class TokT>
+class MergeLoop {
+   public:
+    MergeLoop(hipStream_t stream, Comm* comm, const uint8_t* text, int n_rounds, TrainOutput& out)
+        : s_(stream), comm_(comm), text_(text), n_rounds_(n_rounds), out_(out) {}
+
+    void build_words(const WordCounts& wc, const std::vector<std::string>& specials);
+    void run();
+
+   private:
+    static constexpr int CH = Chunk<TokT>::N;
+    static constexpr int kBatch = 64;
+    static constexpr int kMergeBlocks = 1024;
+    static constexpr int kArgBlocks = 64;
+    static constexpr unsigned long long kTarget = 4096;
+
+    void alloc_pairs(size_t cap);
+    void grow_pairs();
+    void ensure_pool(unsigned need);
+    void push_state() { BPE_HIP(hipMemcpyAsync(st_.p, &hs_, sizeof(hs_), hipMemcpyHostToDevice, s_)); }
+    void pull_state() {
+        BPE_HIP(hipMemcpyAsync(&hs_, st_.p, sizeof(hs_), hipMemcpyDeviceToHost, s_));
+        BPE_HIP(hipStreamSynchronize(s_));
+    }
+    int rebuild();  // 0 ok, 1 exhausted (only zero-count keys), 2 empty
+    void exhaustion();
+    void compact();
+    PairsDev pairs() const { return PairsDev{pkey_.p, pcnt_.p, pflag_.p, pcap_ - 1, C_.p}; }
+    ToksDev toks() const {
+        return ToksDev{pool_.p, toff_.p, tlen_.p, thash_.p, tpw_.p, tkey8_.p, trank_.p, tmap_.p,
+                       (uint32_t)(tmap_.n - 1)};
+    }
+    WordsDev<TokT> words() const { return WordsDev<TokT>{tok_.p, wbeg_.p, wlen_.p, wcnt_.p, act_.p}; }
+
+    hipStream_t s_;
+    Comm* comm_;
+    const uint8_t* text_;
+    int n_rounds_;
+    TrainOutput& out_;
+
+    RoundState hs_{};
+    DevBuf<RoundState> st_;
+    // words
+    unsigned n_words_ = 0, max_len_ = 0;
+    DevBuf<TokT> tok_;
+    DevBuf<uint32_t> wbeg_, wlen_, act_, act2_;
+    DevBuf<unsigned long long> wcnt_;
+    DevBuf<unsigned long long> hist_;
+    // pairs
+    size_t pcap_ = 0;
+    DevBuf<unsigned long long> pkey_;
+    DevBuf<long long> pcnt_;
+    DevBuf<unsigned> pflag_, C_;
+    // tokens
+    unsigned tok_cap_ = 0;
+    DevBuf<uint8_t> pool_;
+    DevBuf<uint32_t> toff_, tlen_, trank_, tmap_;
+    DevBuf<unsigned long long> thash_, tpw_, tkey8_;
+    DevBuf<unsigned long long> LR_;
+    DevBuf<Partial> part_;
+    DevBuf<uint32_t> m_a_, m_b_, m_new_;
+    DevBuf<RebuildStats> rs_;
+};
+
+template <class TokT>
+void MergeLoop<TokT>::build_words(const WordCounts& wc, const std::vector<std::string>& specials) {
+    // specials -> device (compared once per unique word, not per occurrence)
+    std::string spb;
+    std::vector<uint32_t> spo, spl;
+    for (const auto& s : specials) { spo.push_back((uint32_t)spb.size()); spl.push_back((uint32_t)s.size()); spb += s; }
+    DevBuf<uint8_t> d_spb(std::max<size_t>(spb.size(), 1));
+    DevBuf<uint32_t> d_spo(std::max<size_t>(spo.size(), 1)), d_spl(std::max<size_t>(spl.size(), 1));
+    if (!spb.empty()) BPE_HIP(hipMemcpyAsync(d_spb.p, spb.data(), spb.size(), hipMemcpyHostToDevice, s_));
+    if (!spo.empty()) {
+        BPE_HIP(hipMemcpyAsync(d_spo.p, spo.data(), spo.size() * 4, hipMemcpyHostToDevice, s_));
+        BPE_HIP(hipMemcpyAsync(d_spl.p, spl.data(), spl.size() * 4, hipMemcpyHostToDevice, s_));
+    }
+    // compact the occupied count-table slots into (offset, len, count) records
+    DevBuf<unsigned> cnts(2);
+    BPE_HIP(hipMemsetAsync(cnts.p, 0, 8, s_));
+    // upper bound on words: occupied slots (<= cap); count first cheaply by reusing the kernel
+    DevBuf<unsigned long long> w_off(wc.cap), w_cnt(wc.cap);
+    DevBuf<uint32_t> w_len(wc.cap);
+    hipLaunchKernelGGL(k_collect_words, dim3(ceil_div(wc.cap, 256)), dim3(256), 0, s_, wc.key.p,
+                       wc.cnt.p, wc.cap, text_, d_spb.p, d_spo.p, d_spl.p, (int)specials.size(),
+                       w_off.p, w_len.p, w_cnt.p, cnts.p, cnts.p + 1);
+    BPE_HIP(hipGetLastError());
+    unsigned h2[2];
+    BPE_HIP(hipMemcpyAsync(h2, cnts.p, 8, hipMemcpyDeviceToHost, s_));
+    BPE_HIP(hipStreamSynchronize(s_));
+    n_words_ = h2[0];
+    max_len_ = h2[1];
+    const unsigned n = n_words_;
+    // chunked token storage: each word starts on a 16-byte boundary
+    DevBuf<uint32_t> nch(std::max(n, 1u)), cbeg(std::max(n, 1u) + 1);
+    unsigned total_chunks = 0;
+    if (n) {
+        hipLaunchKernelGGL(k_chunks, dim3(ceil_div(n, 256)), dim3(256), 0, s_, w_len.p, n, CH, nch.p);
+        size_t tb = 0;
+        BPE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, nch.p, cbeg.p, (int)n, s_));
+        DevBuf<uint8_t> tmp(tb);
+        BPE_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, nch.p, cbeg.p, (int)n, s_));
+        unsigned last[2];
+        BPE_HIP(hipMemcpyAsync(&last[0], cbeg.p + n - 1, 4, hipMemcpyDeviceToHost, s_));
+        BPE_HIP(hipMemcpyAsync(&last[1], nch.p + n - 1, 4, hipMemcpyDeviceToHost, s_));
+        BPE_HIP(hipStreamSynchronize(s_));
+        total_chunks = last[0] + last[1];
+    }
+    BPE_REQUIRE((unsigned long long)total_chunks * CH < (1ULL << 32), BPE_E_LIMIT,
+                "word table exceeds 2^32 token slots");
+    tok_.alloc((size_t)std::max(total_chunks, 1u) * CH);
+    wbeg_.alloc(std::max(n, 1u));
+    wlen_.alloc(std::max(n, 1u));
+    wcnt_.alloc(std::max(n, 1u));
+    act_.alloc(std::max(n, 1u));
+    hist_.alloc(65536);
+    BPE_HIP(hipMemsetAsync(hist_.p, 0, hist_.bytes(), s_));
+    if (n) {
+        BPE_HIP(hipMemcpyAsync(wlen_.p, w_len.p, n * 4ull, hipMemcpyDeviceToDevice, s_));
+        BPE_HIP(hipMemcpyAsync(wcnt_.p, w_cnt.p, n * 8ull, hipMemcpyDeviceToDevice, s_));
+        hipLaunchKernelGGL(k_fill_words<TokT>, dim3(ceil_div(n, 256)), dim3(256), 0, s_, text_,
+                           w_off.p, w_len.p, w_cnt.p, cbeg.p, n, CH, tok_.p, wbeg_.p, act_.p, hist_.p);
+        BPE_HIP(hipGetLastError());
+    }
+    out_.stats.n_words = n;
+    out_.stats.n_word_tokens = 0;
+    BPE_HIP(hipStreamSynchronize(s_));
+}
+
+template <class TokT>
+void MergeLoop<TokT>::alloc_pairs(size_t cap) {
+    pcap_ = cap;
+    pkey_.alloc(cap);
+    pcnt_.alloc(cap);
+    pflag_.alloc(cap);
+    C_.alloc(cap);
+    BPE_HIP(hipMemsetAsync(pkey_.p, 0, pkey_.bytes(), s_));
+    BPE_HIP(hipMemsetAsync(pcnt_.p, 0, pcnt_.bytes(), s_));
+    BPE_HIP(hipMemsetAsync(pflag_.p, 0, pflag_.bytes(), s_));
+    hs_.capC = (unsigned)cap;
+}
+
+template <class TokT>
+void MergeLoop<TokT>::grow_pairs() {
+    DevBuf<unsigned long long> okey = std::move(pkey_);
+    DevBuf<long long> ocnt = std::move(pcnt_);
+    DevBuf<unsigned> oflag = std::move(pflag_);
+    const size_t ocap = pcap_;
+    alloc_pairs(ocap * 2);
+    hs_.pair_used = 0;
+    push_state();
+    hipLaunchKernelGGL(k_rehash, dim3(ceil_div(ocap, 256)), dim3(256), 0, s_, okey.p, ocnt.p,
+                       oflag.p, ocap, pairs(), st_.p);
+    BPE_HIP(hipGetLastError());
+    pull_state();
+}
+
+template <class TokT>
+void MergeLoop<TokT>::ensure_pool(unsigned need) {
+    if (hs_.pool_used + (unsigned long long)need <= hs_.pool_cap) return;
+    unsigned long long cap = hs_.pool_cap;
+    while (hs_.pool_used + (unsigned long long)need > cap) cap *= 2;
+    BPE_REQUIRE(cap < (1ULL << 32), BPE_E_LIMIT, "token byte pool exceeds 4 GiB");
+    DevBuf<uint8_t> np(cap);
+    BPE_HIP(hipMemcpyAsync(np.p, pool_.p, hs_.pool_used, hipMemcpyDeviceToDevice, s_));
+    pool_ = std::move(np);
+    hs_.pool_cap = (unsigned)cap;
+    push_state();
+}
+
+template <class TokT>
+int MergeLoop<TokT>::rebuild() {
+    out_.stats.n_rebuilds++;
+    const int grid = 1024;
+    BPE_HIP(hipMemsetAsync(rs_.p, 0, sizeof(RebuildStats), s_));
+    hipLaunchKernelGGL(k_rebuild_hist, dim3(grid), dim3(256), 0, s_, pairs(), pcap_, rs_.p);
+    BPE_HIP(hipGetLastError());
+    RebuildStats h;
+    BPE_HIP(hipMemcpyAsync(&h, rs_.p, sizeof(h), hipMemcpyDeviceToHost, s_));
+    BPE_HIP(hipStreamSynchronize(s_));
+    int top = -1;
+    for (int k = 63; k >= 0; --k)
+        if (h.bins[k]) { top = k; break; }
+    if (top < 0) return h.ghosts ? 1 : 2;
+    // the bin where the cumulative count from the top crosses the target
+    unsigned long long cum = 0;
+    int k = top;
+    for (; k >= 0; --k) {
+        if (cum + h.bins[k] > kTarget) break;
+        cum += h.bins[k];
+    }
+    long long T;
+    if (k < 0) {
+        T = 1;
+    } else {
+        const long long lo = 1LL << k;
+        const long long width = std::max(1LL, lo / 1024);
+        hipLaunchKernelGGL(k_rebuild_sub, dim3(grid), dim3(256), 0, s_, pairs(), pcap_, lo, width, rs_.p);
+        BPE_HIP(hipGetLastError());
+        BPE_HIP(hipMemcpyAsync(h.sub, rs_.p->sub, sizeof(h.sub), hipMemcpyDeviceToHost, s_));
+        BPE_HIP(hipStreamSynchronize(s_));
+        T = lo << 1;  // everything above bin k
+        for (int j = 1023; j >= 0; --j) {
+            if (!h.sub[j]) continue;
+            if (cum + h.sub[j] > kTarget && cum > 0) break;
+            cum += h.sub[j];
+            T = lo + (long long)j * width;
+            if (cum > kTarget) break;
+        }
+    }
+    hs_.T = T;
+    hs_.nC = 0;
+    hs_.halt = HALT_NONE;
+    push_state();
+    hipLaunchKernelGGL(k_build_C, dim3(grid), dim3(256), 0, s_, pairs(), pcap_, T, st_.p);
+    hipLaunchKernelGGL(k_argmax, dim3(kArgBlocks), dim3(256), 0, s_, st_.p, pairs(), trank_.p,
+                       part_.p, 0);
+    BPE_HIP(hipGetLastError());
+    pull_state();
+    BPE_REQUIRE(!(hs_.err & ERR_C_FULL), BPE_E_NOMEM, "candidate list overflow");
+    return 0;
+}
+
+template <class TokT>
+void MergeLoop<TokT>::compact() {
+    const unsigned n = hs_.n_act;
+    if (!n) return;
+    DevBuf<uint8_t> keep(n);
+    DevBuf<unsigned> nsel(1);
+    hipLaunchKernelGGL(k_flag_active, dim3(ceil_div(n, 256)), dim3(256), 0, s_, act_.p, n, wlen_.p, keep.p);
+    size_t tb = 0;
+    BPE_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, act_.p, keep.p, act2_.p, nsel.p, (int)n, s_));
+    DevBuf<uint8_t> tmp(tb);
+    BPE_HIP(hipcub::DeviceSelect::Flagged(tmp.p, tb, act_.p, keep.p, act2_.p, nsel.p, (int)n, s_));
+    unsigned m = 0;
+    BPE_HIP(hipMemcpyAsync(&m, nsel.p, 4, hipMemcpyDeviceToHost, s_));
+    BPE_HIP(hipStreamSynchronize(s_));
+    std::swap(act_, act2_);
+    hs_.n_act = m;
+    hs_.n_single = 0;
+    push_state();
+}
+
+template <class TokT>
+void MergeLoop<TokT>::run() {
+    const unsigned n = n_words_;
+    st_.alloc(1);
+    rs_.alloc(1);
+    part_.alloc(kArgBlocks);
+    tok_cap_ = 256u + (unsigned)n_rounds_ + 1u;
+    LR_.alloc(2ull * tok_cap_);
+    BPE_HIP(hipMemsetAsync(LR_.p, 0, LR_.bytes(), s_));
+    m_a_.alloc(n_rounds_); m_b_.alloc(n_rounds_); m_new_.alloc(n_rounds_);
+    toff_.alloc(tok_cap_); tlen_.alloc(tok_cap_); trank_.alloc(tok_cap_);
+    thash_.alloc(tok_cap_); tpw_.alloc(tok_cap_); tkey8_.alloc(tok_cap_);
+    tmap_.alloc(next_pow2(4ull * tok_cap_));
+    BPE_HIP(hipMemsetAsync(tmap_.p, 0, tmap_.bytes(), s_));
+    const unsigned pool_cap = std::max(1u << 16, 64u * std::max(max_len_, 8u));
+    pool_.alloc(pool_cap);
+    act2_.alloc(std::max(n, 1u));
+
+    // global initial pair histogram (train.py:35-49): one all-reduce when sharded
+    if (comm_ && comm_->nranks > 1)
+        comm_->allreduce_i64(reinterpret_cast<int64_t*>(hist_.p), 65536, s_);
+    alloc_pairs(size_t(1) << 22);
+    memset(&hs_, 0, sizeof(hs_));
+    hs_.n_rounds = n_rounds_;
+    hs_.ntok = 256;
+    hs_.capC = (unsigned)pcap_;
+    hs_.n_act = n;
+    hs_.pool_used = 256;
+    hs_.pool_cap = pool_cap;
+    hs_.halt = HALT_REBUILD;
+    push_state();
+    hipLaunchKernelGGL(k_init_tokens, dim3(1), dim3(256), 0, s_, toks());
+    hipLaunchKernelGGL(k_init_pairs, dim3(256), dim3(256), 0, s_, hist_.p, pairs(), st_.p);
+    BPE_HIP(hipGetLastError());
+    pull_state();
+    hs_.halt = HALT_REBUILD;
+
+    const bool timing = timing_enabled();
+    std::vector<hipEvent_t> ev;
+    if (timing) {
+        ev.resize(2 * kBatch);
+        for (auto& e : ev) BPE_HIP(hipEventCreate(&e));
+    }
+    double k1_ms = 0;
+    long long k1_launches = 0;
+    const bool sharded = comm_ && comm_->nranks > 1;
+    const int merge_blocks = (int)std::min<unsigned>(kMergeBlocks, std::max(1u, ceil_div(n, 256)));
+
+    for (;;) {
+        if (hs_.round >= n_rounds_) break;
+        if (hs_.halt == HALT_REBUILD) {
+            const int r = rebuild();
+            if (r == 1) { exhaustion(); break; }
+            if (r == 2) break;   // no keys left: `if len(byte_pair_frequencies) == 0: break`
+        }
+        // capacity headroom for one batch (worst case: 2 new keys per token per round)
+        int R = std::min(kBatch, n_rounds_ - hs_.round);
+        const unsigned long long per_round = 2ull * (hs_.ntok + R + 1);
+        while (hs_.pair_used + per_round * R > pcap_ * 3 / 4) {
+            if (R > 8) { R /= 2; continue; }
+            grow_pairs();
+            hs_.halt = HALT_REBUILD;   // C holds slot indices: rebuild it
+            break;
+        }
+        if (hs_.halt == HALT_REBUILD) continue;
+        ensure_pool((unsigned)R * std::max(max_len_, 1u));
+        const long long start_round = hs_.round;
+        for (int k = 0; k < R; ++k) {
+            if (timing) BPE_HIP(hipEventRecord(ev[2 * k], s_));
+            hipLaunchKernelGGL(k_merge<TokT>, dim3(merge_blocks), dim3(256), 0, s_, st_.p, part_.p,
+                               kArgBlocks, pairs(), toks(), words(), LR_.p, m_a_.p, m_b_.p, m_new_.p);
+            if (timing) BPE_HIP(hipEventRecord(ev[2 * k + 1], s_));
+            if (sharded) {
+                const size_t ntok_bound = 256 + (size_t)start_round + k + 1;
+                comm_->allreduce_i64(reinterpret_cast<int64_t*>(LR_.p), 2 * ntok_bound, s_);
+            }
+            const unsigned ntb = 256u + (unsigned)start_round + (unsigned)k + 1u;
+            hipLaunchKernelGGL(k_apply, dim3(ceil_div(ntb, 256)), dim3(256), 0, s_, st_.p, pairs(),
+                               toks(), LR_.p);
+            hipLaunchKernelGGL(k_argmax, dim3(kArgBlocks), dim3(256), 0, s_, st_.p, pairs(),
+                               trank_.p, part_.p, 1);
+        }
+        BPE_HIP(hipGetLastError());
+        pull_state();
+        if (timing) {
+            const int done = (int)(hs_.round - start_round) + (hs_.halt ? 1 : 0);
+            for (int k = 0; k < std::min(done, R); ++k) {
+                float t = 0;
+                BPE_HIP(hipEventElapsedTime(&t, ev[2 * k], ev[2 * k + 1]));
+                k1_ms += t;
+                ++k1_launches;
+            }
+        }
+        BPE_REQUIRE(!(hs_.err & ERR_PAIRS_FULL), BPE_E_NOMEM, "pair table overflow");
+        BPE_REQUIRE(!(hs_.err & ERR_C_FULL), BPE_E_NOMEM, "candidate list overflow");
+        BPE_REQUIRE(!(hs_.err & ERR_POOL), BPE_E_NOMEM, "token pool overflow");
+        if (hs_.halt == HALT_DONE) break;
+        if (hs_.n_single > hs_.n_act / 4 + 1024) compact();
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    out_.stats.merge_kernel_ms = k1_ms;
+    out_.stats.merge_kernel_launches = k1_launches;
+    out_.stats.merge_kernel_bytes = (double)hs_.scan_slots * sizeof(TokT);
+    out_.stats.n_pairs_final = (int64_t)hs_.pair_used;
+    out_.stats.n_rounds_device = hs_.round;
+
+    // pull the device decisions and replay them on the host (token bytes, dedupe check)
+    const int rd = hs_.round;
+    std::vector<uint32_t> ma(rd), mb(rd), mn(rd);
+    if (rd) {
+        BPE_HIP(hipMemcpyAsync(ma.data(), m_a_.p, rd * 4ull, hipMemcpyDeviceToHost, s_));
+        BPE_HIP(hipMemcpyAsync(mb.data(), m_b_.p, rd * 4ull, hipMemcpyDeviceToHost, s_));
+        BPE_HIP(hipMemcpyAsync(mn.data(), m_new_.p, rd * 4ull, hipMemcpyDeviceToHost, s_));
+        BPE_HIP(hipStreamSynchronize(s_));
+    }
+    // (out_.tok_bytes / merges may already hold the exhaustion tail: prepend device rounds)
+    std::vector<std::pair<std::string, std::string>> tail = std::move(out_.merges);
+    out_.merges.clear();
+    if (out_.tok_bytes.empty()) {
+        for (int b = 0; b < 256; ++b) out_.tok_bytes.push_back(std::string(1, (char)b));
+        std::unordered_map<std::string, uint32_t> index;
+        for (int r = 0; r < rd; ++r) {
+            std::string nb = out_.tok_bytes[ma[r]] + out_.tok_bytes[mb[r]];
+            if (mn[r] == out_.tok_bytes.size()) out_.tok_bytes.push_back(nb);
+            else BPE_REQUIRE(mn[r] < out_.tok_bytes.size() && out_.tok_bytes[mn[r]] == nb,
+                             BPE_E_HIP, "device token dedupe disagrees with host replay");
+            out_.merges.emplace_back(out_.tok_bytes[ma[r]], out_.tok_bytes[mb[r]]);
+        }
+    } else {
+        for (int r = 0; r < rd; ++r) out_.merges.emplace_back(out_.tok_bytes[ma[r]], out_.tok_bytes[mb[r]]);
+    }
+    for (auto& m : tail) out_.merges.push_back(std::move(m));
+}
+
+// Every word is one token: the reference keeps popping the remaining zero-count keys,
+// greatest (bytes a, bytes b) first, until the rounds run out or the dict is empty.
+template <class TokT>
+void MergeLoop<TokT>::exhaustion() {
+    const int rd = hs_.round;
+    std::vector<uint32_t> ma(rd), mb(rd), mn(rd);
+    if (rd) {
+        BPE_HIP(hipMemcpyAsync(ma.data(), m_a_.p, rd * 4ull, hipMemcpyDeviceToHost, s_));
+        BPE_HIP(hipMemcpyAsync(mb.data(), m_b_.p, rd * 4ull, hipMemcpyDeviceToHost, s_));
+        BPE_HIP(hipMemcpyAsync(mn.data(), m_new_.p, rd * 4ull, hipMemcpyDeviceToHost, s_));
+    }
+    DevBuf<unsigned long long> keys(std::max<size_t>(hs_.pair_used, 1));
+    DevBuf<unsigned> nk(1);
+    BPE_HIP(hipMemsetAsync(nk.p, 0, 4, s_));
+    hipLaunchKernelGGL(k_collect_present, dim3(1024), dim3(256), 0, s_, pairs(), pcap_, keys.p, nk.p);
+    unsigned hk = 0;
+    BPE_HIP(hipMemcpyAsync(&hk, nk.p, 4, hipMemcpyDeviceToHost, s_));
+    BPE_HIP(hipStreamSynchronize(s_));
+    std::vector<unsigned long long> hkeys(hk);
+    if (hk) {
+        BPE_HIP(hipMemcpyAsync(hkeys.data(), keys.p, hk * 8ull, hipMemcpyDeviceToHost, s_));
+        BPE_HIP(hipStreamSynchronize(s_));
+    }
+    auto& tb = out_.tok_bytes;
+    tb.clear();
+    for (int b = 0; b < 256; ++b) tb.push_back(std::string(1, (char)b));
+    for (int r = 0; r < rd; ++r) {
+        std::string nb = tb[ma[r]] + tb[mb[r]];
+        if (mn[r] == tb.size()) tb.push_back(nb);
+        else BPE_REQUIRE(mn[r] < tb.size() && tb[mn[r]] == nb, BPE_E_HIP,
+                         "device token dedupe disagrees with host replay");
+    }
+    std::vector<std::pair<std::string, std::string>> ghosts;
+    ghosts.reserve(hk);
+    for (auto k : hkeys) ghosts.emplace_back(tb[k >> 32], tb[k & 0xffffffffu]);
+    std::sort(ghosts.begin(), ghosts.end(), [](const auto& x, const auto& y) { return x > y; });
+    const size_t left = (size_t)(n_rounds_ - rd);
+    if (ghosts.size() > left) ghosts.resize(left);
+    out_.stats.n_rounds_host = (int64_t)ghosts.size();
+    out_.merges = std::move(ghosts);   // the tail; run() prepends the device rounds
+}
+
+}  // namespace
+
+void train_on_device(const uint8_t* d_raw, size_t n, int vocab_size,
+                     const std::vector<std::string>& specials, Comm* comm, hipStream_t stream,
+                     TrainOutput& out) {
+    const auto t0 = std::chrono::steady_clock::now();
+    out = TrainOutput{};
+    DevBuf<uint8_t> scratch;
+    size_t tn = 0;
+    const uint8_t* text = prepare_text(d_raw, n, scratch, &tn, stream);
+    out.stats.t_prepare_ms = ms_since(t0);
+    out.stats.n_bytes = (int64_t)tn;
+
+    // len(vocab) at loop start: Vocab(special_tokens) = specials then the 256 bytes, deduped
+    std::set<std::string> base;
+    for (const auto& s : specials) base.insert(s);
+    for (int b = 0; b < 256; ++b) base.insert(std::string(1, (char)b));
+    const long long rounds = (long long)vocab_size - (long long)base.size();
+
+    auto t1 = std::chrono::steady_clock::now();
+    WordCounts wc;
+    float count_ms = 0;
+    count_words(text, tn, wc, stream, timing_enabled() ? &count_ms : nullptr);
+    out.stats.t_count_ms = ms_since(t1);
+    out.stats.count_kernel_ms = count_ms;
+    out.stats.count_kernel_bytes = (double)tn;
+    out.stats.n_pretokens = (int64_t)wc.n_pretokens;
+    if (rounds <= 0) {
+        out.stats.t_total_ms = ms_since(t0);
+        return;
+    }
+    BPE_REQUIRE(rounds < (1LL << 31) - 512, BPE_E_LIMIT, "vocab_size too large");
+    auto go = [&](auto tag) {
+        using TokT = decltype(tag);
+        auto t2 = std::chrono::steady_clock::now();
+        MergeLoop<TokT> loop(stream, comm, text, (int)rounds, out);
+        loop.build_words(wc, specials);
+        { WordCounts drop = std::move(wc); }
+        out.stats.t_words_ms = ms_since(t2);
+        auto t3 = std::chrono::steady_clock::now();
+        loop.run();
+        out.stats.t_merge_ms = ms_since(t3);
+    };
+    if (256 + rounds + 1 < 65535) go(uint16_t{});
+    else go(uint32_t{});
+    out.stats.t_total_ms = ms_since(t0);
+}
+
+}  // namespace bpe
