@@ -139,8 +139,11 @@ void bpe_tok_free(bpe_tokenizer* tok);
 /* Largest p <= pos such that splitting the text at p does not change its pre-tokenization
  * (a U+0020 between two ASCII non-space bytes), or 0. Used to shard a corpus into slabs. */
 size_t bpe_safe_split(const uint8_t* data, size_t n, size_t pos);
-/* Deterministic synthetic corpus (bench/tests): n bytes of UTF-8 text into device memory. */
-int bpe_synth_corpus_device(uint8_t* d_out, size_t n, uint64_t seed, int flavour, void* hip_stream);
+/* Deterministic synthetic corpus (bench/tests): bytes [first_block*4096, first_block*4096 + n)
+ * of corpus (seed, flavour) into device memory; flavour 0 = OWT-like, 1 = TinyStories-like.
+ * Every 4096-byte block boundary is a safe split point, so slabs of whole blocks shard it. */
+int bpe_synth_corpus_device(uint8_t* d_out, size_t n, uint64_t seed, int flavour,
+                            uint64_t first_block, void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -79,7 +79,8 @@ _SIGS = [
     ("bpe_tok_encode_device", ctypes.c_int, [_P, _P, _SZ, _P, ctypes.POINTER(_SZ), _P]),
     ("bpe_tok_free", None, [_P]),
     ("bpe_safe_split", _SZ, [_U8P, _SZ, _SZ]),
-    ("bpe_synth_corpus_device", ctypes.c_int, [_P, _SZ, ctypes.c_uint64, ctypes.c_int, _P]),
+    ("bpe_synth_corpus_device", ctypes.c_int, [_P, _SZ, ctypes.c_uint64, ctypes.c_int,
+                                               ctypes.c_uint64, _P]),
 ]
 SYMBOLS = [s[0] for s in _SIGS]
 

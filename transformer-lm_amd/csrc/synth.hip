@@ -67,9 +67,11 @@ __device__ void emit_word(Out& o, unsigned long long lex_seed, unsigned rank, in
     }
 }
 
-__global__ void k_synth(uint8_t* __restrict__ out, size_t n, unsigned long long seed, int flavour) {
-    const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t lo = b * kBlock;
+__global__ void k_synth(uint8_t* __restrict__ out, size_t n, unsigned long long seed, int flavour,
+                        unsigned long long first_block) {
+    const size_t lb = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t lo = lb * kBlock;
+    const size_t b = lb + first_block;
     if (lo >= n) return;
     const size_t len = (n - lo < kBlock) ? n - lo : kBlock;
     Rng r{mix64(seed * 0x9E3779B97F4A7C15ULL + b + 1)};
@@ -77,8 +79,11 @@ __global__ void k_synth(uint8_t* __restrict__ out, size_t n, unsigned long long 
     const int lex_bits = flavour == 1 ? 14 : 21;
     const unsigned eot_per = flavour == 1 ? 160 : 800;
     Out o{out + lo, len};
-    bool sentence_start = true;
-    while (o.left > 24) {
+    bool sentence_start = false;
+    // every block starts " The" and ends with a letter run, so every block boundary is a
+    // safe split point: a rank's slab [r*B, (r+1)*B) blocks is exactly its share of the corpus
+    if (len >= 8) o.str(" The");
+    while (o.left > 32) {  // no piece is longer than 30 bytes: nothing is ever truncated
         const unsigned k = r.below(1000);
         if (r.below(eot_per) == 0) {
             o.str(".<|endoftext|>");
@@ -124,24 +129,22 @@ __global__ void k_synth(uint8_t* __restrict__ out, size_t n, unsigned long long 
             emit_word(o, lex_seed, r.below(64), 0, false);
         }
     }
-    // pad the block to its exact size with a letter run (a single pre-token)
-    if (o.left) {
-        o.put(o.left == len ? 'x' : ' ');
-        while (o.left) o.put('z');
-    }
+    // pad the block to its exact size with " zzz..." (one pre-token), ending on a letter
+    if (o.left >= 2) o.put(' ');
+    while (o.left) o.put('z');
 }
 
 }  // namespace
 }  // namespace bpe
 
 extern "C" int bpe_synth_corpus_device(uint8_t* d_out, size_t n, uint64_t seed, int flavour,
-                                       void* hip_stream) {
+                                       uint64_t first_block, void* hip_stream) {
     if (!d_out && n) return BPE_E_ARG;
     if (n == 0) return BPE_OK;
     hipStream_t s = (hipStream_t)hip_stream;
     const size_t blocks = (n + bpe::kBlock - 1) / bpe::kBlock;
     hipLaunchKernelGGL(bpe::k_synth, dim3(bpe::ceil_div(blocks, 128)), dim3(128), 0, s, d_out, n,
-                       (unsigned long long)seed, flavour);
+                       (unsigned long long)seed, flavour, (unsigned long long)first_block);
     if (hipGetLastError() != hipSuccess) return BPE_E_HIP;
     if (hipStreamSynchronize(s) != hipSuccess) return BPE_E_HIP;
     return BPE_OK;
