@@ -71,6 +71,37 @@ __host__ __device__ inline uint64_t mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
+// One atomic per wave for a predicate-driven append (same-address atomics serialize on the
+// memory side, so per-lane appends to one counter are never used).  Every lane of the wave
+// must call it; returns this lane's index, or ~0u when pred is false.
+__device__ __forceinline__ unsigned wave_append(bool pred, unsigned* counter) {
+    const unsigned long long m = __ballot(pred);
+    if (!m) return ~0u;
+    const int leader = __ffsll((long long)m) - 1;
+    const unsigned lane = threadIdx.x & 63;
+    unsigned base = 0;
+    if ((int)lane == leader) base = atomicAdd(counter, (unsigned)__popcll(m));
+    base = __shfl(base, leader);
+    const unsigned below = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    return pred ? base + below : ~0u;
+}
+
+template <class T>
+__device__ __forceinline__ T wave_sum(T v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+template <class T>
+__device__ __forceinline__ T wave_max(T v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const T w = __shfl_xor(v, o);
+        v = w > v ? w : v;
+    }
+    return v;
+}
+
 inline unsigned ceil_div(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 inline size_t next_pow2(size_t x) {
     size_t p = 1;

@@ -64,18 +64,21 @@ __device__ __forceinline__ bool bytes_eq(const uint8_t* x, const uint8_t* y, siz
 __global__ void k_find_specials(const uint8_t* __restrict__ s, size_t n, EncTables E,
                                 const unsigned* __restrict__ first_mask,
                                 unsigned long long* __restrict__ pos_out, int* __restrict__ sp_out,
-                                unsigned long long* __restrict__ n_out, unsigned long long cap) {
+                                unsigned* __restrict__ n_out, unsigned long long cap) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const unsigned b = s[i];
-    if (!((first_mask[b >> 5] >> (b & 31)) & 1u)) return;
-    for (int k = 0; k < E.n_sp; ++k) {  // specials are sorted longest first: first hit wins
-        const unsigned l = E.sp_len[k];
-        if (i + l <= n && bytes_eq(s + i, E.sp_bytes + E.sp_off[k], l)) {
-            const unsigned long long idx = atomicAdd(n_out, 1ULL);
-            if (idx < cap) { pos_out[idx] = i; sp_out[idx] = k; }
-            return;
+    int hit = -1;
+    if (i < n) {
+        const unsigned b = s[i];
+        if ((first_mask[b >> 5] >> (b & 31)) & 1u) {
+            for (int k = 0; k < E.n_sp; ++k) {  // specials are sorted longest first: first hit wins
+                const unsigned l = E.sp_len[k];
+                if (i + l <= n && bytes_eq(s + i, E.sp_bytes + E.sp_off[k], l)) { hit = k; break; }
+            }
         }
+    }
+    const unsigned idx = wave_append(hit >= 0, n_out);
+    if (hit >= 0) {
+        if (idx < cap) { pos_out[idx] = i; sp_out[idx] = hit; }
     }
 }
 
@@ -183,10 +186,9 @@ __global__ void k_collect(const unsigned long long* __restrict__ key, size_t cap
                           uint32_t* __restrict__ slot_word, unsigned long long* __restrict__ w_off,
                           uint32_t* __restrict__ w_len, unsigned* __restrict__ n_words) {
     const size_t sidx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (sidx >= cap) return;
-    const unsigned long long k = key[sidx];
+    const unsigned long long k = sidx < cap ? key[sidx] : 0ULL;
+    const unsigned w = wave_append(k != 0, n_words);
     if (!k) return;
-    const unsigned w = atomicAdd(n_words, 1u);
     slot_word[sidx] = w;
     w_off[w] = (k & kOff40) - 1;
     w_len[w] = (uint32_t)(k >> 40);
@@ -397,13 +399,17 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
         if (!T.specials.empty()) {
             unsigned long long cap = std::max<unsigned long long>(1024, n / 64);
             for (;;) {
-                DevBuf<unsigned long long> d_pos(cap), d_n(1);
+                DevBuf<unsigned long long> d_pos(cap);
+                DevBuf<unsigned> d_n(1);
                 DevBuf<int> d_sp(cap);
-                BPE_HIP(hipMemsetAsync(d_n.p, 0, 8, s));
+                BPE_HIP(hipMemsetAsync(d_n.p, 0, 4, s));
                 hipLaunchKernelGGL(k_find_specials, dim3(ceil_div(n, 256)), dim3(256), 0, s, d_text, n, E,
                                    T.first_mask.p, d_pos.p, d_sp.p, d_n.p, cap);
                 BPE_HIP(hipGetLastError());
-                BPE_HIP(hipMemcpyAsync(&cnt, d_n.p, 8, hipMemcpyDeviceToHost, s));
+                unsigned cnt32 = 0;
+                BPE_HIP(hipMemcpyAsync(&cnt32, d_n.p, 4, hipMemcpyDeviceToHost, s));
+                BPE_HIP(hipStreamSynchronize(s));
+                cnt = cnt32;
                 BPE_HIP(hipStreamSynchronize(s));
                 if (cnt > cap) { cap = cnt; continue; }
                 pos.resize(cnt);

@@ -145,6 +145,37 @@ __device__ __forceinline__ bool bytes_equal(const uint8_t* __restrict__ x,
     return true;
 }
 
+// insert `c` occurrences of the word s[p, p+len) into the global table (exact: a slot's key
+// is the (length, offset) of the first occurrence that claimed it; matches compare bytes)
+__device__ __forceinline__ void global_add(const uint8_t* __restrict__ s, size_t p, size_t len,
+                                           uint64_t h, unsigned long long c,
+                                           unsigned long long* __restrict__ key,
+                                           unsigned long long* __restrict__ cnt, size_t mask,
+                                           unsigned* __restrict__ status) {
+    const unsigned long long mine = ((unsigned long long)len << 40) | (p + 1);
+    size_t slot = h & mask;
+    for (int probe = 0; probe < kMaxProbe; ++probe) {
+        unsigned long long k = key[slot];
+        if (k == 0) {
+            k = atomicCAS(&key[slot], 0ULL, mine);
+            if (k == 0) { atomicAdd(&cnt[slot], c); return; }
+        }
+        if ((k >> 40) == len && bytes_equal(s + ((k & kOffMask) - 1), s + p, len)) {
+            atomicAdd(&cnt[slot], c);
+            return;
+        }
+        slot = (slot + 1) & mask;
+    }
+    atomicOr(status, 1u);
+}
+
+// Per-workgroup LDS word cache in front of the global table: frequent words (" the", ",")
+// are counted in LDS and reach the global table once per workgroup instead of once per
+// occurrence -- global atomics on one hot address serialize.  Entries hold the same
+// (length, offset) key, so the cache is exact too; a word whose LDS slot is taken by another
+// word goes straight to the global table.
+constexpr int kLdsWords = 2048;
+
 // Each thread owns a nominal span [t*span, (t+1)*span): it starts at the first safe point
 // at or after the span start and stops at the first safe point at or after the span end,
 // so the spans tile the text exactly along token boundaries.
@@ -154,11 +185,15 @@ __global__ void __launch_bounds__(256) k_count_words(const uint8_t* __restrict__
                                                      unsigned long long* __restrict__ cnt,
                                                      size_t mask, unsigned* __restrict__ status,
                                                      unsigned long long* __restrict__ n_tok) {
+    __shared__ unsigned long long l_key[kLdsWords];
+    __shared__ unsigned l_cnt[kLdsWords];
+    __shared__ unsigned long long s_tok[4];
+    for (int i = threadIdx.x; i < kLdsWords; i += blockDim.x) { l_key[i] = 0; l_cnt[i] = 0; }
+    __syncthreads();
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t lo = t * span;
-    if (lo >= n) return;
     const size_t hi = lo + span;
-    size_t p = (t == 0) ? 0 : next_safe_point(s, n, lo);
+    size_t p = lo >= n ? n : ((t == 0) ? 0 : next_safe_point(s, n, lo));
     unsigned long long ntok = 0;
     while (p < n) {
         if (p >= hi && is_safe_point(s, n, p)) break;
@@ -167,33 +202,41 @@ __global__ void __launch_bounds__(256) k_count_words(const uint8_t* __restrict__
         if (len >= 2) {
             ++ntok;
             if (len >= (1ULL << 24)) { atomicOr(status, 2u); p = e; continue; }
+            const uint64_t h = hash_word(s + p, len);
+            const unsigned ls = (unsigned)(h >> 40) & (kLdsWords - 1);
             const unsigned long long mine = ((unsigned long long)len << 40) | (p + 1);
-            size_t slot = hash_word(s + p, len) & mask;
-            int probe = 0;
-            for (; probe < kMaxProbe; ++probe) {
-                unsigned long long k = key[slot];
-                if (k == 0) {
-                    k = atomicCAS(&key[slot], 0ULL, mine);
-                    if (k == 0) { atomicAdd(&cnt[slot], 1ULL); break; }
-                }
-                if ((k >> 40) == len && bytes_equal(s + ((k & kOffMask) - 1), s + p, len)) {
-                    atomicAdd(&cnt[slot], 1ULL);
-                    break;
-                }
-                slot = (slot + 1) & mask;
+            unsigned long long k = l_key[ls];
+            if (k == 0) k = atomicCAS(&l_key[ls], 0ULL, mine);
+            if (k == 0 ||
+                ((k >> 40) == len && bytes_equal(s + ((k & kOffMask) - 1), s + p, len))) {
+                atomicAdd(&l_cnt[ls], 1u);
+            } else {
+                global_add(s, p, len, h, 1, key, cnt, mask, status);
             }
-            if (probe == kMaxProbe) atomicOr(status, 1u);
         }
         p = e;
     }
-    if (ntok) atomicAdd(n_tok, ntok);
+    ntok = wave_sum(ntok);
+    if ((threadIdx.x & 63) == 0) s_tok[threadIdx.x >> 6] = ntok;
+    __syncthreads();
+    // flush the cache: one global add per distinct cached word
+    for (int i = threadIdx.x; i < kLdsWords; i += blockDim.x) {
+        const unsigned long long k = l_key[i];
+        if (!k) continue;
+        const size_t len = (size_t)(k >> 40), p0 = (size_t)(k & kOffMask) - 1;
+        global_add(s, p0, len, hash_word(s + p0, len), l_cnt[i], key, cnt, mask, status);
+    }
+    if (threadIdx.x == 0) {  // per-block sum, one atomic per block
+        const unsigned long long b = s_tok[0] + s_tok[1] + s_tok[2] + s_tok[3];
+        if (b) atomicAdd(n_tok, b);
+    }
 }
 
 void count_words(const uint8_t* d_text, size_t n, WordCounts& wc, hipStream_t stream,
                  float* kernel_ms) {
     BPE_REQUIRE(n < (1ULL << 40) - 1, BPE_E_LIMIT, "corpus slab larger than 1 TiB");
     size_t cap = next_pow2(std::max<size_t>(1 << 16, n / 96));
-    constexpr size_t kSpan = 256;
+    constexpr size_t kSpan = 512;
     DevBuf<unsigned> status(1);
     DevBuf<unsigned long long> ntok(1);
     hipEvent_t e0 = nullptr, e1 = nullptr;

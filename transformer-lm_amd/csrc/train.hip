@@ -11,30 +11,36 @@
 // Tokens are identified by their bytes (vocab.py:29): a merge whose bytes already exist
 // reuses that token's id (token dedupe below).
 //
-// Device design (one HIP stream, three kernels per round, batched host checks):
+// HBM layout of the unique-word table (the stream every round reads):
+//   words live in fixed-width SLOTS of W token ids, W in {8, 16, 32, 64}: slot[0] = current
+//   length, slot[1..] = ids, the unused tail filled with a sentinel id that never matches a
+//   pair.  A 16-byte slot (u16 ids) is one dwordx4 load per word, coalesced across the wave,
+//   and the pair test is W-2 register compares with no branch on the length.  Words longer
+//   than 63 ids sit in a CSR side table.  Counts (u64) are a parallel array read only on a hit.
+//   Words that shrink to one id drop out, and words migrate to narrower slots, at compaction.
+//
+// Per round, three kernels on one HIP stream (host checks state once per batch of rounds):
 //   K1 k_merge  : every workgroup reduces K3's per-block partials to the round's best pair,
-//                 resolves the new token id (hash map over token bytes), counts its rank
-//                 among all tokens (for the lexicographic tie-break); block 0 records the
-//                 merge and the new token.  Then all workgroups rewrite the active words
-//                 that contain (a, b) in place and accumulate, per neighbour token, the
-//                 left/right deltas L[x], R[y] (int64).
-//   [allreduce of L/R over ranks when sharded]
-//   K2 k_apply  : for every token x with L[x] / R[y] != 0 apply the four pair updates to the
-//                 pair hash table, mark touched keys present, add keys that cross the
-//                 candidate threshold T to the candidate list C; update lexicographic ranks.
+//                 resolves the new token id (hash map over token bytes) and counts its
+//                 lexicographic rank over a slice of the tokens; block 0 records the merge.
+//                 Then all workgroups rewrite the words containing (a, b) and accumulate, per
+//                 neighbour token, the deltas L[x] (left) and R[y] (right) as int64.
+//   [one all-reduce of L/R over ranks when the corpus is sharded]
+//   K2 k_apply  : 4 threads per token: (x,a)-=L[x], (x,new)+=L[x], (b,y)-=R[y], (new,y)+=R[y]
+//                 on the pair hash table; touched keys become present; increments that lift a
+//                 key across the threshold T append it to the candidate list C.
 //   K3 k_argmax : argmax over C of (count, rank(a), rank(b)) -> per-block partials.
-// Every key with count >= T is in C (they only rise by crossing T inside K2), so the max of
-// C is the global max whenever it is >= T; otherwise the host rebuilds C with a lower T.
-// Zero-count keys that are still "present" (touched and never popped) are exactly the
-// reference's leftover dict keys; once no positive count remains (every word is a single
-// token) the reference pops them in descending byte order, which the host reproduces.
+// Every key with count >= T is in C, so max(C) is the global max whenever it is >= T;
+// otherwise (or when C has bloated) the host rebuilds C with a fresh T.  Zero-count keys that
+// are still present are the reference's leftover dict keys; once no positive count remains
+// (every word is one token) the reference pops them in descending byte order, which the host
+// reproduces.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <chrono>
 #include <climits>
 #include <cstring>
-#include <map>
 #include <set>
 #include <unordered_map>
 
@@ -48,6 +54,8 @@ constexpr unsigned kPresent = 1u, kInC = 2u;
 enum : int { HALT_NONE = 0, HALT_REBUILD = 1, HALT_DONE = 2 };
 enum : unsigned { ERR_PAIRS_FULL = 1u, ERR_C_FULL = 2u, ERR_POOL = 4u };
 constexpr unsigned long long kPolyP = 0x100000001B3ULL * 0x9E3779B97F4A7C15ULL | 1ULL;
+constexpr int kNumCls = 4;
+constexpr int kHistReplicas = 16;
 
 struct RoundState {
     int halt;
@@ -55,13 +63,12 @@ struct RoundState {
     int n_rounds;
     int ntok;
     long long T;
-    unsigned nC, capC;
+    unsigned nC, capC, c_limit, pad0;
     unsigned cur_a, cur_b, cur_new, cur_slot;
     long long cur_cnt;
     int new_is_new;
     unsigned new_rank[2];
     unsigned err;
-    unsigned n_act;
     unsigned n_single;
     unsigned pool_used, pool_cap;
     unsigned long long pair_used;
@@ -94,34 +101,42 @@ struct ToksDev {
     uint32_t map_mask;
 };
 
+__host__ __device__ constexpr int slot_w(int c) { return 8 << c; }   // 8, 16, 32, 64 ids
+__host__ __device__ inline int class_for(unsigned len) {
+    return len <= 7 ? 0 : len <= 15 ? 1 : len <= 31 ? 2 : len <= 63 ? 3 : kNumCls;
+}
+
 template <class TokT>
-struct WordsDev {
-    TokT* tok;
-    const uint32_t* wbeg;
-    uint32_t* wlen;
-    const unsigned long long* wcnt;
-    const uint32_t* act;
+struct SlotCls {
+    TokT* slot;                  // n * slot_w(c) ids
+    unsigned long long* cnt;
+    unsigned n, blk0, nblk, pad;
 };
 
-template <class TokT> struct Chunk;
-template <> struct Chunk<uint16_t> { static constexpr int N = 8; };
-template <> struct Chunk<uint32_t> { static constexpr int N = 4; };
+template <class TokT>
+struct WordsDev {
+    SlotCls<TokT> c[kNumCls];
+    TokT* ltok;                  // long words (> 63 ids): CSR
+    unsigned long long* lbeg;
+    uint32_t* llen;
+    unsigned long long* lcnt;
+    unsigned ln, lblk0, lnblk, pad;
+};
+
+template <class TokT> __host__ __device__ constexpr TokT sentinel() { return (TokT)~(TokT)0; }
 
 __device__ __forceinline__ bool cand_better(long long c1, unsigned long long t1, long long c2,
                                             unsigned long long t2) {
     return c1 > c2 || (c1 == c2 && t1 > t2);
 }
 
-template <class T>
-__device__ __forceinline__ T wave_sum(T v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
 
 // ------------------------------------------------------------------ pair table
+// returns the slot of key (inserting it if absent, *inserted = 1), or ~0 if the table is full
 __device__ __forceinline__ size_t pair_slot(const PairsDev& P, unsigned long long key,
-                                            RoundState* st) {
+                                            RoundState* st, bool* inserted) {
     size_t s = mix64(key) & P.mask;
+    *inserted = false;
     for (size_t probe = 0; probe <= P.mask; ++probe) {
         unsigned long long k = P.key[s];
         if (k == key) return s;
@@ -129,6 +144,7 @@ __device__ __forceinline__ size_t pair_slot(const PairsDev& P, unsigned long lon
             k = atomicCAS(&P.key[s], 0ULL, key);
             if (k == 0) {
                 atomicAdd(&st->pair_used, 1ULL);
+                *inserted = true;
                 return s;
             }
             if (k == key) return s;
@@ -139,22 +155,36 @@ __device__ __forceinline__ size_t pair_slot(const PairsDev& P, unsigned long lon
     return ~(size_t)0;
 }
 
-// frequencies[(p, q)] += d with the reference's defaultdict semantics (the key becomes
-// present); increments that lift a key across T enter the candidate list.
-__device__ __forceinline__ void pair_update(const PairsDev& P, RoundState* st, unsigned p,
-                                            unsigned q, long long d, long long T) {
-    const unsigned long long key = ((((unsigned long long)p) << 32) | q) + 1ULL;
-    const size_t s = pair_slot(P, key, st);
+__device__ __forceinline__ unsigned long long pair_key(unsigned p, unsigned q) {
+    return ((((unsigned long long)p) << 32) | q) + 1ULL;
+}
+
+// frequencies[(p, q)] -= d  (a missing key would be created, as defaultdict does)
+__device__ __forceinline__ void pair_dec(const PairsDev& P, RoundState* st, unsigned p, unsigned q,
+                                         long long d) {
+    bool ins;
+    const size_t s = pair_slot(P, pair_key(p, q), st, &ins);
+    if (s == ~(size_t)0) return;
+    atomicAdd((unsigned long long*)&P.cnt[s], (unsigned long long)(-d));
+    if (ins) atomicOr(&P.flag[s], kPresent);
+}
+
+// frequencies[(p, q)] += d; the key is present from now on; crossing T enters C
+__device__ __forceinline__ void pair_inc(const PairsDev& P, RoundState* st, unsigned p, unsigned q,
+                                         long long d, long long T) {
+    bool ins;
+    const size_t s = pair_slot(P, pair_key(p, q), st, &ins);
     if (s == ~(size_t)0) return;
     const long long old = (long long)atomicAdd((unsigned long long*)&P.cnt[s], (unsigned long long)d);
-    const bool cross = d > 0 && old < T && old + d >= T;
-    unsigned f = kPresent | (cross ? kInC : 0u);
-    if (!cross && (P.flag[s] & kPresent)) return;
-    const unsigned prev = atomicOr(&P.flag[s], f);
-    if (cross && !(prev & kInC)) {
-        const unsigned idx = atomicAdd(&st->nC, 1u);
-        if (idx < st->capC) P.C[idx] = (unsigned)s;
-        else atomicOr(&st->err, ERR_C_FULL);
+    if (old < T && old + d >= T) {
+        const unsigned prev = atomicOr(&P.flag[s], kPresent | kInC);
+        if (!(prev & kInC)) {
+            const unsigned idx = atomicAdd(&st->nC, 1u);
+            if (idx < st->capC) P.C[idx] = (unsigned)s;
+            else atomicOr(&st->err, ERR_C_FULL);
+        }
+    } else {
+        atomicOr(&P.flag[s], kPresent);
     }
 }
 
@@ -195,6 +225,69 @@ __device__ bool equals_concat(const ToksDev& K, unsigned x, unsigned a, unsigned
     return true;
 }
 
+// ------------------------------------------------------------------ word rewrite
+// The reference's in-place merge of one word (train.py:196-224): t[0..len) -> t[0..j).
+// Per occurrence: the left neighbour is already rewritten (t[j-1]); the right one is the
+// original t[r+2].  With `pad`, the freed tail is refilled with the sentinel.
+template <class TokT>
+__device__ uint32_t rewrite_word(TokT* __restrict__ t, uint32_t len, TokT a, TokT b, TokT nw,
+                                 unsigned long long c, unsigned long long* __restrict__ LR, bool pad) {
+    uint32_t j = 0, r = 0;
+    while (r < len) {
+        const TokT x = t[r];
+        if (x == a && r + 1 < len && t[r + 1] == b) {
+            if (j > 0) atomicAdd(&LR[2 * (size_t)t[j - 1]], c);           // (x,a)-=c, (x,new)+=c
+            if (r + 2 < len) atomicAdd(&LR[2 * (size_t)t[r + 2] + 1], c);  // (b,y)-=c, (new,y)+=c
+            t[j++] = nw;
+            r += 2;
+        } else {
+            t[j++] = x;
+            ++r;
+        }
+    }
+    if (pad)
+        for (uint32_t k = j; k < len; ++k) t[k] = sentinel<TokT>();
+    return j;
+}
+
+// scan one slot class: U words in flight per thread, one 16-byte load per 16 bytes of slot
+template <class TokT, int C>
+__device__ __forceinline__ void scan_class(const SlotCls<TokT>& S, unsigned bi, TokT a, TokT b,
+                                           TokT nw, unsigned long long* __restrict__ LR,
+                                           unsigned& singles) {
+    constexpr int W = slot_w(C);
+    constexpr int V = W * (int)sizeof(TokT) / 16;
+    constexpr int U = V == 1 ? 4 : (V == 2 ? 2 : 1);
+    const unsigned stride = S.nblk * blockDim.x;
+    for (unsigned base = bi * blockDim.x + threadIdx.x; base < S.n; base += stride * U) {
+        uint4 r[U][V];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const unsigned i = base + u * stride;
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+                r[u][v] = i < S.n ? reinterpret_cast<const uint4*>(S.slot + (size_t)i * W)[v]
+                                  : make_uint4(~0u, ~0u, ~0u, ~0u);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const unsigned i = base + u * stride;
+            TokT e[W];
+            __builtin_memcpy(e, r[u], sizeof(e));
+            bool hit = false;
+#pragma unroll
+            for (int k = 1; k + 1 < W; ++k) hit |= (e[k] == a) & (e[k + 1] == b);
+            if (hit) {
+                TokT* s = S.slot + (size_t)i * W;
+                const uint32_t len = e[0];
+                const uint32_t j = rewrite_word<TokT>(s + 1, len, a, b, nw, S.cnt[i], LR, true);
+                s[0] = (TokT)j;
+                singles += (j < 2);
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ K1: merge
 struct BestShared {
     int stop;
@@ -212,7 +305,6 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
                                                uint32_t* __restrict__ m_a, uint32_t* __restrict__ m_b,
                                                uint32_t* __restrict__ m_new) {
     __shared__ BestShared sb;
-    __shared__ unsigned long long s_red[4];
     const int tid = threadIdx.x;
     if (tid < 64) {
         // every workgroup redundantly decides the round: no extra launch, no grid sync
@@ -220,6 +312,7 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
         const int halt = st->halt, round = st->round;
         if (halt) stop = -1;
         else if (round >= st->n_rounds) stop = HALT_DONE;
+        else if (st->nC > st->c_limit) stop = HALT_REBUILD;   // C bloated: re-threshold
         long long bc = LLONG_MIN;
         unsigned long long bt = 0;
         unsigned bs = 0;
@@ -303,69 +396,47 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
         if ((tid & 63) == 0 && less) atomicAdd(&st->new_rank[sb.round & 1], less);
     }
 
-    // rewrite every active word containing (a, b)
-    constexpr int CH = Chunk<TokT>::N;
-    const unsigned n_act = st->n_act;
-    unsigned long long scanned = 0;
+    // rewrite every word containing (a, b): this block's share of one slot class
     unsigned singles = 0;
-    for (unsigned i = blockIdx.x * blockDim.x + tid; i < n_act; i += gridDim.x * blockDim.x) {
-        const uint32_t w = W.act[i];
-        const uint32_t len = W.wlen[w];
-        if (len < 2) continue;
-        scanned += len;
-        TokT* t = W.tok + W.wbeg[w];
-        bool hit = false;
-        TokT prev = 0;
-        for (uint32_t base = 0; base < len && !hit; base += CH) {
-            TokT v[CH];
-            *reinterpret_cast<uint4*>(v) = *reinterpret_cast<const uint4*>(t + base);
-#pragma unroll
-            for (int k = 0; k < CH; ++k) {
-                const uint32_t idx = base + k;
-                if (idx < len) {
-                    if (idx > 0 && prev == (TokT)a && v[k] == (TokT)b) hit = true;
-                    prev = v[k];
-                }
-            }
+    const unsigned bid = blockIdx.x;
+    const TokT ta = (TokT)a, tb = (TokT)b, tn = (TokT)nw;
+    if (bid < W.c[1].blk0) {
+        if (bid < W.c[0].blk0 + W.c[0].nblk)
+            scan_class<TokT, 0>(W.c[0], bid - W.c[0].blk0, ta, tb, tn, LR, singles);
+    } else if (bid < W.c[2].blk0) {
+        scan_class<TokT, 1>(W.c[1], bid - W.c[1].blk0, ta, tb, tn, LR, singles);
+    } else if (bid < W.c[3].blk0) {
+        scan_class<TokT, 2>(W.c[2], bid - W.c[2].blk0, ta, tb, tn, LR, singles);
+    } else if (bid < W.lblk0) {
+        scan_class<TokT, 3>(W.c[3], bid - W.c[3].blk0, ta, tb, tn, LR, singles);
+    } else if (bid < W.lblk0 + W.lnblk) {
+        for (unsigned i = (bid - W.lblk0) * blockDim.x + tid; i < W.ln; i += W.lnblk * blockDim.x) {
+            const uint32_t len = W.llen[i];
+            if (len < 2) continue;
+            TokT* t = W.ltok + W.lbeg[i];
+            bool hit = false;
+            for (uint32_t k = 0; k + 1 < len && !hit; ++k) hit = (t[k] == ta) & (t[k + 1] == tb);
+            if (!hit) continue;
+            const uint32_t j = rewrite_word<TokT>(t, len, ta, tb, tn, W.lcnt[i], LR, false);
+            W.llen[i] = j;
+            singles += (j < 2);
         }
-        if (!hit) continue;
-        const unsigned long long c = W.wcnt[w];
-        uint32_t j = 0, r = 0;
-        while (r < len) {
-            const TokT x = t[r];
-            if (x == (TokT)a && r + 1 < len && t[r + 1] == (TokT)b) {
-                if (j > 0) atomicAdd(&LR[2 * (size_t)t[j - 1]], c);          // (x,a)-=c (x,new)+=c
-                if (r + 2 < len) atomicAdd(&LR[2 * (size_t)t[r + 2] + 1], c); // (b,y)-=c (new,y)+=c
-                t[j++] = (TokT)nw;
-                r += 2;
-            } else {
-                t[j++] = x;
-                ++r;
-            }
-        }
-        W.wlen[w] = j;
-        singles += (j < 2);
     }
-    scanned = wave_sum(scanned);
-    singles = wave_sum(singles);
-    if ((tid & 63) == 0) {
-        if (scanned) atomicAdd(&st->scan_slots, scanned);
-        if (singles) atomicAdd(&st->n_single, singles);
-    }
-    (void)s_red;
+    singles = wave_sum(singles);   // words that became one token (rare: no contention)
+    if ((tid & 63) == 0 && singles) atomicAdd(&st->n_single, singles);
 }
 
 // ------------------------------------------------------------------ K2: apply deltas
 __global__ void __launch_bounds__(256) k_apply(RoundState* __restrict__ st, PairsDev P, ToksDev K,
                                                unsigned long long* __restrict__ LR) {
     if (st->halt) return;
-    const unsigned x = blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned x = g >> 2, op = g & 3;   // op: 0 (x,a)-=L  1 (x,new)+=L  2 (b,x)-=R  3 (new,x)+=R
     const int isnew = st->new_is_new;
     const unsigned ntok = (unsigned)st->ntok + (unsigned)isnew;
     const unsigned a = st->cur_a, b = st->cur_b, nw = st->cur_new;
     const int round = st->round;
-    const long long T = st->T;
-    if (x == 0) {
+    if (g == 0) {
         const unsigned bs = st->cur_slot;  // pop(best_pair)
         P.cnt[bs] = 0;
         atomicAnd(&P.flag[bs], ~kPresent);
@@ -377,7 +448,7 @@ __global__ void __launch_bounds__(256) k_apply(RoundState* __restrict__ st, Pair
         }
     }
     if (x >= ntok) return;
-    if (isnew) {
+    if (op == 0 && isnew) {
         const unsigned rnew = st->new_rank[round & 1];
         if (x == nw) K.rank[x] = rnew;
         else {
@@ -385,18 +456,17 @@ __global__ void __launch_bounds__(256) k_apply(RoundState* __restrict__ st, Pair
             K.rank[x] = r + (r >= rnew);
         }
     }
-    const long long l = (long long)LR[2 * (size_t)x];
-    const long long r = (long long)LR[2 * (size_t)x + 1];
-    if (l) {
-        LR[2 * (size_t)x] = 0;
-        if (!(x == a && a == b)) pair_update(P, st, x, a, -l, T);
-        pair_update(P, st, x, nw, l, T);
+    unsigned long long* cell = &LR[2 * (size_t)x + (op >> 1)];
+    const long long d = (long long)*cell;
+    if (!d) return;
+    const long long T = st->T;
+    switch (op) {
+        case 0: if (!(x == a && a == b)) pair_dec(P, st, x, a, d); break;   // never the popped key
+        case 1: pair_inc(P, st, x, nw, d, T); break;
+        case 2: if (!(x == b && a == b)) pair_dec(P, st, b, x, d); break;
+        default: pair_inc(P, st, nw, x, d, T); break;
     }
-    if (r) {
-        LR[2 * (size_t)x + 1] = 0;
-        if (!(x == b && a == b)) pair_update(P, st, b, x, -r, T);
-        pair_update(P, st, nw, x, r, T);
-    }
+    if (op & 1) *cell = 0;   // both lanes of this cell read it in the same load instruction
 }
 
 // ------------------------------------------------------------------ K3: argmax over C
@@ -449,49 +519,66 @@ __global__ void k_collect_words(const unsigned long long* __restrict__ key,
                                 uint32_t* __restrict__ w_len, unsigned long long* __restrict__ w_cnt,
                                 unsigned* __restrict__ n_words, unsigned* __restrict__ max_len) {
     const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= cap) return;
-    const unsigned long long k = key[s];
-    if (!k) return;
+    const unsigned long long k = s < cap ? key[s] : 0ULL;
+    bool keep = k != 0;
     const unsigned len = (unsigned)(k >> 40);
     const unsigned long long off = (k & ((1ULL << 40) - 1)) - 1;
-    for (int i = 0; i < n_sp; ++i) {  // train.py:25 skips matches equal to a special token
+    for (int i = 0; keep && i < n_sp; ++i) {  // train.py:25 skips matches equal to a special
         if (sp_len[i] != len) continue;
         bool eq = true;
         for (unsigned j = 0; j < len && eq; ++j) eq = text[off + j] == sp_bytes[sp_off[i] + j];
-        if (eq) return;
+        if (eq) keep = false;
     }
-    const unsigned idx = atomicAdd(n_words, 1u);
+    const unsigned idx = wave_append(keep, n_words);
+    const unsigned ml = wave_max(keep ? len : 0u);
+    if ((threadIdx.x & 63) == 0 && ml) atomicMax(max_len, ml);
+    if (!keep) return;
     w_off[idx] = off; w_len[idx] = len; w_cnt[idx] = cnt[s];
-    atomicMax(max_len, len);
 }
 
-__global__ void k_chunks(const uint32_t* __restrict__ w_len, unsigned n, int ch,
-                         uint32_t* __restrict__ nch) {
+__global__ void k_len_u64(const uint32_t* __restrict__ w_len, unsigned n, unsigned long long* __restrict__ o) {
     const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) nch[i] = (w_len[i] + ch - 1) / ch;
+    if (i < n) o[i] = w_len[i];
 }
 
+// words -> a CSR of byte ids (the "long" side table)
 template <class TokT>
 __global__ void k_fill_words(const uint8_t* __restrict__ text, const unsigned long long* __restrict__ w_off,
-                             const uint32_t* __restrict__ w_len, const unsigned long long* __restrict__ w_cnt,
-                             const uint32_t* __restrict__ chunk_beg, unsigned n, int ch,
-                             TokT* __restrict__ tok, uint32_t* __restrict__ wbeg,
-                             uint32_t* __restrict__ act, unsigned long long* __restrict__ hist) {
+                             const uint32_t* __restrict__ w_len, const unsigned long long* __restrict__ beg,
+                             unsigned n, TokT* __restrict__ tok) {
     const unsigned w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= n) return;
-    const uint32_t beg = chunk_beg[w] * ch, len = w_len[w];
+    const unsigned long long bg = beg[w];
+    const uint32_t len = w_len[w];
     const uint8_t* src = text + w_off[w];
+    for (uint32_t i = 0; i < len; ++i) tok[bg + i] = (TokT)src[i];
+}
+
+// the initial pair histogram into kHistReplicas copies, so the hottest pairs do not
+// serialize on one address
+__global__ void k_hist_words(const unsigned long long* __restrict__ w_off, const uint32_t* __restrict__ w_len,
+                             const unsigned long long* __restrict__ w_cnt, const uint8_t* __restrict__ text,
+                             unsigned n, unsigned long long* __restrict__ hist) {
+    const unsigned w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= n) return;
+    const uint8_t* src = text + w_off[w];
+    const uint32_t len = w_len[w];
     const unsigned long long c = w_cnt[w];
-    wbeg[w] = beg;
-    act[w] = w;
+    unsigned long long* h = hist + (size_t)(blockIdx.x % kHistReplicas) * 65536;
     unsigned prev = src[0];
-    tok[beg] = (TokT)prev;
-    for (uint32_t i = 1; i < len; ++i) {
+    for (uint32_t i = 1; i < len; ++i) {   // train.py:45-46
         const unsigned cur = src[i];
-        tok[beg + i] = (TokT)cur;
-        atomicAdd(&hist[prev * 256 + cur], c);   // train.py:45-46
+        atomicAdd(&h[prev * 256 + cur], c);
         prev = cur;
     }
+}
+
+__global__ void k_hist_reduce(unsigned long long* __restrict__ hist) {
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 65536) return;
+    unsigned long long s = 0;
+    for (int r = 0; r < kHistReplicas; ++r) s += hist[(size_t)r * 65536 + i];
+    hist[i] = s;
 }
 
 __global__ void k_init_pairs(const unsigned long long* __restrict__ hist, PairsDev P,
@@ -500,8 +587,8 @@ __global__ void k_init_pairs(const unsigned long long* __restrict__ hist, PairsD
     if (i >= 65536) return;
     const long long c = (long long)hist[i];
     if (c <= 0) return;
-    const unsigned long long key = ((((unsigned long long)(i >> 8)) << 32) | (i & 255u)) + 1ULL;
-    const size_t s = pair_slot(P, key, st);
+    bool ins;
+    const size_t s = pair_slot(P, pair_key(i >> 8, i & 255u), st, &ins);
     if (s == ~(size_t)0) return;
     P.cnt[s] = c;
     P.flag[s] = kPresent;
@@ -523,6 +610,81 @@ __global__ void k_init_tokens(ToksDev K) {
             while (K.map[s] != 0) s = (s + 1) & K.map_mask;
             K.map[s] = t + 1;
         }
+    }
+}
+
+// ------------------------------------------------------------------ compaction
+// flat word index -> (class, index); class kNumCls = long table
+template <class TokT>
+__device__ __forceinline__ void word_at(const WordsDev<TokT>& W, unsigned g, int* c, unsigned* i) {
+    unsigned acc = 0;
+    for (int k = 0; k < kNumCls; ++k) {
+        if (g < acc + W.c[k].n) { *c = k; *i = g - acc; return; }
+        acc += W.c[k].n;
+    }
+    *c = kNumCls;
+    *i = g - acc;
+}
+
+template <class TokT>
+__device__ __forceinline__ uint32_t word_len(const WordsDev<TokT>& W, int c, unsigned i) {
+    return c < kNumCls ? (uint32_t)W.c[c].slot[(size_t)i * slot_w(c)] : W.llen[i];
+}
+
+struct MoveCounts {
+    unsigned n[kNumCls + 1];
+    unsigned fill[kNumCls + 1];
+    unsigned long long long_tokens, long_fill;
+};
+
+template <class TokT>
+__global__ void k_move_count(WordsDev<TokT> W, unsigned total, MoveCounts* mc) {
+    const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
+    int d = -1;
+    uint32_t len = 0;
+    if (g < total) {
+        int c;
+        unsigned i;
+        word_at(W, g, &c, &i);
+        len = word_len(W, c, i);
+        if (len >= 2) d = class_for(len);
+    }
+    for (int k = 0; k <= kNumCls; ++k) (void)wave_append(d == k, &mc->n[k]);
+    const unsigned long long lt = wave_sum((unsigned long long)(d == kNumCls ? len : 0u));
+    if ((threadIdx.x & 63) == 0 && lt) atomicAdd(&mc->long_tokens, lt);
+}
+
+template <class TokT>
+__global__ void k_move(WordsDev<TokT> W, unsigned total, WordsDev<TokT> D, MoveCounts* mc) {
+    const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
+    int c = 0, d = -1;
+    unsigned i = 0;
+    uint32_t len = 0;
+    if (g < total) {
+        word_at(W, g, &c, &i);
+        len = word_len(W, c, i);
+        if (len >= 2) d = class_for(len);
+    }
+    unsigned j = ~0u;
+    for (int k = 0; k <= kNumCls; ++k) {
+        const unsigned t = wave_append(d == k, &mc->fill[k]);
+        if (d == k) j = t;
+    }
+    if (d < 0) return;
+    const TokT* src = c < kNumCls ? W.c[c].slot + (size_t)i * slot_w(c) + 1 : W.ltok + W.lbeg[i];
+    const unsigned long long cnt = c < kNumCls ? W.c[c].cnt[i] : W.lcnt[i];
+    if (d < kNumCls) {
+        TokT* dst = D.c[d].slot + (size_t)j * slot_w(d);
+        dst[0] = (TokT)len;
+        for (uint32_t k = 0; k < len; ++k) dst[1 + k] = src[k];
+        for (int k = (int)len + 1; k < slot_w(d); ++k) dst[k] = sentinel<TokT>();
+        D.c[d].cnt[j] = cnt;
+    } else {
+        const unsigned long long bg = atomicAdd(&mc->long_fill, (unsigned long long)len);
+        for (uint32_t k = 0; k < len; ++k) D.ltok[bg + k] = src[k];
+        D.lbeg[j] = bg;
+        D.llen[j] = len;
+        D.lcnt[j] = cnt;
     }
 }
 
@@ -551,24 +713,30 @@ __global__ void k_rebuild_hist(PairsDev P, size_t cap, RebuildStats* rs) {
     if (threadIdx.x < 64 && sh[threadIdx.x]) atomicAdd(&rs->bins[threadIdx.x], sh[threadIdx.x]);
 }
 
-__global__ void k_rebuild_sub(PairsDev P, size_t cap, long long lo, long long width,
+__global__ void k_rebuild_sub(PairsDev P, size_t cap, long long lo, long long hi, long long width,
                               RebuildStats* rs) {
+    __shared__ unsigned sh[1024];
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x) sh[k] = 0;
+    __syncthreads();
     for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap;
          s += (size_t)gridDim.x * blockDim.x) {
         if (!(P.flag[s] & kPresent)) continue;
         const long long c = P.cnt[s];
-        if (c < lo || c >= lo + width * 1024) continue;
-        atomicAdd(&rs->sub[(c - lo) / width], 1ULL);
+        if (c < lo || c >= hi) continue;
+        atomicAdd(&sh[(c - lo) / width], 1u);
     }
+    __syncthreads();
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x)
+        if (sh[k]) atomicAdd(&rs->sub[k], (unsigned long long)sh[k]);
 }
 
 __global__ void k_build_C(PairsDev P, size_t cap, long long T, RoundState* st) {
-    for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap;
-         s += (size_t)gridDim.x * blockDim.x) {
-        const unsigned f = P.flag[s];
+    for (size_t s0 = (size_t)blockIdx.x * blockDim.x; s0 < cap; s0 += (size_t)gridDim.x * blockDim.x) {
+        const size_t s = s0 + threadIdx.x;
+        const unsigned f = s < cap ? P.flag[s] : 0u;
         const bool in = (f & kPresent) && P.cnt[s] >= T;
+        const unsigned idx = wave_append(in, &st->nC);
         if (in) {
-            const unsigned idx = atomicAdd(&st->nC, 1u);
             if (idx < st->capC) P.C[idx] = (unsigned)s;
             else atomicOr(&st->err, ERR_C_FULL);
             if (!(f & kInC)) P.flag[s] = f | kInC;
@@ -580,9 +748,11 @@ __global__ void k_build_C(PairsDev P, size_t cap, long long T, RoundState* st) {
 
 __global__ void k_collect_present(PairsDev P, size_t cap, unsigned long long* out,
                                   unsigned* n_out) {
-    for (size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap;
-         s += (size_t)gridDim.x * blockDim.x) {
-        if (P.flag[s] & kPresent) out[atomicAdd(n_out, 1u)] = P.key[s] - 1ULL;
+    for (size_t s0 = (size_t)blockIdx.x * blockDim.x; s0 < cap; s0 += (size_t)gridDim.x * blockDim.x) {
+        const size_t s = s0 + threadIdx.x;
+        const bool in = s < cap && (P.flag[s] & kPresent);
+        const unsigned idx = wave_append(in, n_out);
+        if (in) out[idx] = P.key[s] - 1ULL;
     }
 }
 
@@ -592,16 +762,11 @@ __global__ void k_rehash(const unsigned long long* __restrict__ okey, const long
     if (i >= ocap) return;
     const unsigned long long k = okey[i];
     if (!k) return;
-    const size_t s = pair_slot(P, k, st);
+    bool ins;
+    const size_t s = pair_slot(P, k, st, &ins);
     if (s == ~(size_t)0) return;
     P.cnt[s] = ocnt[i];
     P.flag[s] = oflag[i] & kPresent;
-}
-
-__global__ void k_flag_active(const uint32_t* __restrict__ act, unsigned n,
-                              const uint32_t* __restrict__ wlen, uint8_t* __restrict__ keep) {
-    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) keep[i] = wlen[act[i]] >= 2;
 }
 
 // ------------------------------------------------------------------ host driver
@@ -609,8 +774,22 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
-struct Timer {
-    hipEvent_t a = nullptr, b = nullptr;
+template <class TokT>
+struct HostWords {   // owns the device arrays behind a WordsDev
+    DevBuf<TokT> slot[kNumCls];
+    DevBuf<unsigned long long> cnt[kNumCls];
+    unsigned n[kNumCls] = {0, 0, 0, 0};
+    DevBuf<TokT> ltok;
+    DevBuf<unsigned long long> lbeg, lcnt;
+    DevBuf<uint32_t> llen;
+    unsigned ln = 0;
+    unsigned total() const { return n[0] + n[1] + n[2] + n[3] + ln; }
+    WordsDev<TokT> dev() const {
+        WordsDev<TokT> W{};
+        for (int c = 0; c < kNumCls; ++c) W.c[c] = SlotCls<TokT>{slot[c].p, cnt[c].p, n[c], 0, 0, 0};
+        W.ltok = ltok.p; W.lbeg = lbeg.p; W.llen = llen.p; W.lcnt = lcnt.p; W.ln = ln;
+        return W;
+    }
 };
 
 template <class TokT>
@@ -623,9 +802,7 @@ class MergeLoop {
     void run();
 
    private:
-    static constexpr int CH = Chunk<TokT>::N;
     static constexpr int kBatch = 64;
-    static constexpr int kMergeBlocks = 1024;
     static constexpr int kArgBlocks = 64;
     static constexpr unsigned long long kTarget = 4096;
 
@@ -640,12 +817,12 @@ class MergeLoop {
     int rebuild();  // 0 ok, 1 exhausted (only zero-count keys), 2 empty
     void exhaustion();
     void compact();
+    void layout_blocks();
     PairsDev pairs() const { return PairsDev{pkey_.p, pcnt_.p, pflag_.p, pcap_ - 1, C_.p}; }
     ToksDev toks() const {
         return ToksDev{pool_.p, toff_.p, tlen_.p, thash_.p, tpw_.p, tkey8_.p, trank_.p, tmap_.p,
                        (uint32_t)(tmap_.n - 1)};
     }
-    WordsDev<TokT> words() const { return WordsDev<TokT>{tok_.p, wbeg_.p, wlen_.p, wcnt_.p, act_.p}; }
 
     hipStream_t s_;
     Comm* comm_;
@@ -657,9 +834,12 @@ class MergeLoop {
     DevBuf<RoundState> st_;
     // words
     unsigned n_words_ = 0, max_len_ = 0;
-    DevBuf<TokT> tok_;
-    DevBuf<uint32_t> wbeg_, wlen_, act_, act2_;
-    DevBuf<unsigned long long> wcnt_;
+    HostWords<TokT> words_;
+    WordsDev<TokT> wdev_{};
+    unsigned merge_grid_ = 1;
+    double scan_bytes_ = 0;
+    unsigned long long long_tokens_ = 0;
+    unsigned n_live_ = 0;
     DevBuf<unsigned long long> hist_;
     // pairs
     size_t pcap_ = 0;
@@ -690,10 +870,9 @@ void MergeLoop<TokT>::build_words(const WordCounts& wc, const std::vector<std::s
         BPE_HIP(hipMemcpyAsync(d_spo.p, spo.data(), spo.size() * 4, hipMemcpyHostToDevice, s_));
         BPE_HIP(hipMemcpyAsync(d_spl.p, spl.data(), spl.size() * 4, hipMemcpyHostToDevice, s_));
     }
-    // compact the occupied count-table slots into (offset, len, count) records
+    // occupied count-table slots -> (offset, len, count) records
     DevBuf<unsigned> cnts(2);
     BPE_HIP(hipMemsetAsync(cnts.p, 0, 8, s_));
-    // upper bound on words: occupied slots (<= cap); count first cheaply by reusing the kernel
     DevBuf<unsigned long long> w_off(wc.cap), w_cnt(wc.cap);
     DevBuf<uint32_t> w_len(wc.cap);
     hipLaunchKernelGGL(k_collect_words, dim3(ceil_div(wc.cap, 256)), dim3(256), 0, s_, wc.key.p,
@@ -706,40 +885,103 @@ void MergeLoop<TokT>::build_words(const WordCounts& wc, const std::vector<std::s
     n_words_ = h2[0];
     max_len_ = h2[1];
     const unsigned n = n_words_;
-    // chunked token storage: each word starts on a 16-byte boundary
-    DevBuf<uint32_t> nch(std::max(n, 1u)), cbeg(std::max(n, 1u) + 1);
-    unsigned total_chunks = 0;
-    if (n) {
-        hipLaunchKernelGGL(k_chunks, dim3(ceil_div(n, 256)), dim3(256), 0, s_, w_len.p, n, CH, nch.p);
-        size_t tb = 0;
-        BPE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, nch.p, cbeg.p, (int)n, s_));
-        DevBuf<uint8_t> tmp(tb);
-        BPE_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, nch.p, cbeg.p, (int)n, s_));
-        unsigned last[2];
-        BPE_HIP(hipMemcpyAsync(&last[0], cbeg.p + n - 1, 4, hipMemcpyDeviceToHost, s_));
-        BPE_HIP(hipMemcpyAsync(&last[1], nch.p + n - 1, 4, hipMemcpyDeviceToHost, s_));
-        BPE_HIP(hipStreamSynchronize(s_));
-        total_chunks = last[0] + last[1];
-    }
-    BPE_REQUIRE((unsigned long long)total_chunks * CH < (1ULL << 32), BPE_E_LIMIT,
-                "word table exceeds 2^32 token slots");
-    tok_.alloc((size_t)std::max(total_chunks, 1u) * CH);
-    wbeg_.alloc(std::max(n, 1u));
-    wlen_.alloc(std::max(n, 1u));
-    wcnt_.alloc(std::max(n, 1u));
-    act_.alloc(std::max(n, 1u));
-    hist_.alloc(65536);
+    hist_.alloc((size_t)kHistReplicas * 65536);
     BPE_HIP(hipMemsetAsync(hist_.p, 0, hist_.bytes(), s_));
+    // all words start in the CSR side table; compact() then sorts them into slot classes
+    HostWords<TokT>& H = words_;
+    unsigned long long total_tok = 0;
+    H.ln = n;
+    H.llen.alloc(std::max(n, 1u));
+    H.lbeg.alloc(std::max(n, 1u));
+    H.lcnt.alloc(std::max(n, 1u));
     if (n) {
-        BPE_HIP(hipMemcpyAsync(wlen_.p, w_len.p, n * 4ull, hipMemcpyDeviceToDevice, s_));
-        BPE_HIP(hipMemcpyAsync(wcnt_.p, w_cnt.p, n * 8ull, hipMemcpyDeviceToDevice, s_));
-        hipLaunchKernelGGL(k_fill_words<TokT>, dim3(ceil_div(n, 256)), dim3(256), 0, s_, text_,
-                           w_off.p, w_len.p, w_cnt.p, cbeg.p, n, CH, tok_.p, wbeg_.p, act_.p, hist_.p);
+        DevBuf<unsigned long long> len64(n);
+        hipLaunchKernelGGL(k_len_u64, dim3(ceil_div(n, 256)), dim3(256), 0, s_, w_len.p, n, len64.p);
+        size_t tb = 0;
+        BPE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, len64.p, H.lbeg.p, (int)n, s_));
+        DevBuf<uint8_t> tmp(tb);
+        BPE_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, len64.p, H.lbeg.p, (int)n, s_));
+        unsigned long long last[2];
+        BPE_HIP(hipMemcpyAsync(&last[0], H.lbeg.p + n - 1, 8, hipMemcpyDeviceToHost, s_));
+        BPE_HIP(hipMemcpyAsync(&last[1], len64.p + n - 1, 8, hipMemcpyDeviceToHost, s_));
+        BPE_HIP(hipStreamSynchronize(s_));
+        total_tok = last[0] + last[1];
+    }
+    H.ltok.alloc(std::max<unsigned long long>(total_tok, 1));
+    if (n) {
+        BPE_HIP(hipMemcpyAsync(H.llen.p, w_len.p, n * 4ull, hipMemcpyDeviceToDevice, s_));
+        BPE_HIP(hipMemcpyAsync(H.lcnt.p, w_cnt.p, n * 8ull, hipMemcpyDeviceToDevice, s_));
+        hipLaunchKernelGGL(k_fill_words<TokT>, dim3(ceil_div(n, 256)), dim3(256), 0, s_, text_, w_off.p,
+                           w_len.p, H.lbeg.p, n, H.ltok.p);
+        hipLaunchKernelGGL(k_hist_words, dim3(ceil_div(n, 256)), dim3(256), 0, s_, w_off.p,
+                           w_len.p, w_cnt.p, text_, n, hist_.p);
         BPE_HIP(hipGetLastError());
     }
+    hipLaunchKernelGGL(k_hist_reduce, dim3(256), dim3(256), 0, s_, hist_.p);
     out_.stats.n_words = n;
-    out_.stats.n_word_tokens = 0;
+    out_.stats.n_word_tokens = (int64_t)total_tok;
     BPE_HIP(hipStreamSynchronize(s_));
+    n_live_ = n;
+    compact();
+}
+
+// Rewrite the word table: drop words of one id, move every word to the narrowest slot class.
+template <class TokT>
+void MergeLoop<TokT>::compact() {
+    HostWords<TokT>& H = words_;
+    const unsigned total = H.total();
+    DevBuf<MoveCounts> mc(1);
+    BPE_HIP(hipMemsetAsync(mc.p, 0, sizeof(MoveCounts), s_));
+    const WordsDev<TokT> src = H.dev();
+    if (total)
+        hipLaunchKernelGGL(k_move_count<TokT>, dim3(ceil_div(total, 256)), dim3(256), 0, s_, src, total, mc.p);
+    MoveCounts h{};
+    BPE_HIP(hipMemcpyAsync(&h, mc.p, sizeof(h), hipMemcpyDeviceToHost, s_));
+    BPE_HIP(hipStreamSynchronize(s_));
+    HostWords<TokT> D;
+    for (int c = 0; c < kNumCls; ++c) {
+        D.n[c] = h.n[c];
+        D.slot[c].alloc(std::max<size_t>((size_t)h.n[c] * slot_w(c), 1));
+        D.cnt[c].alloc(std::max(h.n[c], 1u));
+    }
+    D.ln = h.n[kNumCls];
+    D.ltok.alloc(std::max<unsigned long long>(h.long_tokens, 1));
+    D.lbeg.alloc(std::max(D.ln, 1u));
+    D.llen.alloc(std::max(D.ln, 1u));
+    D.lcnt.alloc(std::max(D.ln, 1u));
+    if (total)
+        hipLaunchKernelGGL(k_move<TokT>, dim3(ceil_div(total, 256)), dim3(256), 0, s_, src, total, D.dev(), mc.p);
+    BPE_HIP(hipGetLastError());
+    BPE_HIP(hipStreamSynchronize(s_));
+    words_ = std::move(D);
+    long_tokens_ = h.long_tokens;
+    n_live_ = words_.total();
+    hs_.n_single = 0;
+    layout_blocks();
+}
+
+// blocks of k_merge per slot class: enough waves to cover each class with a few words per
+// thread in flight, block-uniform class so the scan has no per-lane class branch
+template <class TokT>
+void MergeLoop<TokT>::layout_blocks() {
+    WordsDev<TokT> W = words_.dev();
+    unsigned blk = 0;
+    for (int c = 0; c < kNumCls; ++c) {
+        const unsigned per_thread = c == 0 ? 4 : (c == 1 ? 2 : 1);
+        const unsigned need = ceil_div(W.c[c].n, 256u * per_thread);
+        W.c[c].blk0 = blk;
+        W.c[c].nblk = std::min(need, 2048u);
+        blk += W.c[c].nblk;
+    }
+    W.lblk0 = blk;
+    W.lnblk = std::min(ceil_div(W.ln, 256u), 256u);
+    blk += W.lnblk;
+    merge_grid_ = std::max(blk, 1u);
+    wdev_ = W;
+    // algorithmic bytes of one k_merge launch: every slot, and every long word's ids + length
+    scan_bytes_ = 0;
+    for (int c = 0; c < kNumCls; ++c) scan_bytes_ += (double)W.c[c].n * slot_w(c) * sizeof(TokT);
+    scan_bytes_ += (double)W.ln * 4 + (double)long_tokens_ * sizeof(TokT);
 }
 
 template <class TokT>
@@ -797,7 +1039,7 @@ int MergeLoop<TokT>::rebuild() {
     for (int k = 63; k >= 0; --k)
         if (h.bins[k]) { top = k; break; }
     if (top < 0) return h.ghosts ? 1 : 2;
-    // the bin where the cumulative count from the top crosses the target
+    // the log2 bin where the cumulative count from the top crosses the target
     unsigned long long cum = 0;
     int k = top;
     for (; k >= 0; --k) {
@@ -807,14 +1049,14 @@ int MergeLoop<TokT>::rebuild() {
     long long T;
     if (k < 0) {
         T = 1;
-    } else {
-        const long long lo = 1LL << k;
+    } else {  // refine inside bin k with 1024 linear sub-bins
+        const long long lo = 1LL << k, hi = lo << 1;
         const long long width = std::max(1LL, lo / 1024);
-        hipLaunchKernelGGL(k_rebuild_sub, dim3(grid), dim3(256), 0, s_, pairs(), pcap_, lo, width, rs_.p);
+        hipLaunchKernelGGL(k_rebuild_sub, dim3(grid), dim3(256), 0, s_, pairs(), pcap_, lo, hi, width, rs_.p);
         BPE_HIP(hipGetLastError());
         BPE_HIP(hipMemcpyAsync(h.sub, rs_.p->sub, sizeof(h.sub), hipMemcpyDeviceToHost, s_));
         BPE_HIP(hipStreamSynchronize(s_));
-        T = lo << 1;  // everything above bin k
+        T = hi;  // everything above bin k
         for (int j = 1023; j >= 0; --j) {
             if (!h.sub[j]) continue;
             if (cum + h.sub[j] > kTarget && cum > 0) break;
@@ -833,32 +1075,15 @@ int MergeLoop<TokT>::rebuild() {
     BPE_HIP(hipGetLastError());
     pull_state();
     BPE_REQUIRE(!(hs_.err & ERR_C_FULL), BPE_E_NOMEM, "candidate list overflow");
+    // re-threshold when C has grown 4x (or past 16k) by crossings since this rebuild
+    hs_.c_limit = (unsigned)std::min<unsigned long long>(
+        std::max<unsigned long long>(4ull * hs_.nC, 4 * kTarget), hs_.capC);
+    push_state();
     return 0;
 }
 
 template <class TokT>
-void MergeLoop<TokT>::compact() {
-    const unsigned n = hs_.n_act;
-    if (!n) return;
-    DevBuf<uint8_t> keep(n);
-    DevBuf<unsigned> nsel(1);
-    hipLaunchKernelGGL(k_flag_active, dim3(ceil_div(n, 256)), dim3(256), 0, s_, act_.p, n, wlen_.p, keep.p);
-    size_t tb = 0;
-    BPE_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, act_.p, keep.p, act2_.p, nsel.p, (int)n, s_));
-    DevBuf<uint8_t> tmp(tb);
-    BPE_HIP(hipcub::DeviceSelect::Flagged(tmp.p, tb, act_.p, keep.p, act2_.p, nsel.p, (int)n, s_));
-    unsigned m = 0;
-    BPE_HIP(hipMemcpyAsync(&m, nsel.p, 4, hipMemcpyDeviceToHost, s_));
-    BPE_HIP(hipStreamSynchronize(s_));
-    std::swap(act_, act2_);
-    hs_.n_act = m;
-    hs_.n_single = 0;
-    push_state();
-}
-
-template <class TokT>
 void MergeLoop<TokT>::run() {
-    const unsigned n = n_words_;
     st_.alloc(1);
     rs_.alloc(1);
     part_.alloc(kArgBlocks);
@@ -872,20 +1097,20 @@ void MergeLoop<TokT>::run() {
     BPE_HIP(hipMemsetAsync(tmap_.p, 0, tmap_.bytes(), s_));
     const unsigned pool_cap = std::max(1u << 16, 64u * std::max(max_len_, 8u));
     pool_.alloc(pool_cap);
-    act2_.alloc(std::max(n, 1u));
 
     // global initial pair histogram (train.py:35-49): one all-reduce when sharded
     if (comm_ && comm_->nranks > 1)
         comm_->allreduce_i64(reinterpret_cast<int64_t*>(hist_.p), 65536, s_);
     alloc_pairs(size_t(1) << 22);
+    const unsigned n_single_keep = hs_.n_single;
     memset(&hs_, 0, sizeof(hs_));
+    hs_.n_single = n_single_keep;
     hs_.n_rounds = n_rounds_;
     hs_.ntok = 256;
     hs_.capC = (unsigned)pcap_;
-    hs_.n_act = n;
+    hs_.c_limit = (unsigned)pcap_;
     hs_.pool_used = 256;
     hs_.pool_cap = pool_cap;
-    hs_.halt = HALT_REBUILD;
     push_state();
     hipLaunchKernelGGL(k_init_tokens, dim3(1), dim3(256), 0, s_, toks());
     hipLaunchKernelGGL(k_init_pairs, dim3(256), dim3(256), 0, s_, hist_.p, pairs(), st_.p);
@@ -899,10 +1124,9 @@ void MergeLoop<TokT>::run() {
         ev.resize(2 * kBatch);
         for (auto& e : ev) BPE_HIP(hipEventCreate(&e));
     }
-    double k1_ms = 0;
+    double k1_ms = 0, k1_bytes = 0;
     long long k1_launches = 0;
     const bool sharded = comm_ && comm_->nranks > 1;
-    const int merge_blocks = (int)std::min<unsigned>(kMergeBlocks, std::max(1u, ceil_div(n, 256)));
 
     for (;;) {
         if (hs_.round >= n_rounds_) break;
@@ -925,27 +1149,28 @@ void MergeLoop<TokT>::run() {
         const long long start_round = hs_.round;
         for (int k = 0; k < R; ++k) {
             if (timing) BPE_HIP(hipEventRecord(ev[2 * k], s_));
-            hipLaunchKernelGGL(k_merge<TokT>, dim3(merge_blocks), dim3(256), 0, s_, st_.p, part_.p,
-                               kArgBlocks, pairs(), toks(), words(), LR_.p, m_a_.p, m_b_.p, m_new_.p);
+            hipLaunchKernelGGL(k_merge<TokT>, dim3(merge_grid_), dim3(256), 0, s_, st_.p, part_.p,
+                               kArgBlocks, pairs(), toks(), wdev_, LR_.p, m_a_.p, m_b_.p, m_new_.p);
             if (timing) BPE_HIP(hipEventRecord(ev[2 * k + 1], s_));
             if (sharded) {
                 const size_t ntok_bound = 256 + (size_t)start_round + k + 1;
                 comm_->allreduce_i64(reinterpret_cast<int64_t*>(LR_.p), 2 * ntok_bound, s_);
             }
             const unsigned ntb = 256u + (unsigned)start_round + (unsigned)k + 1u;
-            hipLaunchKernelGGL(k_apply, dim3(ceil_div(ntb, 256)), dim3(256), 0, s_, st_.p, pairs(),
-                               toks(), LR_.p);
+            hipLaunchKernelGGL(k_apply, dim3(ceil_div(4ull * ntb, 256)), dim3(256), 0, s_, st_.p,
+                               pairs(), toks(), LR_.p);
             hipLaunchKernelGGL(k_argmax, dim3(kArgBlocks), dim3(256), 0, s_, st_.p, pairs(),
                                trank_.p, part_.p, 1);
         }
         BPE_HIP(hipGetLastError());
         pull_state();
         if (timing) {
-            const int done = (int)(hs_.round - start_round) + (hs_.halt ? 1 : 0);
+            const int done = (int)(hs_.round - start_round);
             for (int k = 0; k < std::min(done, R); ++k) {
                 float t = 0;
                 BPE_HIP(hipEventElapsedTime(&t, ev[2 * k], ev[2 * k + 1]));
                 k1_ms += t;
+                k1_bytes += scan_bytes_;
                 ++k1_launches;
             }
         }
@@ -953,12 +1178,15 @@ void MergeLoop<TokT>::run() {
         BPE_REQUIRE(!(hs_.err & ERR_C_FULL), BPE_E_NOMEM, "candidate list overflow");
         BPE_REQUIRE(!(hs_.err & ERR_POOL), BPE_E_NOMEM, "token pool overflow");
         if (hs_.halt == HALT_DONE) break;
-        if (hs_.n_single > hs_.n_act / 4 + 1024) compact();
+        if (hs_.n_single > n_live_ / 4 + 1024) {
+            compact();
+            push_state();
+        }
     }
     for (auto& e : ev) (void)hipEventDestroy(e);
     out_.stats.merge_kernel_ms = k1_ms;
     out_.stats.merge_kernel_launches = k1_launches;
-    out_.stats.merge_kernel_bytes = (double)hs_.scan_slots * sizeof(TokT);
+    out_.stats.merge_kernel_bytes = k1_bytes;
     out_.stats.n_pairs_final = (int64_t)hs_.pair_used;
     out_.stats.n_rounds_device = hs_.round;
 
@@ -971,21 +1199,18 @@ void MergeLoop<TokT>::run() {
         BPE_HIP(hipMemcpyAsync(mn.data(), m_new_.p, rd * 4ull, hipMemcpyDeviceToHost, s_));
         BPE_HIP(hipStreamSynchronize(s_));
     }
-    // (out_.tok_bytes / merges may already hold the exhaustion tail: prepend device rounds)
+    // (out_.merges may already hold the exhaustion tail: prepend the device rounds)
     std::vector<std::pair<std::string, std::string>> tail = std::move(out_.merges);
     out_.merges.clear();
-    if (out_.tok_bytes.empty()) {
-        for (int b = 0; b < 256; ++b) out_.tok_bytes.push_back(std::string(1, (char)b));
-        std::unordered_map<std::string, uint32_t> index;
-        for (int r = 0; r < rd; ++r) {
-            std::string nb = out_.tok_bytes[ma[r]] + out_.tok_bytes[mb[r]];
-            if (mn[r] == out_.tok_bytes.size()) out_.tok_bytes.push_back(nb);
-            else BPE_REQUIRE(mn[r] < out_.tok_bytes.size() && out_.tok_bytes[mn[r]] == nb,
-                             BPE_E_HIP, "device token dedupe disagrees with host replay");
-            out_.merges.emplace_back(out_.tok_bytes[ma[r]], out_.tok_bytes[mb[r]]);
-        }
-    } else {
-        for (int r = 0; r < rd; ++r) out_.merges.emplace_back(out_.tok_bytes[ma[r]], out_.tok_bytes[mb[r]]);
+    auto& tb = out_.tok_bytes;
+    tb.clear();
+    for (int b = 0; b < 256; ++b) tb.push_back(std::string(1, (char)b));
+    for (int r = 0; r < rd; ++r) {
+        std::string nb = tb[ma[r]] + tb[mb[r]];
+        if (mn[r] == tb.size()) tb.push_back(nb);
+        else BPE_REQUIRE(mn[r] < tb.size() && tb[mn[r]] == nb, BPE_E_HIP,
+                         "device token dedupe disagrees with host replay");
+        out_.merges.emplace_back(tb[ma[r]], tb[mb[r]]);
     }
     for (auto& m : tail) out_.merges.push_back(std::move(m));
 }
@@ -1013,8 +1238,7 @@ void MergeLoop<TokT>::exhaustion() {
         BPE_HIP(hipMemcpyAsync(hkeys.data(), keys.p, hk * 8ull, hipMemcpyDeviceToHost, s_));
         BPE_HIP(hipStreamSynchronize(s_));
     }
-    auto& tb = out_.tok_bytes;
-    tb.clear();
+    std::vector<std::string> tb;
     for (int b = 0; b < 256; ++b) tb.push_back(std::string(1, (char)b));
     for (int r = 0; r < rd; ++r) {
         std::string nb = tb[ma[r]] + tb[mb[r]];
