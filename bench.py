@@ -211,7 +211,8 @@ def main():
             "phases_ms": {k: round(s0[k], 2) for k in ("t_prepare_ms", "t_count_ms", "t_words_ms",
                                                         "t_merge_ms", "t_total_ms")},
             "counters": {k: s0[k] for k in ("n_pretokens", "n_words", "n_pairs_final",
-                                            "n_rebuilds", "n_rounds_device", "n_rounds_host")},
+                                            "n_rebuilds", "n_rounds_device", "n_rounds_host",
+                                            "n_index_builds")},
         }
         print(json.dumps(line), flush=True)
     if world > 1:

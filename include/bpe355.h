@@ -110,6 +110,7 @@ typedef struct {
     int64_t n_rebuilds;       /* candidate-set rebuilds */
     int64_t n_rounds_device;  /* merges decided on the device */
     int64_t n_rounds_host;    /* zero-count merges emitted after exhaustion */
+    int64_t n_index_builds;   /* word-table compactions + posting-list builds */
 } bpe_train_stats;
 int bpe_result_stats(const bpe_result* r, bpe_train_stats* out);
 void bpe_result_free(bpe_result* r);

@@ -1,0 +1,111 @@
+"""Sharded (multi-rank) training on the GPU, 2 processes sharing one MI355X.
+
+RCCL refuses two ranks on one device, so the per-round all-reduce goes through the library's
+host-staged communicator (bpe_comm_init_host) backed by torch.distributed/gloo; everything
+else -- slab pre-tokenization, local word tables, the delta cells, the replicated pair table,
+the argmax -- is the same HIP code the RCCL path runs.  Every rank must end with exactly the
+unsharded result.
+"""
+import ctypes
+import multiprocessing as mp
+import os
+
+import pytest
+
+import golden_cases as G
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _worker(rank, world, port, slab, vocab_size, specials, q):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from bpe_amd import _lib, train_bpe_bytes
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import datetime
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=180))
+    try:
+        L = _lib.lib()
+
+        @_lib.HOST_ALLREDUCE_FN
+        def allreduce(_ctx, buf, count):
+            arr = np.ctypeslib.as_array(buf, shape=(count,))
+            t = torch.from_numpy(arr)   # shares memory with the library's staging buffer
+            dist.all_reduce(t)
+            return 0
+
+        h = ctypes.c_void_p()
+        _lib.check(L.bpe_comm_init_host(allreduce, None, world, rank, 0, ctypes.byref(h)), "comm")
+
+        class Comm:
+            handle = h
+
+        try:
+            vocab, merges = train_bpe_bytes(slab, vocab_size, specials, comm=Comm())
+        finally:
+            L.bpe_comm_free(h)
+        q.put((rank, (vocab, merges)))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _safe_cuts(data, world):
+    from bpe_amd import _lib
+    L = _lib.lib()
+    return [0] + [L.bpe_safe_split(data, len(data), len(data) * r // world)
+                  for r in range(1, world)] + [len(data)]
+
+
+def run_sharded(data, world, vocab_size, specials):
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cuts = _safe_cuts(data, world)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, data[cuts[r]:cuts[r + 1]],
+                                               vocab_size, specials, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in procs:
+            r, v = q.get(timeout=400)
+            out[r] = v
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    return out
+
+
+@pytest.mark.parametrize("name", ["corpus_en_1000", "tiny_1200", "synth_mixed_200k"])
+def test_sharded_gpu_matches_reference(name):
+    o, vocab, merges = G.train_expect(name)
+    data = G.input_bytes(o["input"])
+    out = run_sharded(data, 2, o["vocab_size"], o["special_tokens"])
+    for r in (0, 1):
+        assert not isinstance(out[r], str), out[r]
+        assert out[r][1] == merges
+        assert out[r][0] == vocab
+
+
+def test_sharded_gpu_synthetic_vs_oracle():
+    import synth_text
+    data = synth_text.generate(31, 4_000_000, "ascii").encode("utf-8")
+    want = oracle.train_raw(data, 5000, ["<|endoftext|>"])
+    out = run_sharded(data, 2, 5000, ["<|endoftext|>"])
+    for r in (0, 1):
+        assert not isinstance(out[r], str), out[r]
+        assert out[r][1] == want[1]
+        assert out[r][0] == want[0]

@@ -32,7 +32,7 @@ class TrainStats(ctypes.Structure):
         ("n_bytes", ctypes.c_int64), ("n_pretokens", ctypes.c_int64), ("n_words", ctypes.c_int64),
         ("n_word_tokens", ctypes.c_int64), ("n_pairs_final", ctypes.c_int64),
         ("n_rebuilds", ctypes.c_int64), ("n_rounds_device", ctypes.c_int64),
-        ("n_rounds_host", ctypes.c_int64),
+        ("n_rounds_host", ctypes.c_int64), ("n_index_builds", ctypes.c_int64),
     ]
 
     def as_dict(self):

@@ -40,6 +40,7 @@
 #include <algorithm>
 #include <chrono>
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 #include <set>
 #include <unordered_map>
@@ -63,7 +64,8 @@ struct RoundState {
     int n_rounds;
     int ntok;
     long long T;
-    unsigned nC, capC, c_limit, pad0;
+    unsigned nC, capC, c_limit, n_touched;
+    unsigned nC_base, pad1;     // |C| before this round's k_argmax appends (set by k_merge)
     unsigned cur_a, cur_b, cur_new, cur_slot;
     long long cur_cnt;
     int new_is_new;
@@ -77,8 +79,8 @@ struct RoundState {
 
 struct Partial {
     long long cnt;
-    unsigned long long tb;
-    unsigned slot, pad;
+    unsigned long long tb;   // (rank a << 32) | rank b
+    unsigned slot, a, b, pad;
 };
 
 struct PairsDev {
@@ -121,6 +123,22 @@ struct WordsDev {
     uint32_t* llen;
     unsigned long long* lcnt;
     unsigned ln, lblk0, lnblk, pad;
+    unsigned off[kNumCls + 1];   // flat word index: class c holds [off[c], off[c+1])
+};
+
+// Posting index over the slot words, rebuilt at every compaction: list[beg[t], beg[t]+len[t])
+// holds the flat index of every word that contained token t at build time.  A token created
+// later inherits anc = the smaller covering list of its two parts (a word that contains it
+// contained both parts when it was formed); a token re-created through token dedupe (its
+// bytes reached by another split) is marked uncovered (kNoAnc) until the next build.
+constexpr unsigned kNoAnc = 0xffffffffu;
+struct IndexDev {
+    const uint32_t* list;
+    const uint32_t* beg;
+    const uint32_t* len;
+    uint32_t* anc;
+    unsigned full_threshold;   // lists longer than this are cheaper to replace by a full scan
+    unsigned n_slot_words;
 };
 
 template <class TokT> __host__ __device__ constexpr TokT sentinel() { return (TokT)~(TokT)0; }
@@ -169,23 +187,18 @@ __device__ __forceinline__ void pair_dec(const PairsDev& P, RoundState* st, unsi
     if (ins) atomicOr(&P.flag[s], kPresent);
 }
 
-// frequencies[(p, q)] += d; the key is present from now on; crossing T enters C
-__device__ __forceinline__ void pair_inc(const PairsDev& P, RoundState* st, unsigned p, unsigned q,
-                                         long long d, long long T) {
+// frequencies[(p, q)] += d; the key is present from now on.  Returns the slot so the caller
+// can list it as touched: whether it enters the candidate list is decided from its FINAL
+// count in k_argmax -- never from the order the atomics happened to land in, which differs
+// between ranks and would let replicated pair tables disagree about C.
+__device__ __forceinline__ size_t pair_inc(const PairsDev& P, RoundState* st, unsigned p, unsigned q,
+                                           long long d) {
     bool ins;
     const size_t s = pair_slot(P, pair_key(p, q), st, &ins);
-    if (s == ~(size_t)0) return;
-    const long long old = (long long)atomicAdd((unsigned long long*)&P.cnt[s], (unsigned long long)d);
-    if (old < T && old + d >= T) {
-        const unsigned prev = atomicOr(&P.flag[s], kPresent | kInC);
-        if (!(prev & kInC)) {
-            const unsigned idx = atomicAdd(&st->nC, 1u);
-            if (idx < st->capC) P.C[idx] = (unsigned)s;
-            else atomicOr(&st->err, ERR_C_FULL);
-        }
-    } else {
-        atomicOr(&P.flag[s], kPresent);
-    }
+    if (s == ~(size_t)0) return s;
+    atomicAdd((unsigned long long*)&P.cnt[s], (unsigned long long)d);
+    atomicOr(&P.flag[s], kPresent);
+    return s;
 }
 
 // ------------------------------------------------------------------ token helpers
@@ -229,15 +242,32 @@ __device__ bool equals_concat(const ToksDev& K, unsigned x, unsigned a, unsigned
 // The reference's in-place merge of one word (train.py:196-224): t[0..len) -> t[0..j).
 // Per occurrence: the left neighbour is already rewritten (t[j-1]); the right one is the
 // original t[r+2].  With `pad`, the freed tail is refilled with the sentinel.
-template <class TokT>
-__device__ uint32_t rewrite_word(TokT* __restrict__ t, uint32_t len, TokT a, TokT b, TokT nw,
-                                 unsigned long long c, unsigned long long* __restrict__ LR, bool pad) {
+// Per-occurrence deltas are keyed by the neighbour token: cell 2x = L[x] for (x,a)-=c and
+// (x,new)+=c, cell 2x+1 = R[x] for (b,x)-=c and (new,x)+=c.  Cells of ids below kLdsLR (the
+// bytes and the first merges: neighbours hot enough to serialize a global atomic) are summed
+// in LDS per workgroup and flushed once; the others go out directly.
+constexpr unsigned kLdsLR = 512;
+
+// (Applying the four pair updates of a cell inside the merge kernel instead was measured
+// slower: one hit's updates form a serial chain on one thread; see DESIGN.md.)
+struct DeltaSink {
+    unsigned long long* LR;     // global delta cells (all-reduced when sharded) for k_apply
+    unsigned long long* lds;
+    __device__ __forceinline__ void add(unsigned cell, unsigned long long c) const {
+        if (cell < 2 * kLdsLR) atomicAdd(&lds[cell], c);
+        else atomicAdd(&LR[cell], c);
+    }
+};
+
+template <class TokT, class Sink>
+__device__ __forceinline__ uint32_t rewrite_word(TokT* __restrict__ t, uint32_t len, TokT a, TokT b,
+                                                 TokT nw, unsigned long long c, const Sink& D, bool pad) {
     uint32_t j = 0, r = 0;
     while (r < len) {
         const TokT x = t[r];
         if (x == a && r + 1 < len && t[r + 1] == b) {
-            if (j > 0) atomicAdd(&LR[2 * (size_t)t[j - 1]], c);           // (x,a)-=c, (x,new)+=c
-            if (r + 2 < len) atomicAdd(&LR[2 * (size_t)t[r + 2] + 1], c);  // (b,y)-=c, (new,y)+=c
+            if (j > 0) D.add(2u * (unsigned)t[j - 1], c);           // (x,a)-=c, (x,new)+=c
+            if (r + 2 < len) D.add(2u * (unsigned)t[r + 2] + 1, c);  // (b,y)-=c, (new,y)+=c
             t[j++] = nw;
             r += 2;
         } else {
@@ -251,10 +281,9 @@ __device__ uint32_t rewrite_word(TokT* __restrict__ t, uint32_t len, TokT a, Tok
 }
 
 // scan one slot class: U words in flight per thread, one 16-byte load per 16 bytes of slot
-template <class TokT, int C>
+template <class TokT, int C, class Sink>
 __device__ __forceinline__ void scan_class(const SlotCls<TokT>& S, unsigned bi, TokT a, TokT b,
-                                           TokT nw, unsigned long long* __restrict__ LR,
-                                           unsigned& singles) {
+                                           TokT nw, const Sink& D, unsigned& singles) {
     constexpr int W = slot_w(C);
     constexpr int V = W * (int)sizeof(TokT) / 16;
     constexpr int U = V == 1 ? 4 : (V == 2 ? 2 : 1);
@@ -280,11 +309,33 @@ __device__ __forceinline__ void scan_class(const SlotCls<TokT>& S, unsigned bi, 
             if (hit) {
                 TokT* s = S.slot + (size_t)i * W;
                 const uint32_t len = e[0];
-                const uint32_t j = rewrite_word<TokT>(s + 1, len, a, b, nw, S.cnt[i], LR, true);
+                const uint32_t j = rewrite_word(s + 1, len, a, b, nw, S.cnt[i], D, true);
                 s[0] = (TokT)j;
                 singles += (j < 2);
             }
         }
+    }
+}
+
+// one word of class C addressed directly (index-list mode)
+template <class TokT, int C, class Sink>
+__device__ __forceinline__ void merge_one(const SlotCls<TokT>& S, unsigned i, TokT a, TokT b,
+                                          TokT nw, const Sink& D, unsigned& singles) {
+    constexpr int W = slot_w(C);
+    constexpr int V = W * (int)sizeof(TokT) / 16;
+    uint4 r[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) r[v] = reinterpret_cast<const uint4*>(S.slot + (size_t)i * W)[v];
+    TokT e[W];
+    __builtin_memcpy(e, r, sizeof(e));
+    bool hit = false;
+#pragma unroll
+    for (int k = 1; k + 1 < W; ++k) hit |= (e[k] == a) & (e[k + 1] == b);
+    if (hit) {
+        TokT* s = S.slot + (size_t)i * W;
+        const uint32_t j = rewrite_word(s + 1, e[0], a, b, nw, S.cnt[i], D, true);
+        s[0] = (TokT)j;
+        singles += (j < 2);
     }
 }
 
@@ -295,62 +346,80 @@ struct BestShared {
     long long cnt;
     unsigned long long hash, k8;
     int round, ntok;
+    unsigned list_beg, list_len, use_list, anc_new;
 };
 
 template <class TokT>
 __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
                                                const Partial* __restrict__ part, int nparts,
                                                PairsDev P, ToksDev K, WordsDev<TokT> W,
-                                               unsigned long long* __restrict__ LR,
+                                               IndexDev X, unsigned long long* __restrict__ LR,
                                                uint32_t* __restrict__ m_a, uint32_t* __restrict__ m_b,
-                                               uint32_t* __restrict__ m_new) {
+                                               uint32_t* __restrict__ m_new, uint32_t* __restrict__ m_mode) {
     __shared__ BestShared sb;
+    __shared__ unsigned long long l_lr[2 * kLdsLR];
     const int tid = threadIdx.x;
+    for (unsigned k = tid; k < 2 * kLdsLR; k += blockDim.x) l_lr[k] = 0;
     if (tid < 64) {
-        // every workgroup redundantly decides the round: no extra launch, no grid sync
-        int stop = HALT_NONE;
-        const int halt = st->halt, round = st->round;
-        if (halt) stop = -1;
-        else if (round >= st->n_rounds) stop = HALT_DONE;
-        else if (st->nC > st->c_limit) stop = HALT_REBUILD;   // C bloated: re-threshold
-        long long bc = LLONG_MIN;
-        unsigned long long bt = 0;
-        unsigned bs = 0;
-        if (!stop) {
-            for (int i = tid; i < nparts; i += 64) {
-                const Partial pp = part[i];
-                if (cand_better(pp.cnt, pp.tb, bc, bt)) { bc = pp.cnt; bt = pp.tb; bs = pp.slot; }
-            }
-            for (int o = 32; o > 0; o >>= 1) {
-                const long long oc = __shfl_xor(bc, o);
-                const unsigned long long ot = __shfl_xor(bt, o);
-                const unsigned os = __shfl_xor(bs, o);
-                if (cand_better(oc, ot, bc, bt)) { bc = oc; bt = ot; bs = os; }
-            }
-            if (bc < st->T) stop = HALT_REBUILD;
+        // Every workgroup redundantly decides the round (no extra launch, no grid sync).  The
+        // loads are grouped by dependency level so the chain is ~4 memory latencies long:
+        // state + partials | token metadata, posting-list ids | map slot, list bounds | (dedupe)
+        const int halt = st->halt, round = st->round, ntok = st->ntok;
+        const int n_rounds = st->n_rounds;
+        const unsigned nC = st->nC, c_limit = st->c_limit;   // only k_argmax appends to C
+        const long long T = st->T;
+        Partial pp{LLONG_MIN, 0, 0, 0, 0, 0};
+        if (tid < nparts) pp = part[tid];
+        for (int o = 32; o > 0; o >>= 1) {
+            const long long oc = __shfl_xor(pp.cnt, o);
+            const unsigned long long ot = __shfl_xor(pp.tb, o);
+            const unsigned os = __shfl_xor(pp.slot, o), oa = __shfl_xor(pp.a, o), ob = __shfl_xor(pp.b, o);
+            if (cand_better(oc, ot, pp.cnt, pp.tb)) { pp.cnt = oc; pp.tb = ot; pp.slot = os; pp.a = oa; pp.b = ob; }
         }
+        int stop = HALT_NONE;
+        if (halt) stop = -1;
+        else if (round >= n_rounds) stop = HALT_DONE;
+        else if (nC > c_limit) stop = HALT_REBUILD;   // C bloated: re-threshold
+        else if (pp.cnt < T) stop = HALT_REBUILD;     // max(C) < T: re-threshold
         if (tid == 0) {
             sb.stop = stop;
             if (!stop) {
-                const unsigned long long key = P.key[bs] - 1ULL;
-                const unsigned a = (unsigned)(key >> 32), b = (unsigned)(key & 0xffffffffu);
-                const int ntok = st->ntok;
-                // token dedupe: does bytes(a) + bytes(b) already exist?
-                const unsigned long long h = K.hash[a] * K.pw[b] + K.hash[b];
-                const unsigned ln = K.len[a] + K.len[b];
-                unsigned nw = (unsigned)ntok;
+                const unsigned a = pp.a, b = pp.b;
+                // level 1: everything keyed by a or b
+                const unsigned long long ha = K.hash[a], pb = K.pw[b], hb = K.hash[b];
+                const unsigned la = K.len[a], lb = K.len[b];
+                const unsigned long long ka = K.key8[a], kb = K.key8[b];
+                const unsigned ua = X.anc[a], ub = X.anc[b];
+                const unsigned long long h = ha * pb + hb;
+                const unsigned ln = la + lb;
+                // level 2: first map slot, posting-list sizes and starts
                 unsigned s = (unsigned)mix64(h) & K.map_mask;
-                for (unsigned m; (m = K.map[s]) != 0; s = (s + 1) & K.map_mask) {
+                unsigned m = K.map[s];
+                const unsigned sa = X.len[ua != kNoAnc ? ua : 0], sb_ = X.len[ub != kNoAnc ? ub : 0];
+                const unsigned ba = X.beg[ua != kNoAnc ? ua : 0], bbg = X.beg[ub != kNoAnc ? ub : 0];
+                // token dedupe: does bytes(a) + bytes(b) already exist? (usually: empty slot)
+                unsigned nw = (unsigned)ntok;
+                for (; m != 0; s = (s + 1) & K.map_mask, m = K.map[s]) {
                     const unsigned id = m - 1;
                     if (K.hash[id] == h && K.len[id] == ln && equals_concat(K, id, a, b)) {
                         nw = id;
                         break;
                     }
                 }
-                sb.a = a; sb.b = b; sb.nw = nw; sb.slot = bs; sb.cnt = bc;
+                sb.a = a; sb.b = b; sb.nw = nw; sb.slot = pp.slot; sb.cnt = pp.cnt;
                 sb.isnew = (nw == (unsigned)ntok);
-                sb.hash = h; sb.k8 = concat_key8(K, a, b);
+                sb.hash = h;
+                sb.k8 = la >= 8 ? ka : (ka | (kb >> (8 * la)));
                 sb.round = round; sb.ntok = ntok;
+                // which words can contain (a, b): the smaller covering posting list, or all
+                const unsigned za = ua != kNoAnc ? sa : 0xffffffffu;
+                const unsigned zb = ub != kNoAnc ? sb_ : 0xffffffffu;
+                const bool pick_a = za <= zb;
+                const unsigned u = pick_a ? ua : ub, lu = pick_a ? za : zb;
+                sb.use_list = u != kNoAnc && lu <= X.full_threshold;
+                sb.list_beg = sb.use_list ? (pick_a ? ba : bbg) : 0;
+                sb.list_len = sb.use_list ? lu : 0;
+                sb.anc_new = sb.isnew ? u : kNoAnc;   // dedupe: uncovered until the next build
             }
         }
     }
@@ -362,11 +431,17 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
     const unsigned a = sb.a, b = sb.b, nw = sb.nw;
     const int ntok = sb.ntok;
 
-    if (blockIdx.x == 0) {  // record the merge and register a new token
+    if (blockIdx.x == 0) {  // record the merge, pop the pair, register a new token
         if (tid == 0) {
+            st->nC_base = st->nC;     // C entries k_argmax may read without racing its appends
+            st->n_touched = 0;
+            P.cnt[sb.slot] = 0;                       // byte_pair_frequencies.pop(best_pair)
+            atomicAnd(&P.flag[sb.slot], ~kPresent);   // (no other update touches this key)
             st->cur_a = a; st->cur_b = b; st->cur_new = nw; st->cur_slot = sb.slot;
             st->cur_cnt = sb.cnt; st->new_is_new = (int)sb.isnew;
             m_a[sb.round] = a; m_b[sb.round] = b; m_new[sb.round] = nw;
+            m_mode[sb.round] = sb.use_list ? sb.list_len : 0xffffffffu;
+            X.anc[nw] = sb.anc_new;
         }
         if (sb.isnew) {
             const unsigned la = K.len[a], ln = la + K.len[b];
@@ -400,15 +475,26 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
     unsigned singles = 0;
     const unsigned bid = blockIdx.x;
     const TokT ta = (TokT)a, tb = (TokT)b, tn = (TokT)nw;
-    if (bid < W.c[1].blk0) {
+    const DeltaSink D{LR, l_lr};
+    if (sb.use_list && bid < W.lblk0) {
+        // index mode: only the words on the posting list (a gather of their slots)
+        const uint32_t* L = X.list + sb.list_beg;
+        for (unsigned i = bid * blockDim.x + tid; i < sb.list_len; i += W.lblk0 * blockDim.x) {
+            const unsigned f = L[i];
+            if (f < W.off[1]) merge_one<TokT, 0>(W.c[0], f, ta, tb, tn, D, singles);
+            else if (f < W.off[2]) merge_one<TokT, 1>(W.c[1], f - W.off[1], ta, tb, tn, D, singles);
+            else if (f < W.off[3]) merge_one<TokT, 2>(W.c[2], f - W.off[2], ta, tb, tn, D, singles);
+            else merge_one<TokT, 3>(W.c[3], f - W.off[3], ta, tb, tn, D, singles);
+        }
+    } else if (bid < W.c[1].blk0) {
         if (bid < W.c[0].blk0 + W.c[0].nblk)
-            scan_class<TokT, 0>(W.c[0], bid - W.c[0].blk0, ta, tb, tn, LR, singles);
+            scan_class<TokT, 0>(W.c[0], bid - W.c[0].blk0, ta, tb, tn, D, singles);
     } else if (bid < W.c[2].blk0) {
-        scan_class<TokT, 1>(W.c[1], bid - W.c[1].blk0, ta, tb, tn, LR, singles);
+        scan_class<TokT, 1>(W.c[1], bid - W.c[1].blk0, ta, tb, tn, D, singles);
     } else if (bid < W.c[3].blk0) {
-        scan_class<TokT, 2>(W.c[2], bid - W.c[2].blk0, ta, tb, tn, LR, singles);
+        scan_class<TokT, 2>(W.c[2], bid - W.c[2].blk0, ta, tb, tn, D, singles);
     } else if (bid < W.lblk0) {
-        scan_class<TokT, 3>(W.c[3], bid - W.c[3].blk0, ta, tb, tn, LR, singles);
+        scan_class<TokT, 3>(W.c[3], bid - W.c[3].blk0, ta, tb, tn, D, singles);
     } else if (bid < W.lblk0 + W.lnblk) {
         for (unsigned i = (bid - W.lblk0) * blockDim.x + tid; i < W.ln; i += W.lnblk * blockDim.x) {
             const uint32_t len = W.llen[i];
@@ -417,92 +503,137 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
             bool hit = false;
             for (uint32_t k = 0; k + 1 < len && !hit; ++k) hit = (t[k] == ta) & (t[k + 1] == tb);
             if (!hit) continue;
-            const uint32_t j = rewrite_word<TokT>(t, len, ta, tb, tn, W.lcnt[i], LR, false);
+            const uint32_t j = rewrite_word(t, len, ta, tb, tn, W.lcnt[i], D, false);
             W.llen[i] = j;
             singles += (j < 2);
         }
     }
     singles = wave_sum(singles);   // words that became one token (rare: no contention)
     if ((tid & 63) == 0 && singles) atomicAdd(&st->n_single, singles);
+    __syncthreads();
+    for (unsigned k = tid; k < 2 * kLdsLR; k += blockDim.x) {
+        const unsigned long long v = l_lr[k];
+        if (v) atomicAdd(&LR[k], v);
+    }
 }
 
 // ------------------------------------------------------------------ K2: apply deltas
-__global__ void __launch_bounds__(256) k_apply(RoundState* __restrict__ st, PairsDev P, ToksDev K,
-                                               unsigned long long* __restrict__ LR) {
+__global__ void __launch_bounds__(256) k_apply(RoundState* __restrict__ st, PairsDev P,
+                                               unsigned long long* __restrict__ LR,
+                                               unsigned* __restrict__ touched) {
     if (st->halt) return;
     const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
     const unsigned x = g >> 2, op = g & 3;   // op: 0 (x,a)-=L  1 (x,new)+=L  2 (b,x)-=R  3 (new,x)+=R
     const int isnew = st->new_is_new;
     const unsigned ntok = (unsigned)st->ntok + (unsigned)isnew;
     const unsigned a = st->cur_a, b = st->cur_b, nw = st->cur_new;
-    const int round = st->round;
-    if (g == 0) {
-        const unsigned bs = st->cur_slot;  // pop(best_pair)
-        P.cnt[bs] = 0;
-        atomicAnd(&P.flag[bs], ~kPresent);
-        st->new_rank[(round + 1) & 1] = 0;
-        if (isnew) {
-            unsigned s = (unsigned)mix64(K.hash[nw]) & K.map_mask;
-            while (K.map[s] != 0) s = (s + 1) & K.map_mask;
-            K.map[s] = nw + 1;
-        }
-    }
-    if (x >= ntok) return;
-    if (op == 0 && isnew) {
-        const unsigned rnew = st->new_rank[round & 1];
-        if (x == nw) K.rank[x] = rnew;
-        else {
-            const unsigned r = K.rank[x];
-            K.rank[x] = r + (r >= rnew);
-        }
-    }
     unsigned long long* cell = &LR[2 * (size_t)x + (op >> 1)];
-    const long long d = (long long)*cell;
-    if (!d) return;
-    const long long T = st->T;
-    switch (op) {
-        case 0: if (!(x == a && a == b)) pair_dec(P, st, x, a, d); break;   // never the popped key
-        case 1: pair_inc(P, st, x, nw, d, T); break;
-        case 2: if (!(x == b && a == b)) pair_dec(P, st, b, x, d); break;
-        default: pair_inc(P, st, nw, x, d, T); break;
+    const long long d = x < ntok ? (long long)*cell : 0;
+    size_t inc_slot = ~(size_t)0;
+    if (d) {
+        switch (op) {
+            case 0: if (!(x == a && a == b)) pair_dec(P, st, x, a, d); break;   // never the popped key
+            case 1: inc_slot = pair_inc(P, st, x, nw, d); break;
+            case 2: if (!(x == b && a == b)) pair_dec(P, st, b, x, d); break;
+            default: inc_slot = pair_inc(P, st, nw, x, d); break;
+        }
+        if (op & 1) *cell = 0;   // both lanes of this cell read it in the same load instruction
     }
-    if (op & 1) *cell = 0;   // both lanes of this cell read it in the same load instruction
+    const bool t = inc_slot != ~(size_t)0;
+    const unsigned idx = wave_append(t, &st->n_touched);
+    if (t) touched[idx] = (unsigned)inc_slot;
 }
 
 // ------------------------------------------------------------------ K3: argmax over C
-__global__ void __launch_bounds__(256) k_argmax(RoundState* __restrict__ st, PairsDev P,
-                                                const uint32_t* __restrict__ rank,
+// With advance=1 it also finishes the round: the new token's lexicographic rank is folded in
+// (ranks are double-buffered by round parity: read rank[r&1] corrected on the fly, write
+// rank[(r+1)&1]), the token enters the dedupe map, and round/ntok step forward.
+__global__ void __launch_bounds__(256) k_argmax(RoundState* __restrict__ st, PairsDev P, ToksDev K,
+                                                uint32_t* __restrict__ rank2, unsigned rank_stride,
+                                                const unsigned* __restrict__ touched,
                                                 Partial* __restrict__ part, int advance) {
     __shared__ long long sc[4];
     __shared__ unsigned long long stb[4];
     __shared__ unsigned ss[4];
+    __shared__ unsigned long long skey[4];
     if (st->halt) return;
-    const unsigned nC = st->nC;
+    const unsigned nC = advance ? st->nC_base : st->nC;
+    const int round = st->round;
+    const unsigned* rank = rank2 + (size_t)(round & 1) * rank_stride;
+    const bool fold = advance && st->new_is_new;
+    const unsigned nw = st->cur_new, rnew = st->new_rank[round & 1];
+    auto rk = [&](unsigned t) -> unsigned {
+        if (!fold) return rank[t];
+        if (t == nw) return rnew;
+        const unsigned r = rank[t];
+        return r + (r >= rnew);
+    };
+    if (advance) {
+        const unsigned ntok = (unsigned)st->ntok + (fold ? 1u : 0u);
+        uint32_t* out = rank2 + (size_t)((round + 1) & 1) * rank_stride;
+        for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < ntok; t += gridDim.x * blockDim.x)
+            out[t] = rk(t);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->new_rank[(round + 1) & 1] = 0;
+            if (fold) {
+                unsigned s = (unsigned)mix64(K.hash[nw]) & K.map_mask;
+                while (K.map[s] != 0) s = (s + 1) & K.map_mask;
+                K.map[s] = nw + 1;
+            }
+        }
+    }
     long long bc = LLONG_MIN;
-    unsigned long long bt = 0;
+    unsigned long long bt = 0, bk = 0;
     unsigned bs = 0;
+    // keys incremented this round: admitted to C by their final count (identical on every
+    // rank); they are also candidates of this very argmax
+    const unsigned nt = advance ? st->n_touched : 0u;
+    const long long T = st->T;
+    for (unsigned i0 = blockIdx.x * blockDim.x; i0 < nt; i0 += gridDim.x * blockDim.x) {
+        const unsigned i = i0 + threadIdx.x;
+        bool add = false;
+        unsigned s = 0;
+        if (i < nt) {
+            s = touched[i];
+            const unsigned f = P.flag[s];
+            const long long c = P.cnt[s];
+            if ((f & kPresent) && c >= T) {
+                const unsigned long long key = P.key[s] - 1ULL;
+                const unsigned long long tb =
+                    ((unsigned long long)rk((unsigned)(key >> 32)) << 32) | rk((unsigned)(key & 0xffffffffu));
+                if (cand_better(c, tb, bc, bt)) { bc = c; bt = tb; bs = s; bk = key; }
+                if (!(f & kInC)) add = !(atomicOr(&P.flag[s], kInC) & kInC);
+            }
+        }
+        const unsigned idx = wave_append(add, &st->nC);
+        if (add) {
+            if (idx < st->capC) P.C[idx] = s;
+            else atomicOr(&st->err, ERR_C_FULL);
+        }
+    }
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < nC; i += gridDim.x * blockDim.x) {
         const unsigned s = P.C[i];
         if (!(P.flag[s] & kPresent)) continue;
         const long long c = P.cnt[s];
         const unsigned long long key = P.key[s] - 1ULL;
         const unsigned long long tb =
-            ((unsigned long long)rank[key >> 32] << 32) | rank[key & 0xffffffffu];
-        if (cand_better(c, tb, bc, bt)) { bc = c; bt = tb; bs = s; }
+            ((unsigned long long)rk((unsigned)(key >> 32)) << 32) | rk((unsigned)(key & 0xffffffffu));
+        if (cand_better(c, tb, bc, bt)) { bc = c; bt = tb; bs = s; bk = key; }
     }
     for (int o = 32; o > 0; o >>= 1) {
         const long long oc = __shfl_xor(bc, o);
         const unsigned long long ot = __shfl_xor(bt, o);
         const unsigned os = __shfl_xor(bs, o);
-        if (cand_better(oc, ot, bc, bt)) { bc = oc; bt = ot; bs = os; }
+        const unsigned long long ok = __shfl_xor(bk, o);
+        if (cand_better(oc, ot, bc, bt)) { bc = oc; bt = ot; bs = os; bk = ok; }
     }
     const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { sc[w] = bc; stb[w] = bt; ss[w] = bs; }
+    if ((threadIdx.x & 63) == 0) { sc[w] = bc; stb[w] = bt; ss[w] = bs; skey[w] = bk; }
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
-            if (cand_better(sc[k], stb[k], bc, bt)) { bc = sc[k]; bt = stb[k]; bs = ss[k]; }
-        part[blockIdx.x] = Partial{bc, bt, bs, 0};
+            if (cand_better(sc[k], stb[k], bc, bt)) { bc = sc[k]; bt = stb[k]; bs = ss[k]; bk = skey[k]; }
+        part[blockIdx.x] = Partial{bc, bt, bs, (unsigned)(bk >> 32), (unsigned)(bk & 0xffffffffu), 0};
         if (advance && blockIdx.x == 0) {
             st->round += 1;
             st->ntok += st->new_is_new;
@@ -688,6 +819,67 @@ __global__ void k_move(WordsDev<TokT> W, unsigned total, WordsDev<TokT> D, MoveC
     }
 }
 
+// ------------------------------------------------------------------ posting index build
+template <class TokT>
+__device__ __forceinline__ const TokT* slot_of(const WordsDev<TokT>& W, unsigned f, uint32_t* len) {
+    int c = 0;
+    while (c + 1 < kNumCls && f >= W.off[c + 1]) ++c;
+    const TokT* s = W.c[c].slot + (size_t)(f - W.off[c]) * slot_w(c);
+    *len = s[0];
+    return s + 1;
+}
+
+template <class TokT>
+__global__ void k_index_count(WordsDev<TokT> W, unsigned n, uint32_t* __restrict__ cnt) {
+    const unsigned f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= n) return;
+    uint32_t len;
+    const TokT* t = slot_of(W, f, &len);
+    uint32_t d = 0;
+    if (len >= 2)
+        for (uint32_t k = 0; k < len; ++k) {
+            bool first = true;
+            for (uint32_t q = 0; q < k && first; ++q) first = t[q] != t[k];
+            d += first;
+        }
+    cnt[f] = d;
+}
+
+template <class TokT>
+__global__ void k_index_emit(WordsDev<TokT> W, unsigned n, const uint32_t* __restrict__ pos,
+                             uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const unsigned f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= n) return;
+    uint32_t len;
+    const TokT* t = slot_of(W, f, &len);
+    if (len < 2) return;
+    uint32_t o = pos[f];
+    for (uint32_t k = 0; k < len; ++k) {
+        bool first = true;
+        for (uint32_t q = 0; q < k && first; ++q) first = t[q] != t[k];
+        if (first) { keys[o] = t[k]; vals[o] = f; ++o; }
+    }
+}
+
+__global__ void k_index_bounds(const uint32_t* __restrict__ keys, unsigned long long e,
+                               uint32_t* __restrict__ beg, uint32_t* __restrict__ len) {
+    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= e) return;
+    const uint32_t k = keys[i];
+    if (i == 0 || keys[i - 1] != k) beg[k] = (uint32_t)i;
+    if (i + 1 == e || keys[i + 1] != k) len[k] = (uint32_t)(i + 1);   // end; beg subtracted below
+}
+
+__global__ void k_index_lens(const uint32_t* __restrict__ beg, uint32_t* __restrict__ len, unsigned ntok) {
+    const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < ntok && len[t]) len[t] -= beg[t];
+}
+
+__global__ void k_anc_init(uint32_t* __restrict__ anc, unsigned ntok) {
+    const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < ntok) anc[t] = t;
+}
+
 // ------------------------------------------------------------------ rebuild helpers
 struct RebuildStats {
     unsigned long long bins[64];
@@ -818,6 +1010,7 @@ class MergeLoop {
     void exhaustion();
     void compact();
     void layout_blocks();
+    void build_index();
     PairsDev pairs() const { return PairsDev{pkey_.p, pcnt_.p, pflag_.p, pcap_ - 1, C_.p}; }
     ToksDev toks() const {
         return ToksDev{pool_.p, toff_.p, tlen_.p, thash_.p, tpw_.p, tkey8_.p, trank_.p, tmap_.p,
@@ -837,7 +1030,7 @@ class MergeLoop {
     HostWords<TokT> words_;
     WordsDev<TokT> wdev_{};
     unsigned merge_grid_ = 1;
-    double scan_bytes_ = 0;
+    double scan_bytes_ = 0, long_bytes_ = 0;
     unsigned long long long_tokens_ = 0;
     unsigned n_live_ = 0;
     DevBuf<unsigned long long> hist_;
@@ -853,8 +1046,13 @@ class MergeLoop {
     DevBuf<unsigned long long> thash_, tpw_, tkey8_;
     DevBuf<unsigned long long> LR_;
     DevBuf<Partial> part_;
-    DevBuf<uint32_t> m_a_, m_b_, m_new_;
+    DevBuf<uint32_t> m_a_, m_b_, m_new_, m_mode_;
     DevBuf<RebuildStats> rs_;
+    // posting index
+    DevBuf<uint32_t> ilist_, ibeg_, ilen_, ianc_;
+    IndexDev idev_{};
+    int next_index_round_ = 256;
+    DevBuf<unsigned> touched_;
 };
 
 template <class TokT>
@@ -960,28 +1158,89 @@ void MergeLoop<TokT>::compact() {
     layout_blocks();
 }
 
+// Posting lists token -> words over the current slot table (long words are always scanned).
+template <class TokT>
+void MergeLoop<TokT>::build_index() {
+    const unsigned n = wdev_.off[kNumCls];
+    const unsigned tcap = 256u + (unsigned)n_rounds_ + 1u;
+    if (!ianc_.p) {
+        ianc_.alloc(tcap);
+        ibeg_.alloc(tcap);
+        ilen_.alloc(tcap);
+    }
+    BPE_HIP(hipMemsetAsync(ibeg_.p, 0, ibeg_.bytes(), s_));
+    BPE_HIP(hipMemsetAsync(ilen_.p, 0, ilen_.bytes(), s_));
+    unsigned long long E = 0;
+    DevBuf<uint32_t> cnt(std::max(n, 1u)), pos(std::max(n, 1u));
+    if (n) {
+        hipLaunchKernelGGL(k_index_count<TokT>, dim3(ceil_div(n, 256)), dim3(256), 0, s_, wdev_, n, cnt.p);
+        size_t tb = 0;
+        BPE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt.p, pos.p, (int)n, s_));
+        DevBuf<uint8_t> tmp(tb);
+        BPE_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, cnt.p, pos.p, (int)n, s_));
+        uint32_t last[2];
+        BPE_HIP(hipMemcpyAsync(&last[0], pos.p + n - 1, 4, hipMemcpyDeviceToHost, s_));
+        BPE_HIP(hipMemcpyAsync(&last[1], cnt.p + n - 1, 4, hipMemcpyDeviceToHost, s_));
+        BPE_HIP(hipStreamSynchronize(s_));
+        E = (unsigned long long)last[0] + last[1];
+    }
+    DevBuf<uint32_t> keys(std::max<unsigned long long>(E, 1)), vals(std::max<unsigned long long>(E, 1));
+    DevBuf<uint32_t> keys2(std::max<unsigned long long>(E, 1));
+    ilist_.alloc(std::max<unsigned long long>(E, 1));
+    if (E) {
+        hipLaunchKernelGGL(k_index_emit<TokT>, dim3(ceil_div(n, 256)), dim3(256), 0, s_, wdev_, n, pos.p,
+                           keys.p, vals.p);
+        int bits = 1;
+        while ((1u << bits) < tcap) ++bits;
+        size_t tb = 0;
+        BPE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys.p, keys2.p, vals.p, ilist_.p,
+                                                   (int)E, 0, bits, s_));
+        DevBuf<uint8_t> tmp(tb);
+        BPE_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, keys.p, keys2.p, vals.p, ilist_.p,
+                                                   (int)E, 0, bits, s_));
+        hipLaunchKernelGGL(k_index_bounds, dim3(ceil_div(E, 256)), dim3(256), 0, s_, keys2.p, E,
+                           ibeg_.p, ilen_.p);
+        hipLaunchKernelGGL(k_index_lens, dim3(ceil_div(tcap, 256)), dim3(256), 0, s_, ibeg_.p, ilen_.p, tcap);
+    }
+    hipLaunchKernelGGL(k_anc_init, dim3(ceil_div(tcap, 256)), dim3(256), 0, s_, ianc_.p,
+                       (unsigned)std::max(hs_.ntok, 256));
+    BPE_HIP(hipGetLastError());
+    BPE_HIP(hipStreamSynchronize(s_));
+    idev_ = IndexDev{ilist_.p, ibeg_.p, ilen_.p, ianc_.p, n / 6, n};
+    out_.stats.n_index_builds++;
+}
+
 // blocks of k_merge per slot class: enough waves to cover each class with a few words per
 // thread in flight, block-uniform class so the scan has no per-lane class branch
 template <class TokT>
 void MergeLoop<TokT>::layout_blocks() {
     WordsDev<TokT> W = words_.dev();
+    W.off[0] = 0;
+    for (int c = 0; c < kNumCls; ++c) W.off[c + 1] = W.off[c] + W.c[c].n;
+    // about one resident generation of workgroups (4 per CU): each block's prologue is a
+    // chain of dependent loads, so a second generation would pay it again
+    constexpr unsigned kGridBudget = 1024;
+    double total_b = 0;
+    for (int c = 0; c < kNumCls; ++c) total_b += (double)W.c[c].n * slot_w(c);
     unsigned blk = 0;
     for (int c = 0; c < kNumCls; ++c) {
         const unsigned per_thread = c == 0 ? 4 : (c == 1 ? 2 : 1);
         const unsigned need = ceil_div(W.c[c].n, 256u * per_thread);
+        const unsigned share = total_b > 0 ? (unsigned)(kGridBudget * (W.c[c].n * (double)slot_w(c)) / total_b) : 0;
         W.c[c].blk0 = blk;
-        W.c[c].nblk = std::min(need, 2048u);
+        W.c[c].nblk = W.c[c].n ? std::max(1u, std::min(need, share)) : 0;
         blk += W.c[c].nblk;
     }
     W.lblk0 = blk;
-    W.lnblk = std::min(ceil_div(W.ln, 256u), 256u);
+    W.lnblk = std::min(ceil_div(W.ln, 256u), 64u);
     blk += W.lnblk;
     merge_grid_ = std::max(blk, 1u);
     wdev_ = W;
     // algorithmic bytes of one k_merge launch: every slot, and every long word's ids + length
     scan_bytes_ = 0;
     for (int c = 0; c < kNumCls; ++c) scan_bytes_ += (double)W.c[c].n * slot_w(c) * sizeof(TokT);
-    scan_bytes_ += (double)W.ln * 4 + (double)long_tokens_ * sizeof(TokT);
+    long_bytes_ = (double)W.ln * 4 + (double)long_tokens_ * sizeof(TokT);
+    scan_bytes_ += long_bytes_;
 }
 
 template <class TokT>
@@ -1070,8 +1329,8 @@ int MergeLoop<TokT>::rebuild() {
     hs_.halt = HALT_NONE;
     push_state();
     hipLaunchKernelGGL(k_build_C, dim3(grid), dim3(256), 0, s_, pairs(), pcap_, T, st_.p);
-    hipLaunchKernelGGL(k_argmax, dim3(kArgBlocks), dim3(256), 0, s_, st_.p, pairs(), trank_.p,
-                       part_.p, 0);
+    hipLaunchKernelGGL(k_argmax, dim3(kArgBlocks), dim3(256), 0, s_, st_.p, pairs(), toks(), trank_.p,
+                       tok_cap_, touched_.p, part_.p, 0);
     BPE_HIP(hipGetLastError());
     pull_state();
     BPE_REQUIRE(!(hs_.err & ERR_C_FULL), BPE_E_NOMEM, "candidate list overflow");
@@ -1089,18 +1348,29 @@ void MergeLoop<TokT>::run() {
     part_.alloc(kArgBlocks);
     tok_cap_ = 256u + (unsigned)n_rounds_ + 1u;
     LR_.alloc(2ull * tok_cap_);
+    touched_.alloc(2ull * tok_cap_);
     BPE_HIP(hipMemsetAsync(LR_.p, 0, LR_.bytes(), s_));
-    m_a_.alloc(n_rounds_); m_b_.alloc(n_rounds_); m_new_.alloc(n_rounds_);
-    toff_.alloc(tok_cap_); tlen_.alloc(tok_cap_); trank_.alloc(tok_cap_);
+    m_a_.alloc(n_rounds_); m_b_.alloc(n_rounds_); m_new_.alloc(n_rounds_); m_mode_.alloc(n_rounds_);
+    toff_.alloc(tok_cap_); tlen_.alloc(tok_cap_); trank_.alloc(2ull * tok_cap_);  // 2 rank buffers
     thash_.alloc(tok_cap_); tpw_.alloc(tok_cap_); tkey8_.alloc(tok_cap_);
     tmap_.alloc(next_pow2(4ull * tok_cap_));
     BPE_HIP(hipMemsetAsync(tmap_.p, 0, tmap_.bytes(), s_));
     const unsigned pool_cap = std::max(1u << 16, 64u * std::max(max_len_, 8u));
     pool_.alloc(pool_cap);
 
-    // global initial pair histogram (train.py:35-49): one all-reduce when sharded
-    if (comm_ && comm_->nranks > 1)
+    // global initial pair histogram (train.py:35-49): one all-reduce when sharded; plus the
+    // longest word over all ranks (a merged token can be as long as any rank's longest word)
+    if (comm_ && comm_->nranks > 1) {
         comm_->allreduce_i64(reinterpret_cast<int64_t*>(hist_.p), 65536, s_);
+        std::vector<int64_t> ml(comm_->nranks, 0);
+        ml[comm_->rank] = max_len_;
+        DevBuf<int64_t> d_ml(ml.size());
+        BPE_HIP(hipMemcpyAsync(d_ml.p, ml.data(), ml.size() * 8, hipMemcpyHostToDevice, s_));
+        comm_->allreduce_i64(d_ml.p, ml.size(), s_);
+        BPE_HIP(hipMemcpyAsync(ml.data(), d_ml.p, ml.size() * 8, hipMemcpyDeviceToHost, s_));
+        BPE_HIP(hipStreamSynchronize(s_));
+        for (int64_t v : ml) max_len_ = std::max<unsigned>(max_len_, (unsigned)v);
+    }
     alloc_pairs(size_t(1) << 22);
     const unsigned n_single_keep = hs_.n_single;
     memset(&hs_, 0, sizeof(hs_));
@@ -1116,10 +1386,12 @@ void MergeLoop<TokT>::run() {
     hipLaunchKernelGGL(k_init_pairs, dim3(256), dim3(256), 0, s_, hist_.p, pairs(), st_.p);
     BPE_HIP(hipGetLastError());
     pull_state();
+    build_index();
     hs_.halt = HALT_REBUILD;
 
     const bool timing = timing_enabled();
     std::vector<hipEvent_t> ev;
+    std::vector<uint32_t> hmode;
     if (timing) {
         ev.resize(2 * kBatch);
         for (auto& e : ev) BPE_HIP(hipEventCreate(&e));
@@ -1149,28 +1421,39 @@ void MergeLoop<TokT>::run() {
         const long long start_round = hs_.round;
         for (int k = 0; k < R; ++k) {
             if (timing) BPE_HIP(hipEventRecord(ev[2 * k], s_));
+            // rewrite -> [one all-reduce of the delta cells when sharded] -> apply -> argmax.
+            // (k_merge<.., true> applies the deltas inside the merge kernel instead; measured
+            // slower: each hit's pair updates serialize on one thread)
             hipLaunchKernelGGL(k_merge<TokT>, dim3(merge_grid_), dim3(256), 0, s_, st_.p, part_.p,
-                               kArgBlocks, pairs(), toks(), wdev_, LR_.p, m_a_.p, m_b_.p, m_new_.p);
+                               kArgBlocks, pairs(), toks(), wdev_, idev_, LR_.p, m_a_.p, m_b_.p,
+                               m_new_.p, m_mode_.p);
             if (timing) BPE_HIP(hipEventRecord(ev[2 * k + 1], s_));
-            if (sharded) {
+            if (sharded) {   // the one collective per merge round
                 const size_t ntok_bound = 256 + (size_t)start_round + k + 1;
                 comm_->allreduce_i64(reinterpret_cast<int64_t*>(LR_.p), 2 * ntok_bound, s_);
             }
             const unsigned ntb = 256u + (unsigned)start_round + (unsigned)k + 1u;
             hipLaunchKernelGGL(k_apply, dim3(ceil_div(4ull * ntb, 256)), dim3(256), 0, s_, st_.p,
-                               pairs(), toks(), LR_.p);
-            hipLaunchKernelGGL(k_argmax, dim3(kArgBlocks), dim3(256), 0, s_, st_.p, pairs(),
-                               trank_.p, part_.p, 1);
+                               pairs(), LR_.p, touched_.p);
+            hipLaunchKernelGGL(k_argmax, dim3(kArgBlocks), dim3(256), 0, s_, st_.p, pairs(), toks(),
+                               trank_.p, tok_cap_, touched_.p, part_.p, 1);
         }
         BPE_HIP(hipGetLastError());
         pull_state();
         if (timing) {
             const int done = (int)(hs_.round - start_round);
+            hmode.resize(std::max(done, 1));
+            if (done)
+                BPE_HIP(hipMemcpy(hmode.data(), m_mode_.p + start_round, done * 4ull, hipMemcpyDeviceToHost));
+            const double slot_avg = scan_bytes_ / std::max(1u, idev_.n_slot_words + words_.ln);
             for (int k = 0; k < std::min(done, R); ++k) {
                 float t = 0;
                 BPE_HIP(hipEventElapsedTime(&t, ev[2 * k], ev[2 * k + 1]));
                 k1_ms += t;
-                k1_bytes += scan_bytes_;
+                // algorithmic bytes: every slot on a full scan; list entries + their slots
+                // (at the table's mean slot size) plus the long words in index mode
+                k1_bytes += hmode[k] == 0xffffffffu ? scan_bytes_
+                                                    : hmode[k] * (4.0 + slot_avg) + long_bytes_;
                 ++k1_launches;
             }
         }
@@ -1178,9 +1461,13 @@ void MergeLoop<TokT>::run() {
         BPE_REQUIRE(!(hs_.err & ERR_C_FULL), BPE_E_NOMEM, "candidate list overflow");
         BPE_REQUIRE(!(hs_.err & ERR_POOL), BPE_E_NOMEM, "token pool overflow");
         if (hs_.halt == HALT_DONE) break;
-        if (hs_.n_single > n_live_ / 4 + 1024) {
+        // compaction (drop finished words, narrower slots) + fresh posting lists: when many
+        // words finished, and on a geometric schedule so later tokens get lists of their own
+        if (hs_.n_single > n_live_ / 4 + 1024 || hs_.round >= next_index_round_) {
             compact();
+            build_index();
             push_state();
+            next_index_round_ = std::max(hs_.round + 512, (int)(hs_.round * 2.5));
         }
     }
     for (auto& e : ev) (void)hipEventDestroy(e);
