@@ -40,6 +40,7 @@
 #include <algorithm>
 #include <chrono>
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <set>
@@ -65,7 +66,8 @@ struct RoundState {
     int ntok;
     long long T;
     unsigned nC, capC, c_limit, n_touched;
-    unsigned nC_base, pad1;     // |C| before this round's k_argmax appends (set by k_merge)
+    unsigned nC_base;           // |C| before this round's k_argmax appends (set by k_merge)
+    unsigned k3_done;           // k_argmax blocks finished this launch (the last one advances)
     unsigned cur_a, cur_b, cur_new, cur_slot;
     long long cur_cnt;
     int new_is_new;
@@ -634,9 +636,16 @@ __global__ void __launch_bounds__(256) k_argmax(RoundState* __restrict__ st, Pai
         for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
             if (cand_better(sc[k], stb[k], bc, bt)) { bc = sc[k]; bt = stb[k]; bs = ss[k]; bk = skey[k]; }
         part[blockIdx.x] = Partial{bc, bt, bs, (unsigned)(bk >> 32), (unsigned)(bk & 0xffffffffu), 0};
-        if (advance && blockIdx.x == 0) {
-            st->round += 1;
-            st->ntok += st->new_is_new;
+        // Advance the round only once every block has read round/ntok/new_rank: the last
+        // block to finish does it.  (Advancing from block 0 raced with blocks that had not
+        // started yet -- they then read the other rank buffer's parity.)
+        if (advance) {
+            __threadfence();
+            if (atomicAdd(&st->k3_done, 1u) == gridDim.x - 1) {
+                st->k3_done = 0;
+                st->round += 1;
+                st->ntok += st->new_is_new;
+            }
         }
     }
 }
@@ -1400,7 +1409,12 @@ void MergeLoop<TokT>::run() {
     long long k1_launches = 0;
     const bool sharded = comm_ && comm_->nranks > 1;
 
+    const bool trace = std::getenv("BPE355_TRACE") != nullptr;
+    const int rank = comm_ ? comm_->rank : 0;
     for (;;) {
+        if (trace)
+            std::fprintf(stderr, "[bpe355 r%d] round %d halt %d nC %u T %lld pairs %llu err %u\n", rank,
+                         hs_.round, hs_.halt, hs_.nC, hs_.T, hs_.pair_used, hs_.err);
         if (hs_.round >= n_rounds_) break;
         if (hs_.halt == HALT_REBUILD) {
             const int r = rebuild();
