@@ -130,7 +130,10 @@ def main():
     k_count_bytes = sum(s["count_kernel_bytes"] for s in stats)
     roofline = None
     if k_merge_ms > 0 or k_count_ms > 0:
-        if k_merge_ms >= k_count_ms:
+        # k_merge is event-timed on a 1-in-8 sample of its launches: compare per-step estimates
+        merge_step_ms = k_merge_ms / max(1, k_merge_launch) * rounds
+        count_step_ms = k_count_ms / len(stats)
+        if merge_step_ms >= count_step_ms:
             kname, kms, kb, kl = "k_merge", k_merge_ms, k_merge_bytes, k_merge_launch
         else:
             kname, kms, kb, kl = "k_count_words", k_count_ms, k_count_bytes, len(stats)
@@ -141,7 +144,9 @@ def main():
             traffic = json.loads(tf.read_text()).get(kname)
         roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": kname, "launches_per_step": kl / len(stats),
+                    "kernel": kname,
+                    "launches_per_step": rounds if kname == "k_merge" else 1,
+                    "timed_launches": kl,
                     "avg_launch_us": round(kms / kl * 1e3, 3),
                     "bytes_per_launch": kb / kl}
 

@@ -20,21 +20,22 @@
 //   Words that shrink to one id drop out, and words migrate to narrower slots, at compaction.
 //
 // Per round, three kernels on one HIP stream (host checks state once per batch of rounds):
-//   K1 k_merge  : every workgroup reduces K3's per-block partials to the round's best pair,
-//                 resolves the new token id (hash map over token bytes) and counts its
-//                 lexicographic rank over a slice of the tokens; block 0 records the merge.
+//   K1 k_merge  : every workgroup reduces K3's per-block partials to the round's best pair and
+//                 resolves the new token id (hash map over token bytes); block 0 records the merge.
 //                 Then all workgroups rewrite the words containing (a, b) and accumulate, per
 //                 neighbour token, the deltas L[x] (left) and R[y] (right) as int64.
 //   [one all-reduce of L/R over ranks when the corpus is sharded]
 //   K2 k_apply  : 4 threads per token: (x,a)-=L[x], (x,new)+=L[x], (b,y)-=R[y], (new,y)+=R[y]
 //                 on the pair hash table; touched keys become present; increments that lift a
 //                 key across the threshold T append it to the candidate list C.
-//   K3 k_argmax : argmax over C of (count, rank(a), rank(b)) -> per-block partials.
+//   K3 k_argmax : argmax over C of (count, bytes a, bytes b) -> per-block partials; bytes
+//                 compare by 8-byte big-endian prefix, the pool only on equal prefixes.
 // Every key with count >= T is in C, so max(C) is the global max whenever it is >= T;
 // otherwise (or when C has bloated) the host rebuilds C with a fresh T.  Zero-count keys that
 // are still present are the reference's leftover dict keys; once no positive count remains
 // (every word is one token) the reference pops them in descending byte order, which the host
 // reproduces.
+#include <hip/hip_ext.h>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -71,7 +72,6 @@ struct RoundState {
     unsigned cur_a, cur_b, cur_new, cur_slot;
     long long cur_cnt;
     int new_is_new;
-    unsigned new_rank[2];
     unsigned err;
     unsigned n_single;
     unsigned pool_used, pool_cap;
@@ -81,7 +81,7 @@ struct RoundState {
 
 struct Partial {
     long long cnt;
-    unsigned long long tb;   // (rank a << 32) | rank b
+    unsigned long long ka, kb;   // key8 of a and of b (first 8 bytes, big-endian)
     unsigned slot, a, b, pad;
 };
 
@@ -100,7 +100,6 @@ struct ToksDev {
     unsigned long long* hash;  // polynomial hash of the bytes
     unsigned long long* pw;    // P^len
     unsigned long long* key8;  // first 8 bytes, big-endian, zero padded
-    uint32_t* rank;            // lexicographic rank among live tokens
     uint32_t* map;             // hash -> id + 1
     uint32_t map_mask;
 };
@@ -130,24 +129,64 @@ struct WordsDev {
 
 // Posting index over the slot words, rebuilt at every compaction: list[beg[t], beg[t]+len[t])
 // holds the flat index of every word that contained token t at build time.  A token created
-// later inherits anc = the smaller covering list of its two parts (a word that contains it
-// contained both parts when it was formed); a token re-created through token dedupe (its
-// bytes reached by another split) is marked uncovered (kNoAnc) until the next build.
+// later gets (beg, len) of the smaller covering list of its two parts (a word that contains it
+// contained both parts when it was formed) -- stored per token, so the merge kernel finds its
+// list in one dependent load; a token re-created through token dedupe (its bytes reached by
+// another split) is marked uncovered (len = kNoAnc) until the next build.
 constexpr unsigned kNoAnc = 0xffffffffu;
 struct IndexDev {
     const uint32_t* list;
-    const uint32_t* beg;
-    const uint32_t* len;
-    uint32_t* anc;
+    uint32_t* beg;
+    uint32_t* len;
     unsigned full_threshold;   // lists longer than this are cheaper to replace by a full scan
     unsigned n_slot_words;
 };
 
 template <class TokT> __host__ __device__ constexpr TokT sentinel() { return (TokT)~(TokT)0; }
 
-__device__ __forceinline__ bool cand_better(long long c1, unsigned long long t1, long long c2,
-                                            unsigned long long t2) {
-    return c1 > c2 || (c1 == c2 && t1 > t2);
+// bytes(x) vs bytes(y) for tokens whose 8-byte prefixes are equal: -1 / 0 / +1
+__device__ __noinline__ int cmp_tok_tail(const uint8_t* __restrict__ pool, const uint32_t* __restrict__ off,
+                                         const uint32_t* __restrict__ len, unsigned x, unsigned y) {
+    const unsigned lx = len[x], ly = len[y], m = lx < ly ? lx : ly;
+    const uint8_t* px = pool + off[x];
+    const uint8_t* py = pool + off[y];
+    for (unsigned i = 8; i < m; ++i)
+        if (px[i] != py[i]) return px[i] < py[i] ? -1 : 1;
+    return lx < ly ? -1 : (lx > ly ? 1 : 0);
+}
+
+// The reference's max key (count, bytes a, bytes b) (train.py:187-189).  Byte strings compare
+// by their zero-padded big-endian 8-byte prefix first: a smaller prefix means smaller bytes;
+// only equal prefixes of different tokens need the bytes themselves (rare: long tokens, or a
+// prefix relation like "ab" vs "ab\0").
+struct Cand {
+    long long cnt;
+    unsigned long long ka, kb;
+    unsigned slot, a, b;
+};
+__device__ __forceinline__ bool cand_better(const Cand& x, const Cand& y, const uint8_t* pool,
+                                            const uint32_t* off, const uint32_t* len) {
+    if (x.cnt != y.cnt) return x.cnt > y.cnt;
+    if (x.a != y.a) {
+        if (x.ka != y.ka) return x.ka > y.ka;
+        return cmp_tok_tail(pool, off, len, x.a, y.a) > 0;
+    }
+    if (x.b != y.b) {
+        if (x.kb != y.kb) return x.kb > y.kb;
+        return cmp_tok_tail(pool, off, len, x.b, y.b) > 0;
+    }
+    return false;
+}
+__device__ __forceinline__ Cand cand_none() { return Cand{LLONG_MIN, 0, 0, 0, 0, 0}; }
+__device__ __forceinline__ Cand shfl_xor_cand(const Cand& c, int o) {
+    Cand r;
+    r.cnt = __shfl_xor(c.cnt, o);
+    r.ka = __shfl_xor(c.ka, o);
+    r.kb = __shfl_xor(c.kb, o);
+    r.slot = __shfl_xor(c.slot, o);
+    r.a = __shfl_xor(c.a, o);
+    r.b = __shfl_xor(c.b, o);
+    return r;
 }
 
 
@@ -214,21 +253,6 @@ __device__ __forceinline__ unsigned long long concat_key8(const ToksDev& K, unsi
 __device__ __forceinline__ uint8_t concat_byte(const ToksDev& K, unsigned a, unsigned la,
                                                unsigned b, unsigned i) {
     return i < la ? K.pool[K.off[a] + i] : K.pool[K.off[b] + (i - la)];
-}
-
-// -1 / 0 / +1: bytes(x) vs bytes(a) + bytes(b)
-__device__ int cmp_with_concat(const ToksDev& K, unsigned x, unsigned a, unsigned b,
-                               unsigned long long k8new) {
-    const unsigned long long kx = K.key8[x];
-    if (kx != k8new) return kx < k8new ? -1 : 1;
-    const unsigned lx = K.len[x], la = K.len[a], ln = la + K.len[b];
-    const unsigned m = lx < ln ? lx : ln;
-    const uint8_t* px = K.pool + K.off[x];
-    for (unsigned i = 8; i < m; ++i) {
-        const uint8_t bx = px[i], bn = concat_byte(K, a, la, b, i);
-        if (bx != bn) return bx < bn ? -1 : 1;
-    }
-    return lx < ln ? -1 : (lx > ln ? 1 : 0);
 }
 
 __device__ bool equals_concat(const ToksDev& K, unsigned x, unsigned a, unsigned b) {
@@ -328,6 +352,7 @@ __device__ __forceinline__ void merge_one(const SlotCls<TokT>& S, unsigned i, To
     uint4 r[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) r[v] = reinterpret_cast<const uint4*>(S.slot + (size_t)i * W)[v];
+    const unsigned long long c = S.cnt[i];   // issued with the slot: no extra dependent load on a hit
     TokT e[W];
     __builtin_memcpy(e, r, sizeof(e));
     bool hit = false;
@@ -335,7 +360,7 @@ __device__ __forceinline__ void merge_one(const SlotCls<TokT>& S, unsigned i, To
     for (int k = 1; k + 1 < W; ++k) hit |= (e[k] == a) & (e[k + 1] == b);
     if (hit) {
         TokT* s = S.slot + (size_t)i * W;
-        const uint32_t j = rewrite_word(s + 1, e[0], a, b, nw, S.cnt[i], D, true);
+        const uint32_t j = rewrite_word(s + 1, e[0], a, b, nw, c, D, true);
         s[0] = (TokT)j;
         singles += (j < 2);
     }
@@ -348,7 +373,7 @@ struct BestShared {
     long long cnt;
     unsigned long long hash, k8;
     int round, ntok;
-    unsigned list_beg, list_len, use_list, anc_new;
+    unsigned list_beg, list_len, use_list, cov_beg, cov_len;
 };
 
 template <class TokT>
@@ -370,13 +395,14 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
         const int n_rounds = st->n_rounds;
         const unsigned nC = st->nC, c_limit = st->c_limit;   // only k_argmax appends to C
         const long long T = st->T;
-        Partial pp{LLONG_MIN, 0, 0, 0, 0, 0};
-        if (tid < nparts) pp = part[tid];
+        Cand pp = cand_none();
+        if (tid < nparts) {
+            const Partial q = part[tid];
+            pp = Cand{q.cnt, q.ka, q.kb, q.slot, q.a, q.b};
+        }
         for (int o = 32; o > 0; o >>= 1) {
-            const long long oc = __shfl_xor(pp.cnt, o);
-            const unsigned long long ot = __shfl_xor(pp.tb, o);
-            const unsigned os = __shfl_xor(pp.slot, o), oa = __shfl_xor(pp.a, o), ob = __shfl_xor(pp.b, o);
-            if (cand_better(oc, ot, pp.cnt, pp.tb)) { pp.cnt = oc; pp.tb = ot; pp.slot = os; pp.a = oa; pp.b = ob; }
+            const Cand oc = shfl_xor_cand(pp, o);
+            if (cand_better(oc, pp, K.pool, K.off, K.len)) pp = oc;
         }
         int stop = HALT_NONE;
         if (halt) stop = -1;
@@ -390,15 +416,14 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
                 // level 1: everything keyed by a or b
                 const unsigned long long ha = K.hash[a], pb = K.pw[b], hb = K.hash[b];
                 const unsigned la = K.len[a], lb = K.len[b];
-                const unsigned long long ka = K.key8[a], kb = K.key8[b];
-                const unsigned ua = X.anc[a], ub = X.anc[b];
+                const unsigned long long ka = pp.ka, kb = pp.kb;
+                const unsigned za = X.len[a], zb = X.len[b];   // kNoAnc (uncovered) sorts last
+                const unsigned ba = X.beg[a], bbg = X.beg[b];
                 const unsigned long long h = ha * pb + hb;
                 const unsigned ln = la + lb;
-                // level 2: first map slot, posting-list sizes and starts
+                // level 2: first map slot
                 unsigned s = (unsigned)mix64(h) & K.map_mask;
                 unsigned m = K.map[s];
-                const unsigned sa = X.len[ua != kNoAnc ? ua : 0], sb_ = X.len[ub != kNoAnc ? ub : 0];
-                const unsigned ba = X.beg[ua != kNoAnc ? ua : 0], bbg = X.beg[ub != kNoAnc ? ub : 0];
                 // token dedupe: does bytes(a) + bytes(b) already exist? (usually: empty slot)
                 unsigned nw = (unsigned)ntok;
                 for (; m != 0; s = (s + 1) & K.map_mask, m = K.map[s]) {
@@ -414,14 +439,13 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
                 sb.k8 = la >= 8 ? ka : (ka | (kb >> (8 * la)));
                 sb.round = round; sb.ntok = ntok;
                 // which words can contain (a, b): the smaller covering posting list, or all
-                const unsigned za = ua != kNoAnc ? sa : 0xffffffffu;
-                const unsigned zb = ub != kNoAnc ? sb_ : 0xffffffffu;
                 const bool pick_a = za <= zb;
-                const unsigned u = pick_a ? ua : ub, lu = pick_a ? za : zb;
-                sb.use_list = u != kNoAnc && lu <= X.full_threshold;
-                sb.list_beg = sb.use_list ? (pick_a ? ba : bbg) : 0;
+                const unsigned lu = pick_a ? za : zb, bu = pick_a ? ba : bbg;
+                sb.use_list = lu != kNoAnc && lu <= X.full_threshold;
+                sb.list_beg = sb.use_list ? bu : 0;
                 sb.list_len = sb.use_list ? lu : 0;
-                sb.anc_new = sb.isnew ? u : kNoAnc;   // dedupe: uncovered until the next build
+                sb.cov_beg = bu;
+                sb.cov_len = sb.isnew ? lu : kNoAnc;   // dedupe: uncovered until the next build
             }
         }
     }
@@ -431,7 +455,6 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
         return;
     }
     const unsigned a = sb.a, b = sb.b, nw = sb.nw;
-    const int ntok = sb.ntok;
 
     if (blockIdx.x == 0) {  // record the merge, pop the pair, register a new token
         if (tid == 0) {
@@ -443,7 +466,8 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
             st->cur_cnt = sb.cnt; st->new_is_new = (int)sb.isnew;
             m_a[sb.round] = a; m_b[sb.round] = b; m_new[sb.round] = nw;
             m_mode[sb.round] = sb.use_list ? sb.list_len : 0xffffffffu;
-            X.anc[nw] = sb.anc_new;
+            X.beg[nw] = sb.cov_beg;
+            X.len[nw] = sb.cov_len;
         }
         if (sb.isnew) {
             const unsigned la = K.len[a], ln = la + K.len[b];
@@ -460,17 +484,6 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
                 st->pool_used = base + ln;
             }
         }
-    }
-
-    // rank of the new token = number of live tokens with smaller bytes (a slice per block)
-    if (sb.isnew) {
-        const unsigned per = (ntok + gridDim.x - 1) / gridDim.x;
-        const unsigned lo = blockIdx.x * per;
-        unsigned less = 0;
-        for (unsigned x = lo + tid; x < lo + per && x < (unsigned)ntok; x += blockDim.x)
-            less += cmp_with_concat(K, x, a, b, sb.k8) < 0;
-        less = wave_sum(less);
-        if ((tid & 63) == 0 && less) atomicAdd(&st->new_rank[sb.round & 1], less);
     }
 
     // rewrite every word containing (a, b): this block's share of one slot class
@@ -522,15 +535,16 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
 // ------------------------------------------------------------------ K2: apply deltas
 __global__ void __launch_bounds__(256) k_apply(RoundState* __restrict__ st, PairsDev P,
                                                unsigned long long* __restrict__ LR,
-                                               unsigned* __restrict__ touched) {
-    if (st->halt) return;
+                                               unsigned* __restrict__ touched, unsigned ntb) {
     const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
     const unsigned x = g >> 2, op = g & 3;   // op: 0 (x,a)-=L  1 (x,new)+=L  2 (b,x)-=R  3 (new,x)+=R
-    const int isnew = st->new_is_new;
-    const unsigned ntok = (unsigned)st->ntok + (unsigned)isnew;
-    const unsigned a = st->cur_a, b = st->cur_b, nw = st->cur_new;
+    // ntb (a launch argument) bounds every token id k_merge can have written; cells below it
+    // past the live tokens stay 0.  So the cell load needs no state and issues together with
+    // the state loads.  (The grid is rounded up to whole blocks: x >= ntb is past LR's end.)
     unsigned long long* cell = &LR[2 * (size_t)x + (op >> 1)];
-    const long long d = x < ntok ? (long long)*cell : 0;
+    const long long d = x < ntb ? (long long)*cell : 0;
+    if (st->halt) return;
+    const unsigned a = st->cur_a, b = st->cur_b, nw = st->cur_new;
     size_t inc_slot = ~(size_t)0;
     if (d) {
         switch (op) {
@@ -547,50 +561,31 @@ __global__ void __launch_bounds__(256) k_apply(RoundState* __restrict__ st, Pair
 }
 
 // ------------------------------------------------------------------ K3: argmax over C
-// With advance=1 it also finishes the round: the new token's lexicographic rank is folded in
-// (ranks are double-buffered by round parity: read rank[r&1] corrected on the fly, write
-// rank[(r+1)&1]), the token enters the dedupe map, and round/ntok step forward.
+// With advance=1 it also finishes the round: the new token enters the dedupe map, and
+// round/ntok step forward (by the last block to finish).
 __global__ void __launch_bounds__(256) k_argmax(RoundState* __restrict__ st, PairsDev P, ToksDev K,
-                                                uint32_t* __restrict__ rank2, unsigned rank_stride,
                                                 const unsigned* __restrict__ touched,
                                                 Partial* __restrict__ part, int advance) {
-    __shared__ long long sc[4];
-    __shared__ unsigned long long stb[4];
-    __shared__ unsigned ss[4];
-    __shared__ unsigned long long skey[4];
+    __shared__ Cand sw[4];
     if (st->halt) return;
     const unsigned nC = advance ? st->nC_base : st->nC;
-    const int round = st->round;
-    const unsigned* rank = rank2 + (size_t)(round & 1) * rank_stride;
-    const bool fold = advance && st->new_is_new;
-    const unsigned nw = st->cur_new, rnew = st->new_rank[round & 1];
-    auto rk = [&](unsigned t) -> unsigned {
-        if (!fold) return rank[t];
-        if (t == nw) return rnew;
-        const unsigned r = rank[t];
-        return r + (r >= rnew);
-    };
-    if (advance) {
-        const unsigned ntok = (unsigned)st->ntok + (fold ? 1u : 0u);
-        uint32_t* out = rank2 + (size_t)((round + 1) & 1) * rank_stride;
-        for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < ntok; t += gridDim.x * blockDim.x)
-            out[t] = rk(t);
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-            st->new_rank[(round + 1) & 1] = 0;
-            if (fold) {
-                unsigned s = (unsigned)mix64(K.hash[nw]) & K.map_mask;
-                while (K.map[s] != 0) s = (s + 1) & K.map_mask;
-                K.map[s] = nw + 1;
-            }
-        }
+    const long long T = st->T;
+    const unsigned nt = advance ? st->n_touched : 0u;
+    if (advance && blockIdx.x == 0 && threadIdx.x == 0 && st->new_is_new) {
+        const unsigned nw = st->cur_new;
+        unsigned s = (unsigned)mix64(K.hash[nw]) & K.map_mask;
+        while (K.map[s] != 0) s = (s + 1) & K.map_mask;
+        K.map[s] = nw + 1;
     }
-    long long bc = LLONG_MIN;
-    unsigned long long bt = 0, bk = 0;
-    unsigned bs = 0;
+    Cand best = cand_none();
+    auto consider = [&](unsigned s, long long c) {
+        const unsigned long long key = P.key[s] - 1ULL;
+        const unsigned a = (unsigned)(key >> 32), b = (unsigned)(key & 0xffffffffu);
+        const Cand x{c, K.key8[a], K.key8[b], s, a, b};
+        if (cand_better(x, best, K.pool, K.off, K.len)) best = x;
+    };
     // keys incremented this round: admitted to C by their final count (identical on every
     // rank); they are also candidates of this very argmax
-    const unsigned nt = advance ? st->n_touched : 0u;
-    const long long T = st->T;
     for (unsigned i0 = blockIdx.x * blockDim.x; i0 < nt; i0 += gridDim.x * blockDim.x) {
         const unsigned i = i0 + threadIdx.x;
         bool add = false;
@@ -600,10 +595,7 @@ __global__ void __launch_bounds__(256) k_argmax(RoundState* __restrict__ st, Pai
             const unsigned f = P.flag[s];
             const long long c = P.cnt[s];
             if ((f & kPresent) && c >= T) {
-                const unsigned long long key = P.key[s] - 1ULL;
-                const unsigned long long tb =
-                    ((unsigned long long)rk((unsigned)(key >> 32)) << 32) | rk((unsigned)(key & 0xffffffffu));
-                if (cand_better(c, tb, bc, bt)) { bc = c; bt = tb; bs = s; bk = key; }
+                consider(s, c);
                 if (!(f & kInC)) add = !(atomicOr(&P.flag[s], kInC) & kInC);
             }
         }
@@ -616,29 +608,22 @@ __global__ void __launch_bounds__(256) k_argmax(RoundState* __restrict__ st, Pai
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < nC; i += gridDim.x * blockDim.x) {
         const unsigned s = P.C[i];
         if (!(P.flag[s] & kPresent)) continue;
-        const long long c = P.cnt[s];
-        const unsigned long long key = P.key[s] - 1ULL;
-        const unsigned long long tb =
-            ((unsigned long long)rk((unsigned)(key >> 32)) << 32) | rk((unsigned)(key & 0xffffffffu));
-        if (cand_better(c, tb, bc, bt)) { bc = c; bt = tb; bs = s; bk = key; }
+        consider(s, P.cnt[s]);
     }
     for (int o = 32; o > 0; o >>= 1) {
-        const long long oc = __shfl_xor(bc, o);
-        const unsigned long long ot = __shfl_xor(bt, o);
-        const unsigned os = __shfl_xor(bs, o);
-        const unsigned long long ok = __shfl_xor(bk, o);
-        if (cand_better(oc, ot, bc, bt)) { bc = oc; bt = ot; bs = os; bk = ok; }
+        const Cand oc = shfl_xor_cand(best, o);
+        if (cand_better(oc, best, K.pool, K.off, K.len)) best = oc;
     }
     const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { sc[w] = bc; stb[w] = bt; ss[w] = bs; skey[w] = bk; }
+    if ((threadIdx.x & 63) == 0) sw[w] = best;
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
-            if (cand_better(sc[k], stb[k], bc, bt)) { bc = sc[k]; bt = stb[k]; bs = ss[k]; bk = skey[k]; }
-        part[blockIdx.x] = Partial{bc, bt, bs, (unsigned)(bk >> 32), (unsigned)(bk & 0xffffffffu), 0};
-        // Advance the round only once every block has read round/ntok/new_rank: the last
+            if (cand_better(sw[k], best, K.pool, K.off, K.len)) best = sw[k];
+        part[blockIdx.x] = Partial{best.cnt, best.ka, best.kb, best.slot, best.a, best.b, 0};
+        // Advance the round only once every block has read round-dependent state: the last
         // block to finish does it.  (Advancing from block 0 raced with blocks that had not
-        // started yet -- they then read the other rank buffer's parity.)
+        // started yet.)
         if (advance) {
             __threadfence();
             if (atomicAdd(&st->k3_done, 1u) == gridDim.x - 1) {
@@ -742,7 +727,6 @@ __global__ void k_init_tokens(ToksDev K) {
     K.hash[i] = i;
     K.pw[i] = kPolyP;
     K.key8[i] = (unsigned long long)i << 56;
-    K.rank[i] = i;
     __syncthreads();
     if (i == 0) {
         for (unsigned t = 0; t < 256; ++t) {
@@ -884,10 +868,6 @@ __global__ void k_index_lens(const uint32_t* __restrict__ beg, uint32_t* __restr
     if (t < ntok && len[t]) len[t] -= beg[t];
 }
 
-__global__ void k_anc_init(uint32_t* __restrict__ anc, unsigned ntok) {
-    const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < ntok) anc[t] = t;
-}
 
 // ------------------------------------------------------------------ rebuild helpers
 struct RebuildStats {
@@ -1005,6 +985,7 @@ class MergeLoop {
    private:
     static constexpr int kBatch = 64;
     static constexpr int kArgBlocks = 64;
+    static constexpr int kTimingStride = 8;   // k_merge launches timed: one in 8
     static constexpr unsigned long long kTarget = 4096;
 
     void alloc_pairs(size_t cap);
@@ -1022,7 +1003,7 @@ class MergeLoop {
     void build_index();
     PairsDev pairs() const { return PairsDev{pkey_.p, pcnt_.p, pflag_.p, pcap_ - 1, C_.p}; }
     ToksDev toks() const {
-        return ToksDev{pool_.p, toff_.p, tlen_.p, thash_.p, tpw_.p, tkey8_.p, trank_.p, tmap_.p,
+        return ToksDev{pool_.p, toff_.p, tlen_.p, thash_.p, tpw_.p, tkey8_.p, tmap_.p,
                        (uint32_t)(tmap_.n - 1)};
     }
 
@@ -1051,14 +1032,14 @@ class MergeLoop {
     // tokens
     unsigned tok_cap_ = 0;
     DevBuf<uint8_t> pool_;
-    DevBuf<uint32_t> toff_, tlen_, trank_, tmap_;
+    DevBuf<uint32_t> toff_, tlen_, tmap_;
     DevBuf<unsigned long long> thash_, tpw_, tkey8_;
     DevBuf<unsigned long long> LR_;
     DevBuf<Partial> part_;
     DevBuf<uint32_t> m_a_, m_b_, m_new_, m_mode_;
     DevBuf<RebuildStats> rs_;
     // posting index
-    DevBuf<uint32_t> ilist_, ibeg_, ilen_, ianc_;
+    DevBuf<uint32_t> ilist_, ibeg_, ilen_;
     IndexDev idev_{};
     int next_index_round_ = 256;
     DevBuf<unsigned> touched_;
@@ -1172,8 +1153,7 @@ template <class TokT>
 void MergeLoop<TokT>::build_index() {
     const unsigned n = wdev_.off[kNumCls];
     const unsigned tcap = 256u + (unsigned)n_rounds_ + 1u;
-    if (!ianc_.p) {
-        ianc_.alloc(tcap);
+    if (!ibeg_.p) {
         ibeg_.alloc(tcap);
         ilen_.alloc(tcap);
     }
@@ -1211,11 +1191,9 @@ void MergeLoop<TokT>::build_index() {
                            ibeg_.p, ilen_.p);
         hipLaunchKernelGGL(k_index_lens, dim3(ceil_div(tcap, 256)), dim3(256), 0, s_, ibeg_.p, ilen_.p, tcap);
     }
-    hipLaunchKernelGGL(k_anc_init, dim3(ceil_div(tcap, 256)), dim3(256), 0, s_, ianc_.p,
-                       (unsigned)std::max(hs_.ntok, 256));
     BPE_HIP(hipGetLastError());
     BPE_HIP(hipStreamSynchronize(s_));
-    idev_ = IndexDev{ilist_.p, ibeg_.p, ilen_.p, ianc_.p, n / 6, n};
+    idev_ = IndexDev{ilist_.p, ibeg_.p, ilen_.p, n / 6, n};
     out_.stats.n_index_builds++;
 }
 
@@ -1338,8 +1316,8 @@ int MergeLoop<TokT>::rebuild() {
     hs_.halt = HALT_NONE;
     push_state();
     hipLaunchKernelGGL(k_build_C, dim3(grid), dim3(256), 0, s_, pairs(), pcap_, T, st_.p);
-    hipLaunchKernelGGL(k_argmax, dim3(kArgBlocks), dim3(256), 0, s_, st_.p, pairs(), toks(), trank_.p,
-                       tok_cap_, touched_.p, part_.p, 0);
+    hipLaunchKernelGGL(k_argmax, dim3(kArgBlocks), dim3(256), 0, s_, st_.p, pairs(), toks(),
+                       touched_.p, part_.p, 0);
     BPE_HIP(hipGetLastError());
     pull_state();
     BPE_REQUIRE(!(hs_.err & ERR_C_FULL), BPE_E_NOMEM, "candidate list overflow");
@@ -1360,7 +1338,7 @@ void MergeLoop<TokT>::run() {
     touched_.alloc(2ull * tok_cap_);
     BPE_HIP(hipMemsetAsync(LR_.p, 0, LR_.bytes(), s_));
     m_a_.alloc(n_rounds_); m_b_.alloc(n_rounds_); m_new_.alloc(n_rounds_); m_mode_.alloc(n_rounds_);
-    toff_.alloc(tok_cap_); tlen_.alloc(tok_cap_); trank_.alloc(2ull * tok_cap_);  // 2 rank buffers
+    toff_.alloc(tok_cap_); tlen_.alloc(tok_cap_);
     thash_.alloc(tok_cap_); tpw_.alloc(tok_cap_); tkey8_.alloc(tok_cap_);
     tmap_.alloc(next_pow2(4ull * tok_cap_));
     BPE_HIP(hipMemsetAsync(tmap_.p, 0, tmap_.bytes(), s_));
@@ -1434,23 +1412,25 @@ void MergeLoop<TokT>::run() {
         ensure_pool((unsigned)R * std::max(max_len_, 1u));
         const long long start_round = hs_.round;
         for (int k = 0; k < R; ++k) {
-            if (timing) BPE_HIP(hipEventRecord(ev[2 * k], s_));
             // rewrite -> [one all-reduce of the delta cells when sharded] -> apply -> argmax.
-            // (k_merge<.., true> applies the deltas inside the merge kernel instead; measured
-            // slower: each hit's pair updates serialize on one thread)
-            hipLaunchKernelGGL(k_merge<TokT>, dim3(merge_grid_), dim3(256), 0, s_, st_.p, part_.p,
-                               kArgBlocks, pairs(), toks(), wdev_, idev_, LR_.p, m_a_.p, m_b_.p,
-                               m_new_.p, m_mode_.p);
-            if (timing) BPE_HIP(hipEventRecord(ev[2 * k + 1], s_));
+            // (Applying the deltas inside the merge kernel instead was measured slower: each
+            // hit's pair updates serialize on one thread, see DESIGN.md.)  With timing on, one
+            // launch in kTimingStride is timed, by events stamped from k_merge's own dispatch
+            // packet (events on every launch cost ~8 us of idle per round).
+            const bool timed = timing && (start_round + k) % kTimingStride == 0;
+            hipExtLaunchKernelGGL(k_merge<TokT>, dim3(merge_grid_), dim3(256), 0, s_,
+                                  timed ? ev[2 * k] : nullptr, timed ? ev[2 * k + 1] : nullptr, 0,
+                                  st_.p, (const Partial*)part_.p, (int)kArgBlocks, pairs(), toks(),
+                                  wdev_, idev_, LR_.p, m_a_.p, m_b_.p, m_new_.p, m_mode_.p);
             if (sharded) {   // the one collective per merge round
                 const size_t ntok_bound = 256 + (size_t)start_round + k + 1;
                 comm_->allreduce_i64(reinterpret_cast<int64_t*>(LR_.p), 2 * ntok_bound, s_);
             }
             const unsigned ntb = 256u + (unsigned)start_round + (unsigned)k + 1u;
             hipLaunchKernelGGL(k_apply, dim3(ceil_div(4ull * ntb, 256)), dim3(256), 0, s_, st_.p,
-                               pairs(), LR_.p, touched_.p);
+                               pairs(), LR_.p, touched_.p, ntb);
             hipLaunchKernelGGL(k_argmax, dim3(kArgBlocks), dim3(256), 0, s_, st_.p, pairs(), toks(),
-                               trank_.p, tok_cap_, touched_.p, part_.p, 1);
+                               touched_.p, part_.p, 1);
         }
         BPE_HIP(hipGetLastError());
         pull_state();
@@ -1461,6 +1441,7 @@ void MergeLoop<TokT>::run() {
                 BPE_HIP(hipMemcpy(hmode.data(), m_mode_.p + start_round, done * 4ull, hipMemcpyDeviceToHost));
             const double slot_avg = scan_bytes_ / std::max(1u, idev_.n_slot_words + words_.ln);
             for (int k = 0; k < std::min(done, R); ++k) {
+                if ((start_round + k) % kTimingStride) continue;
                 float t = 0;
                 BPE_HIP(hipEventElapsedTime(&t, ev[2 * k], ev[2 * k + 1]));
                 k1_ms += t;
