@@ -67,18 +67,9 @@ def main():
     _lib.require_device()
     comm = None
     if world > 1:
+        from bpe_amd.dist import Communicator
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        uid = ctypes.create_string_buffer(128)
-        if rank == 0:
-            _lib.check(L.bpe_comm_unique_id(uid), "comm id")
-        obj = [bytes(uid.raw) if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        h = ctypes.c_void_p()
-        _lib.check(L.bpe_comm_init(obj[0], world, rank, local_rank, ctypes.byref(h)), "comm init")
-
-        class _Comm:
-            handle = h
-        comm = _Comm()
+        comm = Communicator.from_torch(local_rank)   # RCCL: one int64 all-reduce per merge round
 
     # ---------------------------------------------------------------- corpus slab in HBM
     blocks = max(1, int(args.bytes) // BLOCK)
@@ -222,6 +213,7 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
+        comm.close()
         dist.destroy_process_group()
 
 

@@ -6,7 +6,6 @@ else -- slab pre-tokenization, local word tables, the delta cells, the replicate
 the argmax -- is the same HIP code the RCCL path runs.  Every rank must end with exactly the
 unsharded result.
 """
-import ctypes
 import multiprocessing as mp
 import os
 
@@ -19,10 +18,9 @@ pytestmark = pytest.mark.gpu
 
 
 def _worker(rank, world, port, slab, vocab_size, specials, q):
-    import numpy as np
-    import torch
     import torch.distributed as dist
-    from bpe_amd import _lib, train_bpe_bytes
+    from bpe_amd import train_bpe_bytes
+    from bpe_amd.dist import HostCommunicator
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -30,25 +28,8 @@ def _worker(rank, world, port, slab, vocab_size, specials, q):
     dist.init_process_group("gloo", rank=rank, world_size=world,
                             timeout=datetime.timedelta(seconds=180))
     try:
-        L = _lib.lib()
-
-        @_lib.HOST_ALLREDUCE_FN
-        def allreduce(_ctx, buf, count):
-            arr = np.ctypeslib.as_array(buf, shape=(count,))
-            t = torch.from_numpy(arr)   # shares memory with the library's staging buffer
-            dist.all_reduce(t)
-            return 0
-
-        h = ctypes.c_void_p()
-        _lib.check(L.bpe_comm_init_host(allreduce, None, world, rank, 0, ctypes.byref(h)), "comm")
-
-        class Comm:
-            handle = h
-
-        try:
-            vocab, merges = train_bpe_bytes(slab, vocab_size, specials, comm=Comm())
-        finally:
-            L.bpe_comm_free(h)
+        with HostCommunicator() as comm:
+            vocab, merges = train_bpe_bytes(slab, vocab_size, specials, comm=comm)
         q.put((rank, (vocab, merges)))
     except Exception as e:  # noqa: BLE001
         q.put((rank, repr(e)))
@@ -57,10 +38,8 @@ def _worker(rank, world, port, slab, vocab_size, specials, q):
 
 
 def _safe_cuts(data, world):
-    from bpe_amd import _lib
-    L = _lib.lib()
-    return [0] + [L.bpe_safe_split(data, len(data), len(data) * r // world)
-                  for r in range(1, world)] + [len(data)]
+    from bpe_amd.dist import slab_bounds
+    return slab_bounds(data, world)
 
 
 def run_sharded(data, world, vocab_size, specials):
@@ -109,3 +88,48 @@ def test_sharded_gpu_synthetic_vs_oracle():
         assert not isinstance(out[r], str), out[r]
         assert out[r][1] == want[1]
         assert out[r][0] == want[0]
+
+
+def _rccl_worker(port, q):
+    """One rank, a real RCCL communicator, and the sharded exchange forced on: exercises
+    ncclCommInitRank / ncclAllReduce on the library's stream exactly as the N>1 bench does."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["BPE355_FORCE_COMM"] = "1"
+    try:
+        from bpe_amd import train_bpe_bytes
+        from bpe_amd.dist import Communicator
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=0, world_size=1)
+        o, _vocab, _merges = G.train_expect("corpus_en_1000")
+        data = G.input_bytes(o["input"])
+        with Communicator.from_torch(0) as comm:
+            out = train_bpe_bytes(data, o["vocab_size"], o["special_tokens"], comm=comm)
+        q.put(out)
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put(repr(e))
+
+
+def test_rccl_comm_single_rank_forced():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(port, q))
+    p.start()
+    try:
+        out = q.get(timeout=300)
+    finally:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert not isinstance(out, str), out
+    o, vocab, merges = G.train_expect("corpus_en_1000")
+    assert out[1] == merges
+    assert out[0] == vocab

@@ -37,7 +37,7 @@ struct RcclComm final : Comm {
         if (comm) (void)ncclCommDestroy(comm);
     }
     void allreduce_i64(int64_t* d_buf, size_t count, hipStream_t stream) override {
-        if (nranks == 1 || count == 0) return;
+        if (count == 0) return;
         BPE_NCCL(ncclAllReduce(d_buf, d_buf, count, ncclInt64, ncclSum, comm, stream));
     }
 };
@@ -52,7 +52,7 @@ struct HostComm final : Comm {
         device = dev;
     }
     void allreduce_i64(int64_t* d_buf, size_t count, hipStream_t stream) override {
-        if (nranks == 1 || count == 0) return;
+        if (count == 0) return;
         buf.resize(count);
         BPE_HIP(hipMemcpyAsync(buf.data(), d_buf, count * 8, hipMemcpyDeviceToHost, stream));
         BPE_HIP(hipStreamSynchronize(stream));

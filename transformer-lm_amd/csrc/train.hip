@@ -1009,6 +1009,12 @@ class MergeLoop {
 
     hipStream_t s_;
     Comm* comm_;
+    // the sharded exchange runs when there are several ranks; BPE355_FORCE_COMM=1 runs it on a
+    // 1-rank communicator too (tests the RCCL calls on a single-GPU box)
+    bool sharded() const {
+        static const bool force = std::getenv("BPE355_FORCE_COMM") != nullptr;
+        return comm_ && (comm_->nranks > 1 || force);
+    }
     const uint8_t* text_;
     int n_rounds_;
     TrainOutput& out_;
@@ -1347,7 +1353,7 @@ void MergeLoop<TokT>::run() {
 
     // global initial pair histogram (train.py:35-49): one all-reduce when sharded; plus the
     // longest word over all ranks (a merged token can be as long as any rank's longest word)
-    if (comm_ && comm_->nranks > 1) {
+    if (sharded()) {
         comm_->allreduce_i64(reinterpret_cast<int64_t*>(hist_.p), 65536, s_);
         std::vector<int64_t> ml(comm_->nranks, 0);
         ml[comm_->rank] = max_len_;
@@ -1385,7 +1391,7 @@ void MergeLoop<TokT>::run() {
     }
     double k1_ms = 0, k1_bytes = 0;
     long long k1_launches = 0;
-    const bool sharded = comm_ && comm_->nranks > 1;
+    const bool sharded = this->sharded();
 
     const bool trace = std::getenv("BPE355_TRACE") != nullptr;
     const int rank = comm_ ? comm_->rank : 0;
