@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch from two rocprofv3 counter passes (MI355X_MICROARCH.md, HBM section):
+
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d <dir_f> -- python3 bench.py ...
+    rocprofv3 --pmc WRITE_SIZE --output-format csv -d <dir_w> -- python3 bench.py ...
+    pmc_traffic.py <fetch counter_collection.csv> <write counter_collection.csv> <out.json>
+
+FETCH_SIZE / WRITE_SIZE are in KB.  On gfx950 FETCH_SIZE reports half the bytes of wide
+(16 B/lane) reads, so it is doubled (the guide's correction); WRITE_SIZE is taken as is.
+Writes {kernel: bytes per launch} plus the raw per-launch counters and launch counts.
+"""
+import csv
+import json
+import re
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    name = re.sub(r"bpe::\(anonymous namespace\)::|bpe::", "", name)
+    name = re.sub(r"\(.*", "", name).replace("void ", "")
+    return re.sub(r"<.*", "", name)
+
+
+def per_launch(path, counter):
+    tot = defaultdict(float)
+    disp = defaultdict(set)
+    with open(path) as f:
+        for d in csv.DictReader(f):
+            if d.get("Counter_Name") != counter:
+                continue
+            k = short(d["Kernel_Name"])
+            tot[k] += float(d["Counter_Value"])
+            disp[k].add(d["Dispatch_Id"])
+    return {k: (tot[k] / len(disp[k]), len(disp[k])) for k in tot}
+
+
+def main():
+    fetch = per_launch(sys.argv[1], "FETCH_SIZE")
+    write = per_launch(sys.argv[2], "WRITE_SIZE")
+    out = {"_note": "HBM bytes per launch = 2 x FETCH_SIZE(KB) x 1024 + WRITE_SIZE(KB) x 1024 "
+                    "(gfx950 FETCH_SIZE correction, MI355X_MICROARCH.md HBM section); two "
+                    "separate --pmc passes of bench.py --steps 1 --warmup 0"}
+    raw = {}
+    for k in sorted(set(fetch) | set(write)):
+        fkb, n = fetch.get(k, (0.0, 0))
+        wkb, _ = write.get(k, (0.0, 0))
+        out[k] = round(2 * fkb * 1024 + wkb * 1024, 1)
+        raw[k] = {"fetch_kb": round(fkb, 3), "write_kb": round(wkb, 3), "launches": n}
+    out["_raw"] = raw
+    with open(sys.argv[3], "w") as f:
+        json.dump(out, f, indent=1)
+    for k in ("k_merge", "k_apply", "k_argmax", "k_count_words"):
+        if k in raw:
+            print(k, out[k], raw[k])
+
+
+if __name__ == "__main__":
+    main()

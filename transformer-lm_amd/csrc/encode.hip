@@ -99,7 +99,7 @@ __device__ __forceinline__ int seg_of(const Seg* __restrict__ segs, int nseg, si
 // a normal segment
 __device__ __forceinline__ bool is_boundary(const uint8_t* __restrict__ s, const Seg& sg, size_t p) {
     if (p == sg.start) return true;
-    return sg.special < 0 && p + 1 < sg.end && is_safe_point(s, sg.end, p);
+    return sg.special < 0 && p + 1 < sg.end && is_safe_point(s, (size_t)sg.end, p);
 }
 
 __device__ __forceinline__ size_t word_lookup(const uint8_t* __restrict__ s, size_t p, size_t len,
@@ -132,7 +132,7 @@ k_scan(const uint8_t* __restrict__ s, size_t n, const Seg* __restrict__ segs, in
         else if (sg.special >= 0) p = sg.end;
         else {
             p = lo;
-            while (p < sg.end && !is_safe_point(s, sg.end, p)) ++p;
+            while (p < sg.end && !is_safe_point(s, (size_t)sg.end, p)) ++p;
         }
     }
     unsigned long long emitted = 0, woff = (MODE == SCAN_WRITE) ? per_thread[t] : 0;
@@ -147,7 +147,7 @@ k_scan(const uint8_t* __restrict__ s, size_t n, const Seg* __restrict__ segs, in
             p = sg.end;
             continue;
         }
-        const size_t e = token_end(s, sg.end, p);
+        const size_t e = token_end(s, (size_t)sg.end, p);
         const size_t len = e - p;
         if (MODE == SCAN_INSERT) {
             if (len >= (1ULL << 24)) { atomicOr(status, 2u); p = e; continue; }

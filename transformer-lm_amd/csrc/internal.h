@@ -29,8 +29,8 @@ const uint8_t* prepare_text(const uint8_t* d_in, size_t n, DevBuf<uint8_t>& scra
 
 // ---------------------------------------------------------------- unique-word count
 struct WordCounts {
-    DevBuf<unsigned long long> key;   // (len << 40) | (offset + 1); 0 = empty
-    DevBuf<unsigned long long> cnt;
+    DevBuf<unsigned long long> kv;    // cap x {key, count} (layout: text.hip), key 0 = empty
+    DevBuf<unsigned long long> pos;   // cap: an occurrence of each inline-keyed word
     size_t cap = 0;
     uint64_t n_pretokens = 0;         // multi-byte pre-tokens seen
 };

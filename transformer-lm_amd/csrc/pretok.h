@@ -24,12 +24,36 @@ namespace bpe {
 #include "uniclass_tables.inc"
 #undef BPE_UCTAB
 
+// The scanners below read bytes through `Src`: a plain device pointer, or an accessor with
+// operator[](size_t) (e.g. a corpus window staged in LDS with a global fallback).
+
+// ASCII classes by arithmetic (no table load on the per-byte critical path); checked against
+// the generated table at compile time below.
+__host__ __device__ constexpr int ascii_class(uint32_t b) {
+    return ((b | 0x20u) - 'a' < 26u) ? CLS_LETTER
+         : (b - '0' < 10u)           ? CLS_NUMBER
+         : (b == 0x20u || b - 9u < 5u) ? CLS_SPACE
+                                      : CLS_OTHER;
+}
+namespace uctab_check {
+#define BPE_UCTAB constexpr
+#include "uniclass_tables.inc"
+#undef BPE_UCTAB
+constexpr bool ascii_ok() {
+    for (unsigned b = 0; b < 128; ++b)
+        if (ascii_class(b) != BPE_ASCII_CLASS[b]) return false;
+    return true;
+}
+static_assert(ascii_ok(), "ascii_class() disagrees with the generated regex class table");
+}  // namespace uctab_check
+
 // class of the code point at s[i] (validated UTF-8); *len = its byte length
-__device__ __forceinline__ int class_at(const uint8_t* __restrict__ s, size_t i, int* len) {
+template <class Src, class Idx>
+__device__ __forceinline__ int class_at(const Src& s, Idx i, int* len) {
     uint32_t b0 = s[i];
     if (b0 < 0x80u) {
         *len = 1;
-        return BPE_ASCII_CLASS[b0];
+        return ascii_class(b0);
     }
     uint32_t cp;
     if (b0 < 0xE0u) {
@@ -53,19 +77,21 @@ __device__ __forceinline__ bool ascii_nonspace(uint32_t b) {
 
 // A safe point: text[p] == ' ' between two ASCII non-whitespace bytes.  Splitting the text
 // there does not change the pre-tokenization of either side.
-__device__ __forceinline__ bool is_safe_point(const uint8_t* __restrict__ s, size_t n, size_t p) {
+template <class Src, class Idx>
+__device__ __forceinline__ bool is_safe_point(const Src& s, Idx n, Idx p) {
     return p >= 1 && p + 1 < n && s[p] == 0x20 && ascii_nonspace(s[p - 1]) &&
            ascii_nonspace(s[p + 1]);
 }
 
-__device__ __forceinline__ size_t next_safe_point(const uint8_t* __restrict__ s, size_t n,
-                                                  size_t p) {
+template <class Src, class Idx>
+__device__ __forceinline__ Idx next_safe_point(const Src& s, Idx n, Idx p) {
     while (p < n && !is_safe_point(s, n, p)) ++p;
     return p < n ? p : n;
 }
 
 // End (exclusive) of the token that starts at byte p of s[0..n).
-__device__ __forceinline__ size_t token_end(const uint8_t* __restrict__ s, size_t n, size_t p) {
+template <class Src, class Idx>
+__device__ __forceinline__ Idx token_end(const Src& s, Idx n, Idx p) {
     const uint32_t b0 = s[p];
     if (b0 == 0x27u && p + 1 < n) {  // contractions
         const uint32_t b1 = s[p + 1];
@@ -78,7 +104,7 @@ __device__ __forceinline__ size_t token_end(const uint8_t* __restrict__ s, size_
     }
     int l0;
     int run_cls = class_at(s, p, &l0);
-    size_t q = p;
+    Idx q = p;
     if (b0 == 0x20u && p + 1 < n) {  // ' ?' prefix: only if a non-space follows
         int l1;
         const int c1 = class_at(s, p + 1, &l1);
@@ -88,7 +114,7 @@ __device__ __forceinline__ size_t token_end(const uint8_t* __restrict__ s, size_
         }
     }
     if (run_cls != CLS_SPACE) {  // ' ?\p{L}+' | ' ?\p{N}+' | ' ?[^\s\p{L}\p{N}]+'
-        size_t e = q;
+        Idx e = q;
         while (e < n) {
             int l;
             if (class_at(s, e, &l) != run_cls) break;
@@ -97,7 +123,7 @@ __device__ __forceinline__ size_t token_end(const uint8_t* __restrict__ s, size_
         return e;
     }
     // '\s+(?!\S)' | '\s+'
-    size_t e = p + l0, last = p;
+    Idx e = p + l0, last = p;
     while (e < n) {
         int l;
         if (class_at(s, e, &l) != CLS_SPACE) break;
@@ -108,10 +134,14 @@ __device__ __forceinline__ size_t token_end(const uint8_t* __restrict__ s, size_
 }
 
 // FNV-1a over the bytes, then a final avalanche: used to place words in the count table.
-__device__ __forceinline__ uint64_t hash_word(const uint8_t* __restrict__ s, size_t len) {
+template <class Src>
+__device__ __forceinline__ uint64_t hash_word(const Src& s, size_t p, size_t len) {
     uint64_t h = 0xcbf29ce484222325ULL;
-    for (size_t i = 0; i < len; ++i) h = (h ^ s[i]) * 0x100000001b3ULL;
+    for (size_t i = 0; i < len; ++i) h = (h ^ s[p + i]) * 0x100000001b3ULL;
     return mix64(h ^ len);
+}
+__device__ __forceinline__ uint64_t hash_word(const uint8_t* __restrict__ s, size_t len) {
+    return hash_word(s, 0, len);
 }
 
 }  // namespace bpe

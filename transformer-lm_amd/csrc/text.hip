@@ -12,6 +12,9 @@
 // comparing bytes against the corpus itself -- exact counting with no spin-waits.
 #include <hipcub/hipcub.hpp>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include <hip/hip_ext.h>
 
 #include "internal.h"
@@ -137,130 +140,351 @@ const uint8_t* prepare_text(const uint8_t* d_in, size_t n, DevBuf<uint8_t>& scra
 }
 
 // ------------------------------------------------------------------ word counting
+// Global table: open addressing over 16-byte entries {key, count} (one line per probe; the
+// table stays small enough to live in the Infinity Cache -- 32-byte entries measured 1.9x
+// slower).  Words of <= 7 bytes are stored INLINE: key = kInl | len << 56 | bytes, so a hit
+// needs no read of the corpus, and the claimer records an occurrence in the cold `pos` array
+// (read only after the kernel).  Longer words are keyed by len << 40 | (offset + 1) of their
+// first occurrence and verified against the corpus.  Words of <= 16 bytes hash by their packed
+// bytes, longer ones by FNV-1a: a word always takes the same path.
 constexpr unsigned long long kOffMask = (1ULL << 40) - 1;
+constexpr unsigned long long kInl = 1ULL << 63;
+constexpr int kInlineKey = 7;        // longest word stored inline in the key
 constexpr int kMaxProbe = 1 << 16;
+constexpr int kInline = 16;          // words up to this length are packed into two u64
+constexpr int kChunk = 16384;        // corpus bytes a workgroup scans per iteration
+constexpr int kHalo = 1024;          // staged bytes past the chunk (tokens running over its end)
+constexpr int kWin = kChunk + kHalo;
+constexpr int kPadded = kWin + (kWin / 64) * 4;   // +4 B per 64 B: threads' spans hit distinct banks
+constexpr int kCache = 1024;         // LDS word-cache entries (2-way)
+constexpr int kEpoch = 4;            // chunks between cache evictions
+constexpr unsigned kKeep = 2;        // an entry stays if it was hit this often in the epoch
+constexpr int kVec = (kWin + 16 * 256 - 1) / (16 * 256);   // 16-B loads per thread per chunk
+constexpr unsigned long long kBusy = 1ULL << 63;
 
-__device__ __forceinline__ bool bytes_equal(const uint8_t* __restrict__ x,
-                                            const uint8_t* __restrict__ y, size_t len) {
-    for (size_t i = 0; i < len; ++i)
-        if (x[i] != y[i]) return false;
-    return true;
+__device__ __forceinline__ uint64_t short_hash(uint64_t lo, uint64_t hi, size_t len) {
+    return mix64(lo ^ mix64(hi ^ (len << 56) ^ 0x9E3779B97F4A7C15ULL));
 }
 
-// insert `c` occurrences of the word s[p, p+len) into the global table (exact: a slot's key
-// is the (length, offset) of the first occurrence that claimed it; matches compare bytes)
-__device__ __forceinline__ void global_add(const uint8_t* __restrict__ s, size_t p, size_t len,
-                                           uint64_t h, unsigned long long c,
-                                           unsigned long long* __restrict__ key,
-                                           unsigned long long* __restrict__ cnt, size_t mask,
+// The staged window lives in dynamic LDS (kPadded bytes per workgroup), addressed directly:
+// a generic pointer to it inside the accessor trips the gfx950 backend.
+extern __shared__ __attribute__((aligned(16))) uint8_t g_stage[];
+
+// the staged window, addressed by position relative to the chunk start (32-bit)
+struct LdsText {
+    __device__ __forceinline__ uint8_t operator[](uint32_t r) const { return g_stage[r + ((r >> 6) << 2)]; }
+};
+constexpr uint32_t kNotFound = 0xffffffffu;
+
+template <class Src>
+__device__ __forceinline__ void pack_word(const Src& t, size_t p, size_t len, uint64_t& lo, uint64_t& hi) {
+    lo = 0;
+    hi = 0;
+    for (size_t i = 0; i < len; ++i) {
+        const uint64_t b = t[p + i];
+        if (i < 8) lo |= b << (8 * i);
+        else hi |= b << (8 * (i - 8));
+    }
+}
+
+// count `c` occurrences of a word in the global table.  Returns true if it inserted the key.
+// wl/wh: the packed bytes (words <= 16 bytes); t/p: the word's bytes for longer ones.
+template <class Src>
+__device__ __forceinline__ bool global_add(const uint8_t* __restrict__ s, const Src& t, size_t p, size_t len,
+                                           uint64_t wl, uint64_t wh, uint64_t h, unsigned long long c,
+                                           unsigned long long* __restrict__ kv,
+                                           unsigned long long* __restrict__ pos, size_t mask,
                                            unsigned* __restrict__ status) {
-    const unsigned long long mine = ((unsigned long long)len << 40) | (p + 1);
+    const bool inl = len <= (size_t)kInlineKey;
+    const unsigned long long mine = inl ? kInl | ((unsigned long long)len << 56) | wl
+                                        : ((unsigned long long)len << 40) | (p + 1);
     size_t slot = h & mask;
     for (int probe = 0; probe < kMaxProbe; ++probe) {
-        unsigned long long k = key[slot];
+        unsigned long long k = kv[2 * slot];
         if (k == 0) {
-            k = atomicCAS(&key[slot], 0ULL, mine);
-            if (k == 0) { atomicAdd(&cnt[slot], c); return; }
+            k = atomicCAS(&kv[2 * slot], 0ULL, mine);
+            if (k == 0) {   // claimed
+                if (inl) pos[slot] = p;
+                atomicAdd(&kv[2 * slot + 1], c);
+                return true;
+            }
         }
-        if ((k >> 40) == len && bytes_equal(s + ((k & kOffMask) - 1), s + p, len)) {
-            atomicAdd(&cnt[slot], c);
-            return;
+        bool eq = false;
+        if (inl) {
+            eq = k == mine;
+        } else if (!(k & kInl) && (k >> 40) == len) {
+            const size_t q = (k & kOffMask) - 1;
+            if (len <= (size_t)kInline) {
+                uint64_t l2, h2;
+                pack_word(s, q, len, l2, h2);
+                eq = l2 == wl && h2 == wh;
+            } else {
+                eq = true;
+                for (size_t i = 0; i < len && eq; ++i) eq = s[q + i] == t[p + i];
+            }
+        }
+        if (eq) {
+            atomicAdd(&kv[2 * slot + 1], c);
+            return false;
         }
         slot = (slot + 1) & mask;
     }
     atomicOr(status, 1u);
+    return false;
 }
 
-// Per-workgroup LDS word cache in front of the global table: frequent words (" the", ",")
-// are counted in LDS and reach the global table once per workgroup instead of once per
-// occurrence -- global atomics on one hot address serialize.  Entries hold the same
-// (length, offset) key, so the cache is exact too; a word whose LDS slot is taken by another
-// word goes straight to the global table.
-constexpr int kLdsWords = 2048;
-
-// Each thread owns a nominal span [t*span, (t+1)*span): it starts at the first safe point
-// at or after the span start and stops at the first safe point at or after the span end,
-// so the spans tile the text exactly along token boundaries.
-__global__ void __launch_bounds__(256) k_count_words(const uint8_t* __restrict__ s, size_t n,
-                                                     size_t span,
-                                                     unsigned long long* __restrict__ key,
-                                                     unsigned long long* __restrict__ cnt,
-                                                     size_t mask, unsigned* __restrict__ status,
+// Persistent workgroups stream the corpus in kChunk pieces: coalesced 16-B loads of the next
+// chunk (+halo) go to registers while the current one is scanned out of LDS.  Each of the 256
+// threads owns a 64-byte nominal span that starts at the first safe point at or after its
+// start and stops at the first safe point at or after its end, so the spans tile the corpus
+// exactly along token boundaries (tokens that run past the staged window read global memory).
+// Words <= 16 bytes are counted in an LDS cache holding their packed bytes (2-way; a slot is
+// published only after its bytes are written); the rest, and cache conflicts, go to the global
+// table.  The cache is flushed once at the end.  If the table passes max_fill keys, every
+// workgroup stops early and the host recounts with a larger table.
+template <bool kAligned>
+__global__ void __launch_bounds__(256, 3) k_count_words(const uint8_t* __restrict__ s, size_t n,
+                                                     size_t n_chunks, unsigned long long* __restrict__ kv,
+                                                     unsigned long long* __restrict__ pos, size_t mask, unsigned long long max_fill,
+                                                     unsigned long long* __restrict__ fill,
+                                                     unsigned* __restrict__ status,
                                                      unsigned long long* __restrict__ n_tok) {
-    __shared__ unsigned long long l_key[kLdsWords];
-    __shared__ unsigned l_cnt[kLdsWords];
-    __shared__ unsigned long long s_tok[4];
-    for (int i = threadIdx.x; i < kLdsWords; i += blockDim.x) { l_key[i] = 0; l_cnt[i] = 0; }
-    __syncthreads();
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t lo = t * span;
-    const size_t hi = lo + span;
-    size_t p = lo >= n ? n : ((t == 0) ? 0 : next_safe_point(s, n, lo));
-    unsigned long long ntok = 0;
-    while (p < n) {
-        if (p >= hi && is_safe_point(s, n, p)) break;
-        const size_t e = token_end(s, n, p);
-        const size_t len = e - p;
-        if (len >= 2) {
-            ++ntok;
-            if (len >= (1ULL << 24)) { atomicOr(status, 2u); p = e; continue; }
-            const uint64_t h = hash_word(s + p, len);
-            const unsigned ls = (unsigned)(h >> 40) & (kLdsWords - 1);
-            const unsigned long long mine = ((unsigned long long)len << 40) | (p + 1);
-            unsigned long long k = l_key[ls];
-            if (k == 0) k = atomicCAS(&l_key[ls], 0ULL, mine);
-            if (k == 0 ||
-                ((k >> 40) == len && bytes_equal(s + ((k & kOffMask) - 1), s + p, len))) {
-                atomicAdd(&l_cnt[ls], 1u);
+    __shared__ unsigned long long c_key[kCache];
+    __shared__ uint64_t c_lo[kCache], c_hi[kCache];
+    __shared__ unsigned c_cnt[kCache];
+    __shared__ uint16_t c_mark[kCache];   // low 16 bits of c_cnt at the last epoch end
+    __shared__ unsigned long long s_red[4];
+    __shared__ uint32_t s_start[257];
+    __shared__ int s_stop;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kCache; i += blockDim.x) { c_key[i] = 0; c_cnt[i] = 0; c_mark[i] = 0; }
+    unsigned long long ntok = 0, inserted = 0, n_miss = 0, n_long = 0;
+
+    uint4 pre[kVec];
+    auto fetch = [&](size_t c) {
+        const size_t base = c * kChunk;
+#pragma unroll
+        for (int v = 0; v < kVec; ++v) {
+            const size_t off = ((size_t)v * 256 + tid) * 16;
+            if (off >= (size_t)kWin) continue;
+            const size_t g = base + off;
+            if (kAligned && g + 16 <= n) {
+                pre[v] = *reinterpret_cast<const uint4*>(s + g);
             } else {
-                global_add(s, p, len, h, 1, key, cnt, mask, status);
+                uint8_t tmp[16];
+                for (int j = 0; j < 16; ++j) tmp[j] = g + j < n ? s[g + j] : 0;
+                __builtin_memcpy(&pre[v], tmp, 16);
             }
         }
-        p = e;
+    };
+    // one pre-token of length len at position r of src (global offset gpos)
+    auto count_token = [&](const auto& src, auto r, size_t len, size_t gpos) {
+        if (len < 2) return;
+        ++ntok;
+        if (len >= (1ULL << 24)) {
+            atomicOr(status, 2u);
+        } else if (len <= kInline) {
+            uint64_t wl = 0, wh = 0;
+            for (uint32_t i = 0; i < (uint32_t)len; ++i) {
+                const uint64_t b = src[r + i];
+                if (i < 8) wl |= b << (8 * i);
+                else wh |= b << (8 * (i - 8));
+            }
+            const uint64_t h = short_hash(wl, wh, len);
+            const unsigned ls = (unsigned)(h >> 40) & (kCache - 2);
+            const unsigned long long mine = ((unsigned long long)len << 40) | (gpos + 1);
+            for (int way = 0; way < 2; ++way) {
+                const unsigned sl = ls + way;
+                unsigned long long k = c_key[sl];
+                if (k == 0) {
+                    k = atomicCAS(&c_key[sl], 0ULL, kBusy);
+                    if (k == 0) {   // claimed: bytes first, then publish the key (a wave's LDS
+                        c_lo[sl] = wl;  // operations execute in order; the barrier keeps the
+                        c_hi[sl] = wh;  // compiler from reordering them)
+                        __asm__ volatile("" ::: "memory");
+                        atomicExch(&c_key[sl], mine);
+                        atomicAdd(&c_cnt[sl], 1u);
+                        return;
+                    }
+                }
+                if (k != kBusy && (k >> 40) == len) {
+                    __asm__ volatile("" ::: "memory");
+                    if (c_lo[sl] == wl && c_hi[sl] == wh) {
+                        atomicAdd(&c_cnt[sl], 1u);
+                        return;
+                    }
+                }
+            }
+            ++n_miss;
+            inserted += global_add(s, s, gpos, len, wl, wh, h, 1, kv, pos, mask, status);
+        } else {
+            ++n_long;
+            inserted += global_add(s, s, gpos, len, 0, 0, hash_word(s, gpos, len), 1, kv, pos, mask, status);
+        }
+    };
+    if (blockIdx.x < n_chunks) fetch(blockIdx.x);
+    for (size_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+        __syncthreads();   // the previous chunk's scan is done with buf
+#pragma unroll
+        for (int v = 0; v < kVec; ++v) {
+            const size_t off = ((size_t)v * 256 + tid) * 16;
+            if (off >= (size_t)kWin) continue;
+            uint32_t* d = reinterpret_cast<uint32_t*>(g_stage + off + ((off >> 6) << 2));
+            d[0] = pre[v].x; d[1] = pre[v].y; d[2] = pre[v].z; d[3] = pre[v].w;
+        }
+        if (tid == 0) s_stop = *(volatile unsigned long long*)fill > max_fill;
+        __syncthreads();
+        if (s_stop) {
+            if (tid == 0) atomicOr(status, 1u);
+            break;
+        }
+        if (c + gridDim.x < n_chunks) fetch(c + gridDim.x);   // in flight during the scan
+
+        const size_t base = c * kChunk;
+        const size_t rem = n - base;
+        const bool text_ends = rem <= (size_t)kWin;          // the window reaches the end of text
+        const uint32_t nloc = text_ends ? (uint32_t)rem : (uint32_t)kWin;
+        const uint32_t search_end = text_ends ? nloc : nloc - 2;   // safe points need p+1 staged
+        // span starts: the first safe point at or after each nominal start, searched inside the
+        // window only (kNotFound: it lies past the window)
+        const LdsText L{};
+        auto find_start = [&](uint32_t r) -> uint32_t {
+            if (c == 0 && r == 0) return 0;
+            if (r >= nloc) return text_ends ? nloc : kNotFound;
+            if (r == 0) {   // position 0's left neighbour is the previous chunk's last byte
+                if (nloc > 1 && L[0] == 0x20 && ascii_nonspace(s[base - 1]) && ascii_nonspace(L[1]))
+                    return 0;
+                r = 1;
+            }
+            for (; r < search_end; ++r)
+                if (is_safe_point(L, nloc, r)) return r;
+            return text_ends ? nloc : kNotFound;
+        };
+        s_start[tid] = find_start((uint32_t)tid * 64);
+        if (tid == 0) s_start[256] = find_start((uint32_t)kChunk);
+        __syncthreads();
+        const uint32_t r0 = s_start[tid], r1 = s_start[tid + 1];
+        if (r0 != kNotFound && r1 != kNotFound) {
+            // fast path: [r0, r1) and its one-byte lookahead are staged
+            for (uint32_t r = r0; r < r1;) {
+                const uint32_t e = token_end(L, nloc, r);
+                count_token(L, r, e - r, base + r);
+                r = e;
+            }
+        } else if (r0 != kNotFound) {
+            // slow path (rare): no safe point in the rest of the window -- scan global memory
+            // from r0 to the first safe point past this thread's nominal end
+            const size_t hi = base + (size_t)tid * 64 + 64;
+            for (size_t p = base + r0; p < n;) {
+                if (p >= hi && is_safe_point(s, n, p)) break;
+                const size_t e = token_end(s, n, p);
+                count_token(s, p, e - p, p);
+                p = e;
+            }
+        }
+        // epoch end: entries hit fewer than kKeep times since the last epoch go to the global
+        // table and free their slot (the cache fills first-come; without eviction a frequent
+        // word whose two ways were taken early would miss for the whole stream)
+        if ((c - blockIdx.x) / gridDim.x % kEpoch == kEpoch - 1) {
+            __syncthreads();
+            for (int i = tid; i < kCache; i += blockDim.x) {
+                const unsigned long long k = c_key[i];
+                if (k == 0 || k == kBusy) continue;
+                const unsigned cc = c_cnt[i];
+                if ((uint16_t)(cc - c_mark[i]) >= kKeep) {   // < 65536 hits per 64 KB epoch
+                    c_mark[i] = (uint16_t)cc;
+                    continue;
+                }
+                const size_t len = (size_t)(k >> 40), p0 = (size_t)(k & kOffMask) - 1;
+                const uint64_t wl = c_lo[i], wh = c_hi[i];
+                inserted += global_add(s, s, p0, len, wl, wh, short_hash(wl, wh, len), cc, kv, pos, mask, status);
+                c_key[i] = 0;
+                c_cnt[i] = 0;
+                c_mark[i] = 0;
+            }
+        }
+        // publish this chunk's new keys (one atomic per workgroup per chunk)
+        const unsigned long long ins = wave_sum(inserted);
+        inserted = 0;
+        if ((tid & 63) == 0) s_red[tid >> 6] = ins;
+        __syncthreads();
+        if (tid == 0) {
+            const unsigned long long b = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+            if (b) atomicAdd(fill, b);
+        }
     }
-    ntok = wave_sum(ntok);
-    if ((threadIdx.x & 63) == 0) s_tok[threadIdx.x >> 6] = ntok;
     __syncthreads();
     // flush the cache: one global add per distinct cached word
-    for (int i = threadIdx.x; i < kLdsWords; i += blockDim.x) {
-        const unsigned long long k = l_key[i];
-        if (!k) continue;
+    for (int i = tid; i < kCache; i += blockDim.x) {
+        const unsigned long long k = c_key[i];
+        if (k == 0 || k == kBusy) continue;
         const size_t len = (size_t)(k >> 40), p0 = (size_t)(k & kOffMask) - 1;
-        global_add(s, p0, len, hash_word(s + p0, len), l_cnt[i], key, cnt, mask, status);
+        const uint64_t wl = c_lo[i], wh = c_hi[i];
+        inserted += global_add(s, s, p0, len, wl, wh, short_hash(wl, wh, len), c_cnt[i], kv, pos, mask, status);
     }
-    if (threadIdx.x == 0) {  // per-block sum, one atomic per block
-        const unsigned long long b = s_tok[0] + s_tok[1] + s_tok[2] + s_tok[3];
+    ntok = wave_sum(ntok);
+    inserted = wave_sum(inserted);
+    n_miss = wave_sum(n_miss);
+    n_long = wave_sum(n_long);
+    if ((tid & 63) == 0 && (n_miss | n_long)) {   // diagnostics (BPE355_TRACE)
+        atomicAdd(n_tok + 1, n_miss);
+        atomicAdd(n_tok + 2, n_long);
+    }
+    __syncthreads();
+    if ((tid & 63) == 0) s_red[tid >> 6] = ntok;
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned long long b = s_red[0] + s_red[1] + s_red[2] + s_red[3];
         if (b) atomicAdd(n_tok, b);
+    }
+    __syncthreads();
+    if ((tid & 63) == 0) s_red[tid >> 6] = inserted;
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned long long b = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+        if (b) atomicAdd(fill, b);
     }
 }
 
 void count_words(const uint8_t* d_text, size_t n, WordCounts& wc, hipStream_t stream,
                  float* kernel_ms) {
     BPE_REQUIRE(n < (1ULL << 40) - 1, BPE_E_LIMIT, "corpus slab larger than 1 TiB");
-    size_t cap = next_pow2(std::max<size_t>(1 << 16, n / 96));
-    constexpr size_t kSpan = 512;
+    // first guess ~1 slot per KiB of text (7.4 M words in 11.9 GB of OWT-like text: load 0.46);
+    // the kernel stops early past load 1/2 and the count reruns with 4x the slots
+    size_t cap = next_pow2(std::max<size_t>(1 << 16, n / 1024));
     DevBuf<unsigned> status(1);
-    DevBuf<unsigned long long> ntok(1);
+    DevBuf<unsigned long long> ntok(3), fill(1);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (kernel_ms) {
         BPE_HIP(hipEventCreate(&e0));
         BPE_HIP(hipEventCreate(&e1));
     }
+    const size_t n_chunks = (n + kChunk - 1) / kChunk;
+    const bool aligned = (reinterpret_cast<uintptr_t>(d_text) & 15u) == 0;
+    // one resident wave of persistent workgroups: every workgroup takes the same number of
+    // chunks, so a second, queued wave would nearly double the time
+    auto kern = aligned ? k_count_words<true> : k_count_words<false>;
+    int per_cu = 0, dev = 0, n_cu = 0;
+    BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, kPadded));
+    BPE_HIP(hipGetDevice(&dev));
+    BPE_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    const unsigned grid = (unsigned)std::min<size_t>(std::max<size_t>(n_chunks, 1),
+                                                     (size_t)std::max(1, per_cu) * std::max(1, n_cu));
     for (int attempt = 0;; ++attempt) {
-        wc.key.alloc(cap);
-        wc.cnt.alloc(cap);
+        wc.kv.alloc(2 * cap);
+        wc.pos.alloc(cap);
         wc.cap = cap;
-        BPE_HIP(hipMemsetAsync(wc.key.p, 0, wc.key.bytes(), stream));
-        BPE_HIP(hipMemsetAsync(wc.cnt.p, 0, wc.cnt.bytes(), stream));
+        BPE_HIP(hipMemsetAsync(wc.kv.p, 0, wc.kv.bytes(), stream));
         BPE_HIP(hipMemsetAsync(status.p, 0, 4, stream));
-        BPE_HIP(hipMemsetAsync(ntok.p, 0, 8, stream));
+        BPE_HIP(hipMemsetAsync(ntok.p, 0, 24, stream));
+        BPE_HIP(hipMemsetAsync(fill.p, 0, 8, stream));
         if (n) {
-            const size_t threads = (n + kSpan - 1) / kSpan;
             // timed launch: the events are stamped by the kernel's own dispatch packet (the
             // interval rocprofv3 reports), not by marker packets around it
-            hipExtLaunchKernelGGL(k_count_words, dim3(ceil_div(threads, 256)), dim3(256), 0, stream,
+            hipExtLaunchKernelGGL(kern, dim3(grid), dim3(256), kPadded, stream,
                                   kernel_ms ? e0 : nullptr, kernel_ms ? e1 : nullptr, 0,
-                                  d_text, n, kSpan, wc.key.p, wc.cnt.p, cap - 1, status.p, ntok.p);
+                                  d_text, n, n_chunks, wc.kv.p, wc.pos.p, cap - 1,
+                                  (unsigned long long)(cap / 2), fill.p, status.p, ntok.p);
             BPE_HIP(hipGetLastError());
         }
         unsigned st = 0;
@@ -269,8 +493,14 @@ void count_words(const uint8_t* d_text, size_t n, WordCounts& wc, hipStream_t st
         BPE_HIP(hipStreamSynchronize(stream));
         if (st & 2u) throw Error{BPE_E_LIMIT, "a pre-token is longer than 16 MiB"};
         if (kernel_ms && n) BPE_HIP(hipEventElapsedTime(kernel_ms, e0, e1));
+        if (std::getenv("BPE355_TRACE")) {
+            unsigned long long d[3];
+            BPE_HIP(hipMemcpy(d, ntok.p, 24, hipMemcpyDeviceToHost));
+            std::fprintf(stderr, "[bpe355] count: cap %zu pretokens %llu cache-miss %llu long %llu grid %u\n",
+                         cap, d[0], d[1], d[2], grid);
+        }
         if (!(st & 1u)) break;
-        BPE_REQUIRE(attempt < 4, BPE_E_NOMEM, "word table overflow");
+        BPE_REQUIRE(attempt < 6, BPE_E_NOMEM, "word table overflow");
         cap *= 4;  // the table filled up: grow and recount
     }
     if (e0) (void)hipEventDestroy(e0);

@@ -636,18 +636,21 @@ __global__ void __launch_bounds__(256) k_argmax(RoundState* __restrict__ st, Pai
 }
 
 // ------------------------------------------------------------------ word table build
-__global__ void k_collect_words(const unsigned long long* __restrict__ key,
-                                const unsigned long long* __restrict__ cnt, size_t cap,
+__global__ void k_collect_words(const unsigned long long* __restrict__ kv,
+                                const unsigned long long* __restrict__ pos, size_t cap,
                                 const uint8_t* __restrict__ text, const uint8_t* __restrict__ sp_bytes,
                                 const uint32_t* __restrict__ sp_off, const uint32_t* __restrict__ sp_len,
                                 int n_sp, unsigned long long* __restrict__ w_off,
                                 uint32_t* __restrict__ w_len, unsigned long long* __restrict__ w_cnt,
                                 unsigned* __restrict__ n_words, unsigned* __restrict__ max_len) {
     const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const unsigned long long k = s < cap ? key[s] : 0ULL;
+    // {key, count} entries (text.hip): the key's top bit marks a word stored inline (length in
+    // bits 56..62, an occurrence in pos[]), else key = len << 40 | offset + 1
+    const unsigned long long k = s < cap ? kv[2 * s] : 0ULL;
     bool keep = k != 0;
-    const unsigned len = (unsigned)(k >> 40);
-    const unsigned long long off = (k & ((1ULL << 40) - 1)) - 1;
+    const bool inl = (k >> 63) != 0;
+    const unsigned len = inl ? (unsigned)((k >> 56) & 0x7f) : (unsigned)(k >> 40);
+    const unsigned long long off = inl ? (keep ? pos[s] : 0ULL) : (k & ((1ULL << 40) - 1)) - 1;
     for (int i = 0; keep && i < n_sp; ++i) {  // train.py:25 skips matches equal to a special
         if (sp_len[i] != len) continue;
         bool eq = true;
@@ -658,7 +661,7 @@ __global__ void k_collect_words(const unsigned long long* __restrict__ key,
     const unsigned ml = wave_max(keep ? len : 0u);
     if ((threadIdx.x & 63) == 0 && ml) atomicMax(max_len, ml);
     if (!keep) return;
-    w_off[idx] = off; w_len[idx] = len; w_cnt[idx] = cnt[s];
+    w_off[idx] = off; w_len[idx] = len; w_cnt[idx] = kv[2 * s + 1];
 }
 
 __global__ void k_len_u64(const uint32_t* __restrict__ w_len, unsigned n, unsigned long long* __restrict__ o) {
@@ -1069,8 +1072,8 @@ void MergeLoop<TokT>::build_words(const WordCounts& wc, const std::vector<std::s
     BPE_HIP(hipMemsetAsync(cnts.p, 0, 8, s_));
     DevBuf<unsigned long long> w_off(wc.cap), w_cnt(wc.cap);
     DevBuf<uint32_t> w_len(wc.cap);
-    hipLaunchKernelGGL(k_collect_words, dim3(ceil_div(wc.cap, 256)), dim3(256), 0, s_, wc.key.p,
-                       wc.cnt.p, wc.cap, text_, d_spb.p, d_spo.p, d_spl.p, (int)specials.size(),
+    hipLaunchKernelGGL(k_collect_words, dim3(ceil_div(wc.cap, 256)), dim3(256), 0, s_, wc.kv.p,
+                       wc.pos.p, wc.cap, text_, d_spb.p, d_spo.p, d_spl.p, (int)specials.size(),
                        w_off.p, w_len.p, w_cnt.p, cnts.p, cnts.p + 1);
     BPE_HIP(hipGetLastError());
     unsigned h2[2];
@@ -1212,7 +1215,10 @@ void MergeLoop<TokT>::layout_blocks() {
     for (int c = 0; c < kNumCls; ++c) W.off[c + 1] = W.off[c] + W.c[c].n;
     // about one resident generation of workgroups (4 per CU): each block's prologue is a
     // chain of dependent loads, so a second generation would pay it again
-    constexpr unsigned kGridBudget = 1024;
+    static const unsigned kGridBudget = [] {
+        const char* e = std::getenv("BPE355_GRID");   // experiment knob
+        return e ? (unsigned)std::max(16, std::atoi(e)) : 1024u;
+    }();
     double total_b = 0;
     for (int c = 0; c < kNumCls; ++c) total_b += (double)W.c[c].n * slot_w(c);
     unsigned blk = 0;
