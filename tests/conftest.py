@@ -4,7 +4,7 @@ import sys
 import pytest
 
 ROOT = pathlib.Path(__file__).resolve().parent.parent
-for p in (ROOT / "tests", ROOT / "transformer-lm_amd", ROOT):
+for p in (ROOT / "tests" / "golden", ROOT / "tests", ROOT / "transformer-lm_amd", ROOT):
     if str(p) not in sys.path:
         sys.path.insert(0, str(p))
 

@@ -66,7 +66,9 @@ def _boundary_text(seed, n_chunks=48):
 
 
 def _oracle_pretokens(data: bytes) -> int:
-    return sum(c for w, c in oracle.word_counts(data, []).items() if len(w) >= 2)
+    # train_bpe reads text mode: universal newlines first (train.py:22), then pre-tokenizes
+    text = oracle.decode_text(data)
+    return sum(c for w, c in oracle.word_counts(text, []).items() if len(w) >= 2)
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
@@ -80,3 +82,31 @@ def test_chunk_boundaries_train(seed):
     want_vocab, want_merges = oracle.train_raw(data, 900, [])
     assert merges == want_merges
     assert vocab == want_vocab
+
+
+# Few workgroups (BPE355_STREAM_WG): each streams ~90 chunks through its LDS word cache,
+# across many eviction epochs -- the regime of full-size corpora, at test size.
+@pytest.mark.parametrize("wg", [1, 3])
+def test_streaming_workgroups_train(monkeypatch, wg):
+    import synth_text
+    from bpe_amd import train_bpe_bytes
+    from bpe_amd.train import last_train_stats
+    monkeypatch.setenv("BPE355_STREAM_WG", str(wg))
+    data = synth_text.generate(41, 3_000_000, "mixed").encode("utf-8")
+    vocab, merges = train_bpe_bytes(data, 2000, ["<|endoftext|>"])
+    assert last_train_stats()["n_pretokens"] == _oracle_pretokens(data)
+    want_vocab, want_merges = oracle.train_raw(data, 2000, ["<|endoftext|>"])
+    assert merges == want_merges
+    assert vocab == want_vocab
+
+
+@pytest.mark.parametrize("wg", [1, 3])
+def test_streaming_workgroups_encode(monkeypatch, wg):
+    import gpt2_files
+    import synth_text
+    import bpe_amd
+    monkeypatch.setenv("BPE355_STREAM_WG", str(wg))
+    vocab, merges = gpt2_files.load_gpt2(["<|endoftext|>"])
+    text = synth_text.generate(42, 2_500_000, "mixed") + _boundary_text(4).decode("utf-8")
+    tok = bpe_amd.Tokenizer(dict(vocab), list(merges), ["<|endoftext|>"])
+    assert tok.encode(text) == oracle.encode(vocab, merges, ["<|endoftext|>"], text)

@@ -44,3 +44,23 @@ def test_encode_matches_oracle_synthetic(seed, n_chars, flavour):
     text = synth_text.generate(seed, n_chars, flavour)
     tok = bpe_amd.Tokenizer(dict(vocab), list(merges), ["<|endoftext|>"])
     assert tok.encode(text) == oracle.encode(vocab, merges, ["<|endoftext|>"], text)
+
+
+def test_encode_bench_corpus_sample_vs_oracle():
+    """48 MB of bench.py's own synthetic corpus (every workgroup streams several chunks through
+    eviction epochs), merges trained on the device, encode checked against the oracle."""
+    import ctypes
+    import torch
+    from bpe_amd import _lib, train_bpe_device
+    L = _lib.lib()
+    n = 48 * (1 << 20)
+    corpus = torch.empty(n, dtype=torch.uint8, device="cuda")
+    _lib.check(L.bpe_synth_corpus_device(ctypes.c_void_p(corpus.data_ptr()), n, 7, 0, 0, None), "synth")
+    torch.cuda.synchronize()
+    vocab, merges = train_bpe_device(corpus.data_ptr(), n, 4000, ["<|endoftext|>"])
+    text = corpus.cpu().numpy().tobytes().decode("utf-8")
+    tok = bpe_amd.Tokenizer(dict(vocab), list(merges), ["<|endoftext|>"])
+    got = tok.encode(text)
+    want = oracle.encode(vocab, merges, ["<|endoftext|>"], text)
+    assert len(got) == len(want)
+    assert got == want

@@ -92,6 +92,14 @@ def lib():
         if not LIB_PATH.exists():
             raise LibraryMissing(f"{LIB_PATH} not built; run `python -c 'import __graft_entry__ as g; "
                                  "g.build()'` (hipcc --offload-arch=gfx950)")
+        # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64, and whichever
+        # copy is loaded first serves every later library that needs that soname.  Loading
+        # torch's first keeps torch.cuda usable next to this library (loading ours first left
+        # torch with "No HIP GPUs are available").  Importing torch does not touch the GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(str(LIB_PATH))
         for name, res, args in _SIGS:
             fn = getattr(L, name)

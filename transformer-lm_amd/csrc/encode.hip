@@ -20,6 +20,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -28,12 +29,12 @@
 
 #include "internal.h"
 #include "pretok.h"
+#include "stage.h"
 
 namespace bpe {
 namespace {
 
 constexpr unsigned long long kOff40 = (1ULL << 40) - 1;
-constexpr size_t kSpan = 256;
 
 struct Seg {                 // a piece of the text: normal (special = -1) or one special token
     unsigned long long start, end;
@@ -82,8 +83,18 @@ __global__ void k_find_specials(const uint8_t* __restrict__ s, size_t n, EncTabl
     }
 }
 
-// ------------------------------------------------------------------ 2/4. segment-aware scan
-enum { SCAN_INSERT = 0, SCAN_COUNT = 1, SCAN_WRITE = 2 };
+// ------------------------------------------------------------------ 2. segment-aware scan
+// Persistent workgroups stream the text in kChunk pieces staged in LDS (stage.h), like the
+// training counter.  Scan boundaries are segment starts and safe points inside normal
+// segments; thread t of chunk c owns the pre-tokens starting in [first boundary >= its nominal
+// start, first boundary >= its nominal end).  Each pre-token is found or inserted in the word
+// table (an LDS cache maps words <= 16 bytes to their slot) and recorded as one u32 -- its
+// slot, or kSpecialRec | special index -- at recs[span start + k]: a span of B bytes holds at
+// most B pre-tokens, so the records of all spans fit in an n-entry array with no prefix sum.
+constexpr uint32_t kSpecialRec = 0x80000000u;
+constexpr int kEncCache = 1024;
+constexpr int kEncEpoch = 4;
+constexpr unsigned kEncKeep = 2;
 
 __device__ __forceinline__ int seg_of(const Seg* __restrict__ segs, int nseg, size_t p) {
     int lo = 0, hi = nseg - 1;  // last segment with start <= p
@@ -95,103 +106,256 @@ __device__ __forceinline__ int seg_of(const Seg* __restrict__ segs, int nseg, si
     return lo;
 }
 
-// a position where an independent scan may start: a segment start, or a safe point inside
-// a normal segment
-__device__ __forceinline__ bool is_boundary(const uint8_t* __restrict__ s, const Seg& sg, size_t p) {
-    if (p == sg.start) return true;
-    return sg.special < 0 && p + 1 < sg.end && is_safe_point(s, (size_t)sg.end, p);
-}
-
-__device__ __forceinline__ size_t word_lookup(const uint8_t* __restrict__ s, size_t p, size_t len,
-                                              const unsigned long long* __restrict__ key, size_t mask) {
-    size_t slot = hash_word(s + p, len) & mask;
-    for (;;) {
-        const unsigned long long k = key[slot];
-        if (k == 0) return ~(size_t)0;
-        if ((k >> 40) == len && bytes_eq(s + ((k & kOff40) - 1), s + p, len)) return slot;
-        slot = (slot + 1) & mask;
-    }
-}
-
-template <int MODE>
-__global__ void __launch_bounds__(256)
-k_scan(const uint8_t* __restrict__ s, size_t n, const Seg* __restrict__ segs, int nseg, EncTables E,
-       unsigned long long* __restrict__ key, size_t mask, const uint32_t* __restrict__ slot_word,
-       const uint32_t* __restrict__ w_nids, const unsigned long long* __restrict__ w_idoff,
-       const uint32_t* __restrict__ ids_pool, unsigned long long* __restrict__ per_thread,
-       uint32_t* __restrict__ out, unsigned* __restrict__ status) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t lo = t * kSpan;
-    if (lo >= n) return;
-    const size_t hi = lo + kSpan;
-    int k = seg_of(segs, nseg, lo);
-    size_t p;
-    {
+// first scan boundary at or after global position p, looking no further than `limit`
+// (returns ~0 if none below it).  Reads go through `byte(q)`.
+template <class ByteAt>
+__device__ __forceinline__ size_t first_boundary(const Seg* __restrict__ segs, int nseg, size_t p,
+                                                 size_t limit, const ByteAt& byte) {
+    int k = seg_of(segs, nseg, p);
+    while (p < limit) {
         const Seg sg = segs[k];
-        if (lo == sg.start) p = lo;
-        else if (sg.special >= 0) p = sg.end;
-        else {
-            p = lo;
-            while (p < sg.end && !is_safe_point(s, (size_t)sg.end, p)) ++p;
-        }
-    }
-    unsigned long long emitted = 0, woff = (MODE == SCAN_WRITE) ? per_thread[t] : 0;
-    while (p < n) {
-        while (k < nseg && p >= segs[k].end) ++k;
-        if (k >= nseg) break;
-        const Seg sg = segs[k];
-        if (p >= hi && is_boundary(s, sg, p)) break;
-        if (sg.special >= 0) {  // a special segment (p == sg.start here)
-            if (MODE == SCAN_WRITE) out[woff++] = (uint32_t)E.sp_vid[sg.special];
-            ++emitted;
+        if (p == sg.start) return p;
+        if (sg.special >= 0) {           // inside a special: the next segment starts a scan
             p = sg.end;
+            ++k;
             continue;
         }
-        const size_t e = token_end(s, (size_t)sg.end, p);
-        const size_t len = e - p;
-        if (MODE == SCAN_INSERT) {
-            if (len >= (1ULL << 24)) { atomicOr(status, 2u); p = e; continue; }
-            const unsigned long long mine = ((unsigned long long)len << 40) | (p + 1);
-            size_t slot = hash_word(s + p, len) & mask;
-            int probe = 0;
-            for (; probe < (1 << 16); ++probe) {
-                unsigned long long kk = key[slot];
-                if (kk == 0) {
-                    kk = atomicCAS(&key[slot], 0ULL, mine);
-                    if (kk == 0) break;
-                }
-                if ((kk >> 40) == len && bytes_eq(s + ((kk & kOff40) - 1), s + p, len)) break;
-                slot = (slot + 1) & mask;
-            }
-            if (probe == (1 << 16)) atomicOr(status, 1u);
-        } else {
-            const size_t slot = word_lookup(s, p, len, key, mask);
-            if (slot == ~(size_t)0) { atomicOr(status, 8u); p = e; continue; }
-            const uint32_t w = slot_word[slot];
-            const uint32_t m = w_nids[w];
-            if (MODE == SCAN_WRITE) {
-                const uint32_t* src = ids_pool + w_idoff[w];
-                for (uint32_t j = 0; j < m; ++j) out[woff + j] = src[j];
-                woff += m;
-            }
-            emitted += m;
+        const size_t stop = sg.end < limit ? sg.end : limit;
+        for (; p < stop; ++p) {
+            if (p + 1 < sg.end && byte(p) == 0x20 && ascii_nonspace(byte(p - 1)) &&
+                ascii_nonspace(byte(p + 1)))
+                return p;
         }
-        p = e;
+        if (p == sg.end) ++k;            // p is the next segment's start: a boundary
     }
-    if (MODE == SCAN_COUNT) per_thread[t] = emitted;
+    return ~(size_t)0;
+}
+
+template <bool kAligned>
+__global__ void __launch_bounds__(256, 3)
+k_enc_scan(const uint8_t* __restrict__ s, size_t n, size_t n_chunks, const Seg* __restrict__ segs,
+           int nseg, unsigned long long* __restrict__ kv, unsigned long long* __restrict__ pos,
+           size_t mask, unsigned long long max_fill, unsigned long long* __restrict__ fill,
+           uint32_t* __restrict__ recs, unsigned long long* __restrict__ t_start,
+           uint32_t* __restrict__ t_count, unsigned* __restrict__ status, int use_cache) {
+    __shared__ unsigned long long c_key[kEncCache];
+    __shared__ uint64_t c_lo[kEncCache], c_hi[kEncCache];
+    __shared__ uint32_t c_slot[kEncCache];
+    __shared__ uint16_t c_hit[kEncCache], c_mark[kEncCache];   // hit counts mod 2^16 per epoch
+    __shared__ uint32_t s_start[257];   // relative to the chunk; kNotFound: past the window
+    __shared__ unsigned long long s_red[4];
+    __shared__ int s_stop;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kEncCache; i += blockDim.x) { c_key[i] = 0; c_hit[i] = 0; c_mark[i] = 0; }
+    unsigned long long inserted = 0;
+
+    // one pre-token [p, p + len) of src (global position gp); returns its record
+    auto word_rec = [&](const auto& src, auto p, size_t len, size_t gp) -> uint32_t {
+        if (len >= (1ULL << 24)) { atomicOr(status, 2u); return 0u; }
+        bool ins = false;
+        if (len <= (size_t)kInline) {
+            uint64_t wl = 0, wh = 0;
+            for (uint32_t i = 0; i < (uint32_t)len; ++i) {
+                const uint64_t b = src[p + i];
+                if (i < 8) wl |= b << (8 * i);
+                else wh |= b << (8 * (i - 8));
+            }
+            const uint64_t h = short_hash(wl, wh, len);
+            const unsigned ls = (unsigned)(h >> 40) & (kEncCache - 2);
+            for (int way = 0; way < 2 && use_cache; ++way) {
+                const unsigned sl = ls + way;
+                const unsigned long long k = c_key[sl];
+                if (k != 0 && k != kBusy && (k >> 40) == len) {
+                    __asm__ volatile("" ::: "memory");
+                    if (c_lo[sl] == wl && c_hi[sl] == wh) {
+                        c_hit[sl] = (uint16_t)(c_hit[sl] + 1);   // a heuristic: races may drop hits
+                        return c_slot[sl];
+                    }
+                }
+            }
+            const size_t slot = table_add(s, s, gp, len, wl, wh, h, 0, kv, pos, mask, status, &ins);
+            inserted += ins;
+            if (slot == ~(size_t)0) return 0u;
+            for (int way = 0; way < 2 && use_cache; ++way) {   // cache it if a way is free
+                const unsigned sl = ls + way;
+                if (c_key[sl] == 0 && atomicCAS(&c_key[sl], 0ULL, kBusy) == 0) {
+                    c_lo[sl] = wl;
+                    c_hi[sl] = wh;
+                    c_slot[sl] = (uint32_t)slot;
+                    // the entry's LDS writes complete before the key publishes it
+                    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    atomicExch(&c_key[sl], ((unsigned long long)len << 40) | (gp + 1));
+                    break;
+                }
+            }
+            return (uint32_t)slot;
+        }
+        const size_t slot = table_add(s, s, gp, len, 0, 0, hash_word(s, gp, len), 0, kv, pos, mask,
+                                      status, &ins);
+        inserted += ins;
+        return slot == ~(size_t)0 ? 0u : (uint32_t)slot;
+    };
+
+    uint4 pre[kVec];
+    if (blockIdx.x < n_chunks) stage_fetch<kAligned>(pre, s, n, (size_t)blockIdx.x * kChunk, tid);
+    for (size_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+        __syncthreads();
+        stage_store(pre, tid);
+        if (tid == 0) s_stop = *(volatile unsigned long long*)fill > max_fill;
+        __syncthreads();
+        if (s_stop) {
+            if (tid == 0) atomicOr(status, 1u);
+            break;
+        }
+        if (c + gridDim.x < n_chunks) stage_fetch<kAligned>(pre, s, n, (c + gridDim.x) * kChunk, tid);
+
+        const size_t base = c * kChunk;
+        const size_t rem = n - base;
+        const bool text_ends = rem <= (size_t)kWin;
+        const size_t wend = base + (text_ends ? rem : (size_t)kWin);   // staged: [base, wend)
+        const LdsText L{};
+        // staged reads, one byte left of the window from global memory
+        auto byte_at = [&](size_t q) -> uint8_t {
+            return q >= base ? L[(uint32_t)(q - base)] : s[q];
+        };
+        // span starts: first boundary >= nominal start, searched inside the window
+        // (~0: past it; at the end of the text, n)
+        auto find = [&](size_t q) -> uint32_t {
+            if (q >= n) return (uint32_t)(n - base);
+            const size_t lim = text_ends ? n : wend - 2;
+            const size_t b = first_boundary(segs, nseg, q, lim, byte_at);
+            return b != ~(size_t)0 ? (uint32_t)(b - base) : (text_ends ? (uint32_t)(n - base) : kNotFound);
+        };
+        s_start[tid] = find(base + (size_t)tid * 64);
+        if (tid == 0) s_start[256] = find(base + kChunk);
+        __syncthreads();
+        const uint32_t r0 = s_start[tid], r1 = s_start[tid + 1];
+        const unsigned long long g0 = r0 == kNotFound ? ~0ULL : base + r0;
+        const unsigned long long g1 = r1 == kNotFound ? ~0ULL : base + r1;
+        const size_t gt = c * 256 + tid;
+        uint32_t k = 0;
+        if (g0 != ~0ULL) {
+            const bool fast = g1 != ~0ULL;
+            const size_t hi = base + (size_t)tid * 64 + 64;
+            size_t p = g0;
+            int sk = seg_of(segs, nseg, p);
+            Seg sg = segs[sk];                  // current segment, kept in registers
+            for (;;) {
+                if (fast ? p >= g1 : p >= n) break;
+                while (p >= sg.end && sk + 1 < nseg) sg = segs[++sk];
+                if (!fast && p >= hi && (p == sg.start || (sg.special < 0 && p + 1 < sg.end &&
+                                                           is_safe_point(s, (size_t)sg.end, p))))
+                    break;
+                size_t e;
+                uint32_t rec;
+                if (sg.special >= 0) {
+                    rec = kSpecialRec | (uint32_t)sg.special;
+                    e = sg.end;
+                } else if (fast) {
+                    const uint32_t r = (uint32_t)(p - base);
+                    const uint32_t se = (uint32_t)((sg.end < wend ? sg.end : wend) - base);
+                    e = base + token_end(L, se, r);
+                    rec = word_rec(L, r, e - p, p);
+                } else {
+                    e = token_end(s, (size_t)sg.end, p);
+                    rec = word_rec(s, p, e - p, p);
+                }
+                // a span of B bytes holds at most B records; anything else is a bug: report it
+                // (status 16) rather than write past the span
+                if (e <= p || g0 + k >= (fast ? g1 : n)) { atomicOr(status, 16u); break; }
+                recs[g0 + k] = rec;
+                ++k;
+                p = e;
+            }
+        }
+        t_start[gt] = g0 == ~0ULL ? 0 : g0;
+        t_count[gt] = k;
+        // cache eviction every kEncEpoch chunks (see k_count_words)
+        if ((c - blockIdx.x) / gridDim.x % kEncEpoch == kEncEpoch - 1) {
+            __syncthreads();
+            for (int i = tid; i < kEncCache; i += blockDim.x) {
+                const unsigned long long kk = c_key[i];
+                if (kk == 0 || kk == kBusy) continue;
+                const uint16_t hh = c_hit[i];
+                if ((uint16_t)(hh - c_mark[i]) >= kEncKeep) { c_mark[i] = hh; continue; }
+                c_key[i] = 0;
+                c_hit[i] = 0;
+                c_mark[i] = 0;
+            }
+        }
+        const unsigned long long ins = wave_sum(inserted);
+        inserted = 0;
+        if ((tid & 63) == 0) s_red[tid >> 6] = ins;
+        __syncthreads();
+        if (tid == 0) {
+            const unsigned long long b = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+            if (b) atomicAdd(fill, b);
+        }
+    }
 }
 
 // ------------------------------------------------------------------ 3. unique words
-__global__ void k_collect(const unsigned long long* __restrict__ key, size_t cap,
-                          uint32_t* __restrict__ slot_word, unsigned long long* __restrict__ w_off,
+__global__ void k_collect(const unsigned long long* __restrict__ kv, const unsigned long long* __restrict__ pos,
+                          size_t cap, uint32_t* __restrict__ slot_word, unsigned long long* __restrict__ w_off,
                           uint32_t* __restrict__ w_len, unsigned* __restrict__ n_words) {
     const size_t sidx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const unsigned long long k = sidx < cap ? key[sidx] : 0ULL;
+    const unsigned long long k = sidx < cap ? kv[2 * sidx] : 0ULL;
     const unsigned w = wave_append(k != 0, n_words);
     if (!k) return;
     slot_word[sidx] = w;
-    w_off[w] = (k & kOff40) - 1;
-    w_len[w] = (uint32_t)(k >> 40);
+    const bool inl = (k >> 63) != 0;   // key format: stage.h
+    w_off[w] = inl ? pos[sidx] : (k & kOff40) - 1;
+    w_len[w] = inl ? (uint32_t)((k >> 56) & 0x7f) : (uint32_t)(k >> 40);
+}
+
+// ------------------------------------------------------------------ 5. ids per span, then write
+__device__ __forceinline__ uint32_t rec_nids(uint32_t rec, const uint32_t* __restrict__ slot_word,
+                                             const uint32_t* __restrict__ w_nids, size_t cap, unsigned nw,
+                                             unsigned* __restrict__ status) {
+    if (rec & kSpecialRec) return 1u;
+    const uint32_t w = rec < cap ? slot_word[rec] : 0xffffffffu;
+    if (w >= nw) { atomicOr(status, 32u); return 0u; }   // a record naming no word: a bug
+    return w_nids[w];
+}
+
+__global__ void k_enc_count(const uint32_t* __restrict__ recs, const unsigned long long* __restrict__ t_start,
+                            const uint32_t* __restrict__ t_count, size_t n_spans,
+                            const uint32_t* __restrict__ slot_word, const uint32_t* __restrict__ w_nids,
+                            size_t cap, unsigned nw, unsigned* __restrict__ status,
+                            unsigned long long* __restrict__ per) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_spans) return;
+    const uint32_t* r = recs + t_start[t];
+    const uint32_t m = t_count[t];
+    unsigned long long ids = 0;
+    for (uint32_t i = 0; i < m; ++i) ids += rec_nids(r[i], slot_word, w_nids, cap, nw, status);
+    per[t] = ids;
+}
+
+__global__ void k_enc_write(const uint32_t* __restrict__ recs, const unsigned long long* __restrict__ t_start,
+                            const uint32_t* __restrict__ t_count, size_t n_spans,
+                            const uint32_t* __restrict__ slot_word, const uint32_t* __restrict__ w_nids,
+                            const unsigned long long* __restrict__ w_idoff, const uint32_t* __restrict__ ids_pool,
+                            const int64_t* __restrict__ sp_vid, const unsigned long long* __restrict__ per_off,
+                            size_t cap, unsigned nw, uint32_t* __restrict__ out) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_spans) return;
+    const uint32_t* r = recs + t_start[t];
+    const uint32_t m = t_count[t];
+    unsigned long long o = per_off[t];
+    for (uint32_t i = 0; i < m; ++i) {
+        const uint32_t rec = r[i];
+        if (rec & kSpecialRec) {
+            out[o++] = (uint32_t)sp_vid[rec & ~kSpecialRec];
+            continue;
+        }
+        const uint32_t w = rec < cap ? slot_word[rec] : 0xffffffffu;
+        if (w >= nw) continue;   // reported by k_enc_count
+        const uint32_t* src = ids_pool + w_idoff[w];
+        const uint32_t nm = w_nids[w];
+        for (uint32_t j = 0; j < nm; ++j) out[o + j] = src[j];
+        o += nm;
+    }
 }
 
 __device__ __forceinline__ uint2 rank_of(const EncTables& E, uint32_t a, uint32_t b) {
@@ -210,11 +374,12 @@ __global__ void __launch_bounds__(256)
 k_encode_words(const uint8_t* __restrict__ s, EncTables E, const unsigned long long* __restrict__ w_off,
                const uint32_t* __restrict__ w_len, const unsigned long long* __restrict__ w_idoff,
                unsigned n_words, uint32_t* __restrict__ pool, uint32_t* __restrict__ w_nids,
-               unsigned* __restrict__ status) {
+               unsigned* __restrict__ status, size_t n) {
     const unsigned w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= n_words) return;
-    const uint8_t* src = s + w_off[w];
     const uint32_t len = w_len[w];
+    if (w_off[w] + len > n) { atomicOr(status, 64u); w_nids[w] = 0; return; }   // a bug: report
+    const uint8_t* src = s + w_off[w];
     for (int k = 0; k < E.n_sp; ++k)  // match() drops pre-tokens equal to a special (73)
         if (E.sp_len[k] == len && bytes_eq(src, E.sp_bytes + E.sp_off[k], len)) { w_nids[w] = 0; return; }
     uint32_t* t = pool + w_idoff[w];
@@ -440,33 +605,51 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
     DevBuf<Seg> d_segs(nseg);
     BPE_HIP(hipMemcpyAsync(d_segs.p, segs.data(), nseg * sizeof(Seg), hipMemcpyHostToDevice, s));
 
-    // 2. unique pre-tokens
-    const size_t threads = (n + kSpan - 1) / kSpan;
-    const unsigned grid = ceil_div(threads, 256);
-    size_t cap = next_pow2(std::max<size_t>(1 << 12, n / 48));
-    DevBuf<unsigned long long> key;
+    // 2. one staged pass: unique pre-tokens into the word table, one record per pre-token
+    const size_t n_chunks = (n + kChunk - 1) / kChunk;
+    const size_t n_spans = n_chunks * 256;
+    const bool aligned = (reinterpret_cast<uintptr_t>(d_text) & 15u) == 0;
+    auto kern = aligned ? k_enc_scan<true> : k_enc_scan<false>;
+    int per_cu = 0, dev = 0, n_cu = 0;
+    BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, kPadded));
+    BPE_HIP(hipGetDevice(&dev));
+    BPE_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    unsigned sgrid = (unsigned)std::min<size_t>(n_chunks, (size_t)std::max(1, per_cu) * std::max(1, n_cu));
+    if (const char* e = std::getenv("BPE355_STREAM_WG"))   // test knob (see count_words)
+        sgrid = std::max(1u, std::min(sgrid, (unsigned)std::atoi(e)));
+    // first guess: small texts have many more unique words per byte than large corpora
+    size_t cap = next_pow2(std::max<size_t>(1 << 16, n < (1u << 26) ? n / 16 : n / 1024));
+    DevBuf<unsigned long long> kv, pos;
+    DevBuf<uint32_t> recs(n), t_count(n_spans);
+    DevBuf<unsigned long long> t_start(n_spans), fill(1);
     DevBuf<unsigned> status(1);
     for (int attempt = 0;; ++attempt) {
-        key.alloc(cap);
-        BPE_HIP(hipMemsetAsync(key.p, 0, key.bytes(), s));
+        kv.alloc(2 * cap);
+        pos.alloc(cap);
+        BPE_HIP(hipMemsetAsync(kv.p, 0, kv.bytes(), s));
         BPE_HIP(hipMemsetAsync(status.p, 0, 4, s));
-        hipLaunchKernelGGL(k_scan<SCAN_INSERT>, dim3(grid), dim3(256), 0, s, d_text, n, d_segs.p, nseg, E,
-                           key.p, cap - 1, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, status.p);
+        BPE_HIP(hipMemsetAsync(fill.p, 0, 8, s));
+        hipLaunchKernelGGL(kern, dim3(sgrid), dim3(256), kPadded, s, d_text, n, n_chunks, d_segs.p, nseg,
+                           kv.p, pos.p, cap - 1, (unsigned long long)(cap / 2), fill.p, recs.p,
+                           t_start.p, t_count.p, status.p,
+                           std::getenv("BPE355_NOCACHE") ? 0 : 1);   // test knob: global table only
         BPE_HIP(hipGetLastError());
         unsigned st = 0;
         BPE_HIP(hipMemcpyAsync(&st, status.p, 4, hipMemcpyDeviceToHost, s));
         BPE_HIP(hipStreamSynchronize(s));
         if (st & 2u) throw Error{BPE_E_LIMIT, "a pre-token is longer than 16 MiB"};
+        BPE_REQUIRE(!(st & 16u), BPE_E_HIP, "internal error: encode scan overran a span");
         if (!(st & 1u)) break;
-        BPE_REQUIRE(attempt < 4, BPE_E_NOMEM, "word table overflow");
+        BPE_REQUIRE(attempt < 6, BPE_E_NOMEM, "word table overflow");
         cap *= 4;
     }
     DevBuf<uint32_t> slot_word(cap);
+    BPE_HIP(hipMemsetAsync(slot_word.p, 0xff, slot_word.bytes(), s));
     DevBuf<unsigned long long> w_off(cap);
     DevBuf<uint32_t> w_len(cap);
     DevBuf<unsigned> d_nw(1);
     BPE_HIP(hipMemsetAsync(d_nw.p, 0, 4, s));
-    hipLaunchKernelGGL(k_collect, dim3(ceil_div(cap, 256)), dim3(256), 0, s, key.p, cap, slot_word.p,
+    hipLaunchKernelGGL(k_collect, dim3(ceil_div(cap, 256)), dim3(256), 0, s, kv.p, pos.p, cap, slot_word.p,
                        w_off.p, w_len.p, d_nw.p);
     unsigned nw = 0;
     BPE_HIP(hipMemcpyAsync(&nw, d_nw.p, 4, hipMemcpyDeviceToHost, s));
@@ -492,29 +675,31 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
     BPE_HIP(hipMemsetAsync(status.p, 0, 4, s));
     if (nw) {
         hipLaunchKernelGGL(k_encode_words, dim3(ceil_div(nw, 256)), dim3(256), 0, s, d_text, E, w_off.p,
-                           w_len.p, idoff.p, nw, pool.p, nids.p, status.p);
+                           w_len.p, idoff.p, nw, pool.p, nids.p, status.p, n);
         BPE_HIP(hipGetLastError());
     }
-    // 4. output offsets per thread, then write
-    DevBuf<unsigned long long> per(threads), per_off(threads);
-    hipLaunchKernelGGL(k_scan<SCAN_COUNT>, dim3(grid), dim3(256), 0, s, d_text, n, d_segs.p, nseg, E,
-                       key.p, cap - 1, slot_word.p, nids.p, idoff.p, pool.p, per.p, nullptr, status.p);
+    // 4. ids per span, offsets, then write: two streams over the records
+    DevBuf<unsigned long long> per(n_spans), per_off(n_spans);
+    hipLaunchKernelGGL(k_enc_count, dim3(ceil_div(n_spans, 256)), dim3(256), 0, s, recs.p, t_start.p,
+                       t_count.p, n_spans, slot_word.p, nids.p, cap, nw, status.p, per.p);
     size_t tb = 0;
-    BPE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, per.p, per_off.p, (int64_t)threads, s));
+    BPE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, per.p, per_off.p, (int64_t)n_spans, s));
     DevBuf<uint8_t> tmp(tb);
-    BPE_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, per.p, per_off.p, (int64_t)threads, s));
+    BPE_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, per.p, per_off.p, (int64_t)n_spans, s));
     unsigned long long last[2];
     unsigned st = 0;
-    BPE_HIP(hipMemcpyAsync(&last[0], per_off.p + threads - 1, 8, hipMemcpyDeviceToHost, s));
-    BPE_HIP(hipMemcpyAsync(&last[1], per.p + threads - 1, 8, hipMemcpyDeviceToHost, s));
+    BPE_HIP(hipMemcpyAsync(&last[0], per_off.p + n_spans - 1, 8, hipMemcpyDeviceToHost, s));
+    BPE_HIP(hipMemcpyAsync(&last[1], per.p + n_spans - 1, 8, hipMemcpyDeviceToHost, s));
     BPE_HIP(hipMemcpyAsync(&st, status.p, 4, hipMemcpyDeviceToHost, s));
     BPE_HIP(hipStreamSynchronize(s));
     if (st & 4u) throw Error{BPE_E_KEY, "a merged token is not in the vocab"};
-    BPE_REQUIRE(!(st & 8u), BPE_E_HIP, "encode lost a pre-token between passes");
+    BPE_REQUIRE(!(st & 112u), BPE_E_HIP, "internal error: encode records inconsistent (status " +
+                                           std::to_string(st) + ")");
     const size_t total = last[0] + last[1];
     BPE_REQUIRE(total <= n, BPE_E_HIP, "encode produced more ids than input bytes");
-    hipLaunchKernelGGL(k_scan<SCAN_WRITE>, dim3(grid), dim3(256), 0, s, d_text, n, d_segs.p, nseg, E,
-                       key.p, cap - 1, slot_word.p, nids.p, idoff.p, pool.p, per_off.p, d_out, status.p);
+    hipLaunchKernelGGL(k_enc_write, dim3(ceil_div(n_spans, 256)), dim3(256), 0, s, recs.p, t_start.p,
+                       t_count.p, n_spans, slot_word.p, nids.p, idoff.p, pool.p, E.sp_vid, per_off.p, cap, nw,
+                       d_out);
     BPE_HIP(hipGetLastError());
     BPE_HIP(hipStreamSynchronize(s));
     return total;

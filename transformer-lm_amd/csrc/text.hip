@@ -19,6 +19,7 @@
 
 #include "internal.h"
 #include "pretok.h"
+#include "stage.h"
 
 namespace bpe {
 
@@ -140,98 +141,20 @@ const uint8_t* prepare_text(const uint8_t* d_in, size_t n, DevBuf<uint8_t>& scra
 }
 
 // ------------------------------------------------------------------ word counting
-// Global table: open addressing over 16-byte entries {key, count} (one line per probe; the
-// table stays small enough to live in the Infinity Cache -- 32-byte entries measured 1.9x
-// slower).  Words of <= 7 bytes are stored INLINE: key = kInl | len << 56 | bytes, so a hit
-// needs no read of the corpus, and the claimer records an occurrence in the cold `pos` array
-// (read only after the kernel).  Longer words are keyed by len << 40 | (offset + 1) of their
-// first occurrence and verified against the corpus.  Words of <= 16 bytes hash by their packed
-// bytes, longer ones by FNV-1a: a word always takes the same path.
-constexpr unsigned long long kOffMask = (1ULL << 40) - 1;
-constexpr unsigned long long kInl = 1ULL << 63;
-constexpr int kInlineKey = 7;        // longest word stored inline in the key
-constexpr int kMaxProbe = 1 << 16;
-constexpr int kInline = 16;          // words up to this length are packed into two u64
-constexpr int kChunk = 16384;        // corpus bytes a workgroup scans per iteration
-constexpr int kHalo = 1024;          // staged bytes past the chunk (tokens running over its end)
-constexpr int kWin = kChunk + kHalo;
-constexpr int kPadded = kWin + (kWin / 64) * 4;   // +4 B per 64 B: threads' spans hit distinct banks
-constexpr int kCache = 1024;         // LDS word-cache entries (2-way)
-constexpr int kEpoch = 4;            // chunks between cache evictions
-constexpr unsigned kKeep = 2;        // an entry stays if it was hit this often in the epoch
-constexpr int kVec = (kWin + 16 * 256 - 1) / (16 * 256);   // 16-B loads per thread per chunk
-constexpr unsigned long long kBusy = 1ULL << 63;
-
-__device__ __forceinline__ uint64_t short_hash(uint64_t lo, uint64_t hi, size_t len) {
-    return mix64(lo ^ mix64(hi ^ (len << 56) ^ 0x9E3779B97F4A7C15ULL));
-}
-
-// The staged window lives in dynamic LDS (kPadded bytes per workgroup), addressed directly:
-// a generic pointer to it inside the accessor trips the gfx950 backend.
-extern __shared__ __attribute__((aligned(16))) uint8_t g_stage[];
-
-// the staged window, addressed by position relative to the chunk start (32-bit)
-struct LdsText {
-    __device__ __forceinline__ uint8_t operator[](uint32_t r) const { return g_stage[r + ((r >> 6) << 2)]; }
-};
-constexpr uint32_t kNotFound = 0xffffffffu;
-
-template <class Src>
-__device__ __forceinline__ void pack_word(const Src& t, size_t p, size_t len, uint64_t& lo, uint64_t& hi) {
-    lo = 0;
-    hi = 0;
-    for (size_t i = 0; i < len; ++i) {
-        const uint64_t b = t[p + i];
-        if (i < 8) lo |= b << (8 * i);
-        else hi |= b << (8 * (i - 8));
-    }
-}
-
-// count `c` occurrences of a word in the global table.  Returns true if it inserted the key.
-// wl/wh: the packed bytes (words <= 16 bytes); t/p: the word's bytes for longer ones.
 template <class Src>
 __device__ __forceinline__ bool global_add(const uint8_t* __restrict__ s, const Src& t, size_t p, size_t len,
                                            uint64_t wl, uint64_t wh, uint64_t h, unsigned long long c,
                                            unsigned long long* __restrict__ kv,
                                            unsigned long long* __restrict__ pos, size_t mask,
                                            unsigned* __restrict__ status) {
-    const bool inl = len <= (size_t)kInlineKey;
-    const unsigned long long mine = inl ? kInl | ((unsigned long long)len << 56) | wl
-                                        : ((unsigned long long)len << 40) | (p + 1);
-    size_t slot = h & mask;
-    for (int probe = 0; probe < kMaxProbe; ++probe) {
-        unsigned long long k = kv[2 * slot];
-        if (k == 0) {
-            k = atomicCAS(&kv[2 * slot], 0ULL, mine);
-            if (k == 0) {   // claimed
-                if (inl) pos[slot] = p;
-                atomicAdd(&kv[2 * slot + 1], c);
-                return true;
-            }
-        }
-        bool eq = false;
-        if (inl) {
-            eq = k == mine;
-        } else if (!(k & kInl) && (k >> 40) == len) {
-            const size_t q = (k & kOffMask) - 1;
-            if (len <= (size_t)kInline) {
-                uint64_t l2, h2;
-                pack_word(s, q, len, l2, h2);
-                eq = l2 == wl && h2 == wh;
-            } else {
-                eq = true;
-                for (size_t i = 0; i < len && eq; ++i) eq = s[q + i] == t[p + i];
-            }
-        }
-        if (eq) {
-            atomicAdd(&kv[2 * slot + 1], c);
-            return false;
-        }
-        slot = (slot + 1) & mask;
-    }
-    atomicOr(status, 1u);
-    return false;
+    bool ins;
+    table_add(s, t, p, len, wl, wh, h, c, kv, pos, mask, status, &ins);
+    return ins;
 }
+
+constexpr int kCache = 1024;         // LDS word-cache entries (2-way)
+constexpr int kEpoch = 4;            // chunks between cache evictions
+constexpr unsigned kKeep = 2;        // an entry stays if it was hit this often in the epoch
 
 // Persistent workgroups stream the corpus in kChunk pieces: coalesced 16-B loads of the next
 // chunk (+halo) go to registers while the current one is scanned out of LDS.  Each of the 256
@@ -261,22 +184,6 @@ __global__ void __launch_bounds__(256, 3) k_count_words(const uint8_t* __restric
     unsigned long long ntok = 0, inserted = 0, n_miss = 0, n_long = 0;
 
     uint4 pre[kVec];
-    auto fetch = [&](size_t c) {
-        const size_t base = c * kChunk;
-#pragma unroll
-        for (int v = 0; v < kVec; ++v) {
-            const size_t off = ((size_t)v * 256 + tid) * 16;
-            if (off >= (size_t)kWin) continue;
-            const size_t g = base + off;
-            if (kAligned && g + 16 <= n) {
-                pre[v] = *reinterpret_cast<const uint4*>(s + g);
-            } else {
-                uint8_t tmp[16];
-                for (int j = 0; j < 16; ++j) tmp[j] = g + j < n ? s[g + j] : 0;
-                __builtin_memcpy(&pre[v], tmp, 16);
-            }
-        }
-    };
     // one pre-token of length len at position r of src (global offset gpos)
     auto count_token = [&](const auto& src, auto r, size_t len, size_t gpos) {
         if (len < 2) return;
@@ -298,10 +205,10 @@ __global__ void __launch_bounds__(256, 3) k_count_words(const uint8_t* __restric
                 unsigned long long k = c_key[sl];
                 if (k == 0) {
                     k = atomicCAS(&c_key[sl], 0ULL, kBusy);
-                    if (k == 0) {   // claimed: bytes first, then publish the key (a wave's LDS
-                        c_lo[sl] = wl;  // operations execute in order; the barrier keeps the
-                        c_hi[sl] = wh;  // compiler from reordering them)
-                        __asm__ volatile("" ::: "memory");
+                    if (k == 0) {   // claimed: bytes first (drained), then publish the key
+                        c_lo[sl] = wl;
+                        c_hi[sl] = wh;
+                        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                         atomicExch(&c_key[sl], mine);
                         atomicAdd(&c_cnt[sl], 1u);
                         return;
@@ -322,23 +229,18 @@ __global__ void __launch_bounds__(256, 3) k_count_words(const uint8_t* __restric
             inserted += global_add(s, s, gpos, len, 0, 0, hash_word(s, gpos, len), 1, kv, pos, mask, status);
         }
     };
-    if (blockIdx.x < n_chunks) fetch(blockIdx.x);
+    if (blockIdx.x < n_chunks) stage_fetch<kAligned>(pre, s, n, (size_t)blockIdx.x * kChunk, tid);
     for (size_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
         __syncthreads();   // the previous chunk's scan is done with buf
-#pragma unroll
-        for (int v = 0; v < kVec; ++v) {
-            const size_t off = ((size_t)v * 256 + tid) * 16;
-            if (off >= (size_t)kWin) continue;
-            uint32_t* d = reinterpret_cast<uint32_t*>(g_stage + off + ((off >> 6) << 2));
-            d[0] = pre[v].x; d[1] = pre[v].y; d[2] = pre[v].z; d[3] = pre[v].w;
-        }
+        stage_store(pre, tid);
         if (tid == 0) s_stop = *(volatile unsigned long long*)fill > max_fill;
         __syncthreads();
         if (s_stop) {
             if (tid == 0) atomicOr(status, 1u);
             break;
         }
-        if (c + gridDim.x < n_chunks) fetch(c + gridDim.x);   // in flight during the scan
+        if (c + gridDim.x < n_chunks)   // in flight during the scan
+            stage_fetch<kAligned>(pre, s, n, (c + gridDim.x) * kChunk, tid);
 
         const size_t base = c * kChunk;
         const size_t rem = n - base;
@@ -449,9 +351,10 @@ __global__ void __launch_bounds__(256, 3) k_count_words(const uint8_t* __restric
 void count_words(const uint8_t* d_text, size_t n, WordCounts& wc, hipStream_t stream,
                  float* kernel_ms) {
     BPE_REQUIRE(n < (1ULL << 40) - 1, BPE_E_LIMIT, "corpus slab larger than 1 TiB");
-    // first guess ~1 slot per KiB of text (7.4 M words in 11.9 GB of OWT-like text: load 0.46);
-    // the kernel stops early past load 1/2 and the count reruns with 4x the slots
-    size_t cap = next_pow2(std::max<size_t>(1 << 16, n / 1024));
+    // first guess ~1 slot per KiB of a large corpus (7.4 M words in 11.9 GB of OWT-like text:
+    // load 0.46), 1 per 16 bytes below 64 MiB (small texts have many more unique words per
+    // byte); the kernel stops early past load 1/2 and the count reruns with 4x the slots
+    size_t cap = next_pow2(std::max<size_t>(1 << 16, n < (1u << 26) ? n / 16 : n / 1024));
     DevBuf<unsigned> status(1);
     DevBuf<unsigned long long> ntok(3), fill(1);
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -468,8 +371,10 @@ void count_words(const uint8_t* d_text, size_t n, WordCounts& wc, hipStream_t st
     BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, kPadded));
     BPE_HIP(hipGetDevice(&dev));
     BPE_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-    const unsigned grid = (unsigned)std::min<size_t>(std::max<size_t>(n_chunks, 1),
-                                                     (size_t)std::max(1, per_cu) * std::max(1, n_cu));
+    unsigned grid = (unsigned)std::min<size_t>(std::max<size_t>(n_chunks, 1),
+                                               (size_t)std::max(1, per_cu) * std::max(1, n_cu));
+    if (const char* e = std::getenv("BPE355_STREAM_WG"))   // test knob: fewer workgroups, each
+        grid = std::max(1u, std::min(grid, (unsigned)std::atoi(e)));   // streaming many chunks
     for (int attempt = 0;; ++attempt) {
         wc.kv.alloc(2 * cap);
         wc.pos.alloc(cap);

@@ -66,7 +66,7 @@ struct RoundState {
     int n_rounds;
     int ntok;
     long long T;
-    unsigned nC, capC, c_limit, n_touched;
+    unsigned nC, capC, c_limit, pad0;
     unsigned nC_base;           // |C| before this round's k_argmax appends (set by k_merge)
     unsigned k3_done;           // k_argmax blocks finished this launch (the last one advances)
     unsigned cur_a, cur_b, cur_new, cur_slot;
@@ -90,7 +90,8 @@ struct PairsDev {
     long long* cnt;
     unsigned* flag;           // kPresent | kInC
     size_t mask;
-    unsigned* C;
+    uint4* C;                 // candidate list: {slot, a, b, 0} (ids carried so the argmax loads
+                              // the slot's count and the tokens' prefixes in one step)
 };
 
 struct ToksDev {
@@ -373,7 +374,7 @@ struct BestShared {
     long long cnt;
     unsigned long long hash, k8;
     int round, ntok;
-    unsigned list_beg, list_len, use_list, cov_beg, cov_len;
+    unsigned ln, list_beg, list_len, use_list, cov_beg, cov_len;
 };
 
 template <class TokT>
@@ -419,23 +420,9 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
                 const unsigned long long ka = pp.ka, kb = pp.kb;
                 const unsigned za = X.len[a], zb = X.len[b];   // kNoAnc (uncovered) sorts last
                 const unsigned ba = X.beg[a], bbg = X.beg[b];
-                const unsigned long long h = ha * pb + hb;
-                const unsigned ln = la + lb;
-                // level 2: first map slot
-                unsigned s = (unsigned)mix64(h) & K.map_mask;
-                unsigned m = K.map[s];
-                // token dedupe: does bytes(a) + bytes(b) already exist? (usually: empty slot)
-                unsigned nw = (unsigned)ntok;
-                for (; m != 0; s = (s + 1) & K.map_mask, m = K.map[s]) {
-                    const unsigned id = m - 1;
-                    if (K.hash[id] == h && K.len[id] == ln && equals_concat(K, id, a, b)) {
-                        nw = id;
-                        break;
-                    }
-                }
-                sb.a = a; sb.b = b; sb.nw = nw; sb.slot = pp.slot; sb.cnt = pp.cnt;
-                sb.isnew = (nw == (unsigned)ntok);
-                sb.hash = h;
+                sb.a = a; sb.b = b; sb.slot = pp.slot; sb.cnt = pp.cnt;
+                sb.hash = ha * pb + hb;
+                sb.ln = la + lb;
                 sb.k8 = la >= 8 ? ka : (ka | (kb >> (8 * la)));
                 sb.round = round; sb.ntok = ntok;
                 // which words can contain (a, b): the smaller covering posting list, or all
@@ -445,7 +432,7 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
                 sb.list_beg = sb.use_list ? bu : 0;
                 sb.list_len = sb.use_list ? lu : 0;
                 sb.cov_beg = bu;
-                sb.cov_len = sb.isnew ? lu : kNoAnc;   // dedupe: uncovered until the next build
+                sb.cov_len = lu;
             }
         }
     }
@@ -454,12 +441,43 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
         if (blockIdx.x == 0 && tid == 0 && sb.stop > 0) st->halt = sb.stop;
         return;
     }
+    // While thread 0 resolves the new token's id (token dedupe: does bytes(a) + bytes(b) exist
+    // already? usually an empty map slot), every thread pulls its first posting-list entry and
+    // that word's slot line toward the CU; the barrier below waits for both.
+    {
+        const unsigned i = blockIdx.x * blockDim.x + tid;
+        if (sb.use_list && blockIdx.x < W.lblk0 && i < sb.list_len) {
+            const unsigned f = X.list[sb.list_beg + i];
+            const TokT* line = f < W.off[1] ? W.c[0].slot + (size_t)f * slot_w(0)
+                             : f < W.off[2] ? W.c[1].slot + (size_t)(f - W.off[1]) * slot_w(1)
+                             : f < W.off[3] ? W.c[2].slot + (size_t)(f - W.off[2]) * slot_w(2)
+                                            : W.c[3].slot + (size_t)(f - W.off[3]) * slot_w(3);
+            (void)*reinterpret_cast<const volatile unsigned*>(line);   // kept: volatile
+        }
+        if (tid == 0) {
+            const unsigned a = sb.a, b = sb.b, ln = sb.ln, ntok = (unsigned)sb.ntok;
+            const unsigned long long h = sb.hash;
+            unsigned s = (unsigned)mix64(h) & K.map_mask;
+            unsigned m = K.map[s];
+            unsigned nw = ntok;
+            for (; m != 0; s = (s + 1) & K.map_mask, m = K.map[s]) {
+                const unsigned id = m - 1;
+                if (K.hash[id] == h && K.len[id] == ln && equals_concat(K, id, a, b)) {
+                    nw = id;
+                    break;
+                }
+            }
+            sb.nw = nw;
+            sb.isnew = nw == ntok;
+            if (!sb.isnew) sb.cov_len = kNoAnc;   // dedupe: uncovered until the next build
+        }
+    }
+    __syncthreads();
     const unsigned a = sb.a, b = sb.b, nw = sb.nw;
 
     if (blockIdx.x == 0) {  // record the merge, pop the pair, register a new token
         if (tid == 0) {
             st->nC_base = st->nC;     // C entries k_argmax may read without racing its appends
-            st->n_touched = 0;
             P.cnt[sb.slot] = 0;                       // byte_pair_frequencies.pop(best_pair)
             atomicAnd(&P.flag[sb.slot], ~kPresent);   // (no other update touches this key)
             st->cur_a = a; st->cur_b = b; st->cur_new = nw; st->cur_slot = sb.slot;
@@ -535,7 +553,7 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
 // ------------------------------------------------------------------ K2: apply deltas
 __global__ void __launch_bounds__(256) k_apply(RoundState* __restrict__ st, PairsDev P,
                                                unsigned long long* __restrict__ LR,
-                                               unsigned* __restrict__ touched, unsigned ntb) {
+                                               unsigned long long* __restrict__ touched, unsigned ntb) {
     const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
     const unsigned x = g >> 2, op = g & 3;   // op: 0 (x,a)-=L  1 (x,new)+=L  2 (b,x)-=R  3 (new,x)+=R
     // ntb (a launch argument) bounds every token id k_merge can have written; cells below it
@@ -553,62 +571,74 @@ __global__ void __launch_bounds__(256) k_apply(RoundState* __restrict__ st, Pair
             case 2: if (!(x == b && a == b)) pair_dec(P, st, b, x, d); break;
             default: inc_slot = pair_inc(P, st, nw, x, d); break;
         }
-        if (op & 1) *cell = 0;   // both lanes of this cell read it in the same load instruction
+        if (op & 1) {
+            *cell = 0;   // both lanes of this cell read it in the same load instruction
+            // the incremented key, tagged with the round, at the cell's own index: k_argmax
+            // scans the cells instead of a list built with a returning atomic
+            if (inc_slot != ~(size_t)0)
+                touched[2 * (size_t)x + (op >> 1)] = ((unsigned long long)(st->round + 1) << 32) | inc_slot;
+        }
     }
-    const bool t = inc_slot != ~(size_t)0;
-    const unsigned idx = wave_append(t, &st->n_touched);
-    if (t) touched[idx] = (unsigned)inc_slot;
 }
 
 // ------------------------------------------------------------------ K3: argmax over C
 // With advance=1 it also finishes the round: the new token enters the dedupe map, and
 // round/ntok step forward (by the last block to finish).
 __global__ void __launch_bounds__(256) k_argmax(RoundState* __restrict__ st, PairsDev P, ToksDev K,
-                                                const unsigned* __restrict__ touched,
+                                                const unsigned long long* __restrict__ touched,
                                                 Partial* __restrict__ part, int advance) {
     __shared__ Cand sw[4];
     if (st->halt) return;
     const unsigned nC = advance ? st->nC_base : st->nC;
     const long long T = st->T;
-    const unsigned nt = advance ? st->n_touched : 0u;
+    const int round = st->round;
+    const unsigned nw = st->cur_new;
+    // cells k_apply may have tagged this round: 2 per token id
+    const unsigned n_cells = advance ? 2u * ((unsigned)st->ntok + (unsigned)st->new_is_new) : 0u;
     if (advance && blockIdx.x == 0 && threadIdx.x == 0 && st->new_is_new) {
-        const unsigned nw = st->cur_new;
         unsigned s = (unsigned)mix64(K.hash[nw]) & K.map_mask;
         while (K.map[s] != 0) s = (s + 1) & K.map_mask;
         K.map[s] = nw + 1;
     }
     Cand best = cand_none();
-    auto consider = [&](unsigned s, long long c) {
-        const unsigned long long key = P.key[s] - 1ULL;
-        const unsigned a = (unsigned)(key >> 32), b = (unsigned)(key & 0xffffffffu);
-        const Cand x{c, K.key8[a], K.key8[b], s, a, b};
-        if (cand_better(x, best, K.pool, K.off, K.len)) best = x;
-    };
-    // keys incremented this round: admitted to C by their final count (identical on every
-    // rank); they are also candidates of this very argmax
-    for (unsigned i0 = blockIdx.x * blockDim.x; i0 < nt; i0 += gridDim.x * blockDim.x) {
+    // keys incremented this round (k_apply tagged them with round + 1): admitted to C by
+    // their final count (identical on every rank); they are also candidates of this argmax.
+    // The key is (x, new) for cell 2x and (new, x) for cell 2x+1.
+    const unsigned long long tag = (unsigned long long)(round + 1);
+    for (unsigned i0 = blockIdx.x * blockDim.x; i0 < n_cells; i0 += gridDim.x * blockDim.x) {
         const unsigned i = i0 + threadIdx.x;
         bool add = false;
-        unsigned s = 0;
-        if (i < nt) {
-            s = touched[i];
-            const unsigned f = P.flag[s];
-            const long long c = P.cnt[s];
-            if ((f & kPresent) && c >= T) {
-                consider(s, c);
-                if (!(f & kInC)) add = !(atomicOr(&P.flag[s], kInC) & kInC);
+        unsigned s = 0, a = 0, b = 0;
+        if (i < n_cells) {
+            const unsigned long long e = touched[i];
+            if ((e >> 32) == tag) {
+                s = (unsigned)e;
+                a = (i & 1) ? nw : i >> 1;
+                b = (i & 1) ? i >> 1 : nw;
+                const unsigned f = P.flag[s];
+                const long long c = P.cnt[s];
+                const unsigned long long ka = K.key8[a], kb = K.key8[b];
+                if ((f & kPresent) && c >= T) {
+                    const Cand x{c, ka, kb, s, a, b};
+                    if (cand_better(x, best, K.pool, K.off, K.len)) best = x;
+                    if (!(f & kInC)) add = !(atomicOr(&P.flag[s], kInC) & kInC);
+                }
             }
         }
         const unsigned idx = wave_append(add, &st->nC);
         if (add) {
-            if (idx < st->capC) P.C[idx] = s;
+            if (idx < st->capC) P.C[idx] = make_uint4(s, a, b, 0u);
             else atomicOr(&st->err, ERR_C_FULL);
         }
     }
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < nC; i += gridDim.x * blockDim.x) {
-        const unsigned s = P.C[i];
-        if (!(P.flag[s] & kPresent)) continue;
-        consider(s, P.cnt[s]);
+        const uint4 e = P.C[i];
+        const unsigned f = P.flag[e.x];
+        const long long c = P.cnt[e.x];
+        const unsigned long long ka = K.key8[e.y], kb = K.key8[e.z];
+        if (!(f & kPresent)) continue;
+        const Cand x{c, ka, kb, e.x, e.y, e.z};
+        if (cand_better(x, best, K.pool, K.off, K.len)) best = x;
     }
     for (int o = 32; o > 0; o >>= 1) {
         const Cand oc = shfl_xor_cand(best, o);
@@ -921,7 +951,8 @@ __global__ void k_build_C(PairsDev P, size_t cap, long long T, RoundState* st) {
         const bool in = (f & kPresent) && P.cnt[s] >= T;
         const unsigned idx = wave_append(in, &st->nC);
         if (in) {
-            if (idx < st->capC) P.C[idx] = (unsigned)s;
+            const unsigned long long key = P.key[s] - 1ULL;
+            if (idx < st->capC) P.C[idx] = make_uint4((unsigned)s, (unsigned)(key >> 32), (unsigned)key, 0u);
             else atomicOr(&st->err, ERR_C_FULL);
             if (!(f & kInC)) P.flag[s] = f | kInC;
         } else if (f & kInC) {
@@ -1037,7 +1068,8 @@ class MergeLoop {
     size_t pcap_ = 0;
     DevBuf<unsigned long long> pkey_;
     DevBuf<long long> pcnt_;
-    DevBuf<unsigned> pflag_, C_;
+    DevBuf<unsigned> pflag_;
+    DevBuf<uint4> C_;
     // tokens
     unsigned tok_cap_ = 0;
     DevBuf<uint8_t> pool_;
@@ -1051,7 +1083,7 @@ class MergeLoop {
     DevBuf<uint32_t> ilist_, ibeg_, ilen_;
     IndexDev idev_{};
     int next_index_round_ = 256;
-    DevBuf<unsigned> touched_;
+    DevBuf<unsigned long long> touched_;   // per delta cell: (round + 1) << 32 | slot it incremented
 };
 
 template <class TokT>
@@ -1348,6 +1380,7 @@ void MergeLoop<TokT>::run() {
     tok_cap_ = 256u + (unsigned)n_rounds_ + 1u;
     LR_.alloc(2ull * tok_cap_);
     touched_.alloc(2ull * tok_cap_);
+    BPE_HIP(hipMemsetAsync(touched_.p, 0, touched_.bytes(), s_));
     BPE_HIP(hipMemsetAsync(LR_.p, 0, LR_.bytes(), s_));
     m_a_.alloc(n_rounds_); m_b_.alloc(n_rounds_); m_new_.alloc(n_rounds_); m_mode_.alloc(n_rounds_);
     toff_.alloc(tok_cap_); tlen_.alloc(tok_cap_);
@@ -1414,7 +1447,9 @@ void MergeLoop<TokT>::run() {
         // capacity headroom for one batch (worst case: 2 new keys per token per round)
         int R = std::min(kBatch, n_rounds_ - hs_.round);
         const unsigned long long per_round = 2ull * (hs_.ntok + R + 1);
-        while (hs_.pair_used + per_round * R > pcap_ * 3 / 4) {
+        // keep the load <= 1/2: an insert is an unsuccessful linear-probe search, ~2.5 probes at
+        // load 1/2 vs ~8.5 at 3/4 -- each probe a dependent load in k_apply
+        while (hs_.pair_used + per_round * R > pcap_ / 2) {
             if (R > 8) { R /= 2; continue; }
             grow_pairs();
             hs_.halt = HALT_REBUILD;   // C holds slot indices: rebuild it
