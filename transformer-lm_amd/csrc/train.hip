@@ -67,8 +67,8 @@ struct RoundState {
     int ntok;
     long long T;
     unsigned nC, capC, c_limit, pad0;
-    unsigned nC_base;           // |C| before this round's k_argmax appends (set by k_merge)
-    unsigned k3_done;           // k_argmax blocks finished this launch (the last one advances)
+    unsigned nC_base;           // |C| before this round's appends (set by k_merge)
+    int cur_round, cur_ntok;    // for k_apply_argmax: this round, and ntok after it (k_merge)
     unsigned cur_a, cur_b, cur_new, cur_slot;
     long long cur_cnt;
     int new_is_new;
@@ -397,9 +397,10 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
         const unsigned nC = st->nC, c_limit = st->c_limit;   // only k_argmax appends to C
         const long long T = st->T;
         Cand pp = cand_none();
-        if (tid < nparts) {
-            const Partial q = part[tid];
-            pp = Cand{q.cnt, q.ka, q.kb, q.slot, q.a, q.b};
+        for (int i = tid; i < nparts; i += 64) {   // independent loads: one latency
+            const Partial q = part[i];
+            const Cand c{q.cnt, q.ka, q.kb, q.slot, q.a, q.b};
+            if (cand_better(c, pp, K.pool, K.off, K.len)) pp = c;
         }
         for (int o = 32; o > 0; o >>= 1) {
             const Cand oc = shfl_xor_cand(pp, o);
@@ -477,7 +478,9 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
 
     if (blockIdx.x == 0) {  // record the merge, pop the pair, register a new token
         if (tid == 0) {
-            st->nC_base = st->nC;     // C entries k_argmax may read without racing its appends
+            st->nC_base = st->nC;     // C entries k_apply_argmax may scan without racing its appends
+            st->cur_round = sb.round;
+            st->cur_ntok = sb.ntok + (int)sb.isnew;
             P.cnt[sb.slot] = 0;                       // byte_pair_frequencies.pop(best_pair)
             atomicAnd(&P.flag[sb.slot], ~kPresent);   // (no other update touches this key)
             st->cur_a = a; st->cur_b = b; st->cur_new = nw; st->cur_slot = sb.slot;
@@ -550,87 +553,166 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
     }
 }
 
-// ------------------------------------------------------------------ K2: apply deltas
-__global__ void __launch_bounds__(256) k_apply(RoundState* __restrict__ st, PairsDev P,
-                                               unsigned long long* __restrict__ LR,
-                                               unsigned long long* __restrict__ touched, unsigned ntb) {
-    const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
-    const unsigned x = g >> 2, op = g & 3;   // op: 0 (x,a)-=L  1 (x,new)+=L  2 (b,x)-=R  3 (new,x)+=R
-    // ntb (a launch argument) bounds every token id k_merge can have written; cells below it
-    // past the live tokens stay 0.  So the cell load needs no state and issues together with
-    // the state loads.  (The grid is rounded up to whole blocks: x >= ntb is past LR's end.)
-    unsigned long long* cell = &LR[2 * (size_t)x + (op >> 1)];
-    const long long d = x < ntb ? (long long)*cell : 0;
-    if (st->halt) return;
-    const unsigned a = st->cur_a, b = st->cur_b, nw = st->cur_new;
-    size_t inc_slot = ~(size_t)0;
-    if (d) {
-        switch (op) {
-            case 0: if (!(x == a && a == b)) pair_dec(P, st, x, a, d); break;   // never the popped key
-            case 1: inc_slot = pair_inc(P, st, x, nw, d); break;
-            case 2: if (!(x == b && a == b)) pair_dec(P, st, b, x, d); break;
-            default: inc_slot = pair_inc(P, st, nw, x, d); break;
-        }
-        if (op & 1) {
-            *cell = 0;   // both lanes of this cell read it in the same load instruction
-            // the incremented key, tagged with the round, at the cell's own index: k_argmax
-            // scans the cells instead of a list built with a returning atomic
-            if (inc_slot != ~(size_t)0)
-                touched[2 * (size_t)x + (op >> 1)] = ((unsigned long long)(st->round + 1) << 32) | inc_slot;
-        }
+// ------------------------------------------------------------------ K2: apply + argmax
+// One launch applies the round's deltas and takes the argmax for the next round.
+//  * cell threads (4 per token x, op = g & 3):  0 (x,a) -= L[x]   1 (x,new) += L[x]
+//                                               2 (b,x) -= R[x]   3 (new,x) += R[x]
+//    Only four keys can receive two of these updates -- (b,a), (b,new), (new,a), (new,new) --
+//    and thread 0 applies those; every other key has ONE updater, so counts are updated with
+//    plain loads/stores and the updater sees the key's final count: it evaluates the key for
+//    the argmax and admits it to C when an increment lifts it to T (identical on every rank).
+//  * C threads scan the candidate list C (entries before this round's appends).  An entry is
+//    skipped iff this round's cells touch it -- exactly the rule above -- and its updater
+//    evaluates it instead; the others' counts do not change during the launch.
+// The cells are double-buffered by round parity: this launch reads LR (this round) and clears
+// LRold (the previous round's, already applied).  Round state is written only into fields the
+// other kernel reads (k_merge -> cur_*, this kernel -> round/ntok), so no grid-wide ordering.
+// apply `delta` to the key (p, q) (its only updater this round); present if incremented or
+// created (a decrement of a missing key creates it, as the reference's defaultdict does)
+__device__ __forceinline__ size_t pair_update(const PairsDev& P, RoundState* st, unsigned p, unsigned q,
+                                              long long delta, bool inc, long long* c_out, unsigned* f_out) {
+    bool ins;
+    const size_t s = pair_slot(P, pair_key(p, q), st, &ins);
+    if (s == ~(size_t)0) return s;
+    const long long c = P.cnt[s] + delta;
+    unsigned f = P.flag[s];
+    P.cnt[s] = c;
+    if ((inc || ins) && !(f & kPresent)) {
+        f |= kPresent;
+        P.flag[s] = f;
     }
+    *c_out = c;
+    *f_out = f;
+    return s;
 }
 
-// ------------------------------------------------------------------ K3: argmax over C
-// With advance=1 it also finishes the round: the new token enters the dedupe map, and
-// round/ntok step forward (by the last block to finish).
-__global__ void __launch_bounds__(256) k_argmax(RoundState* __restrict__ st, PairsDev P, ToksDev K,
-                                                const unsigned long long* __restrict__ touched,
-                                                Partial* __restrict__ part, int advance) {
+__global__ void __launch_bounds__(256) k_apply_argmax(RoundState* __restrict__ st, PairsDev P, ToksDev K,
+                                                      const unsigned long long* __restrict__ LR,
+                                                      unsigned long long* __restrict__ LRold,
+                                                      unsigned ntb, unsigned cell_blocks,
+                                                      Partial* __restrict__ part) {
     __shared__ Cand sw[4];
-    if (st->halt) return;
-    const unsigned nC = advance ? st->nC_base : st->nC;
-    const long long T = st->T;
-    const int round = st->round;
-    const unsigned nw = st->cur_new;
-    // cells k_apply may have tagged this round: 2 per token id
-    const unsigned n_cells = advance ? 2u * ((unsigned)st->ntok + (unsigned)st->new_is_new) : 0u;
-    if (advance && blockIdx.x == 0 && threadIdx.x == 0 && st->new_is_new) {
-        unsigned s = (unsigned)mix64(K.hash[nw]) & K.map_mask;
-        while (K.map[s] != 0) s = (s + 1) & K.map_mask;
-        K.map[s] = nw + 1;
-    }
+    const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool cell_thread = blockIdx.x < cell_blocks;
+    const unsigned x = g >> 2, op = g & 3;
+    // the cell load needs no state (ntb bounds every id k_merge can have written)
+    const long long d = cell_thread && x < ntb ? (long long)LR[2 * (size_t)x + (op >> 1)] : 0;
+    if (cell_thread && (op & 1) && x < ntb) LRold[2 * (size_t)x + (op >> 1)] = 0;
     Cand best = cand_none();
-    // keys incremented this round (k_apply tagged them with round + 1): admitted to C by
-    // their final count (identical on every rank); they are also candidates of this argmax.
-    // The key is (x, new) for cell 2x and (new, x) for cell 2x+1.
-    const unsigned long long tag = (unsigned long long)(round + 1);
-    for (unsigned i0 = blockIdx.x * blockDim.x; i0 < n_cells; i0 += gridDim.x * blockDim.x) {
-        const unsigned i = i0 + threadIdx.x;
+    if (!st->halt) {
+        const unsigned a = st->cur_a, b = st->cur_b, nw = st->cur_new;
+        const long long T = st->T;
+        // a key this thread updated: candidate if present and >= T; increments may admit it
+        auto consider = [&](size_t s, unsigned p, unsigned q, long long c, unsigned f, bool inc) -> bool {
+            if (s == ~(size_t)0 || !(f & kPresent) || c < T) return false;
+            const Cand cand{c, K.key8[p], K.key8[q], (unsigned)s, p, q};
+            if (cand_better(cand, best, K.pool, K.off, K.len)) best = cand;
+            if (inc && !(f & kInC)) {
+                P.flag[s] = f | kInC;
+                return true;
+            }
+            return false;
+        };
         bool add = false;
-        unsigned s = 0, a = 0, b = 0;
-        if (i < n_cells) {
-            const unsigned long long e = touched[i];
-            if ((e >> 32) == tag) {
-                s = (unsigned)e;
-                a = (i & 1) ? nw : i >> 1;
-                b = (i & 1) ? i >> 1 : nw;
-                const unsigned f = P.flag[s];
-                const long long c = P.cnt[s];
-                const unsigned long long ka = K.key8[a], kb = K.key8[b];
-                if ((f & kPresent) && c >= T) {
-                    const Cand x{c, ka, kb, s, a, b};
-                    if (cand_better(x, best, K.pool, K.off, K.len)) best = x;
-                    if (!(f & kInC)) add = !(atomicOr(&P.flag[s], kInC) & kInC);
+        uint4 add_e = make_uint4(0, 0, 0, 0);
+        if (cell_thread) {
+            if (d) {
+                const bool special = (op <= 1) ? (x == b || x == nw) : (x == a || x == nw);
+                const bool popped = (op == 0 && x == a && a == b) || (op == 2 && x == b && a == b);
+                if (!special && !popped) {
+                    const unsigned p = op == 0 ? x : op == 1 ? x : op == 2 ? b : nw;
+                    const unsigned q = op == 0 ? a : op == 1 ? nw : x;
+                    const bool inc = op & 1;
+                    long long c;
+                    unsigned f;
+                    const size_t s = pair_update(P, st, p, q, inc ? d : -d, inc, &c, &f);
+                    if (consider(s, p, q, c, f, inc)) { add = true; add_e = make_uint4((unsigned)s, p, q, 0u); }
                 }
+            }
+            if (g == 0) {   // the four keys two cells can update
+                const long long Lb = (long long)LR[2 * (size_t)b], Ln = (long long)LR[2 * (size_t)nw];
+                const long long Ra = (long long)LR[2 * (size_t)a + 1], Rn = (long long)LR[2 * (size_t)nw + 1];
+                struct Sp { unsigned p, q; long long dec, inc; };
+                const Sp sp[4] = {{b, a, a == b ? 0 : Lb + Ra, 0},   // (a,b) itself when a == b: popped
+                                  {b, nw, Rn, Lb},
+                                  {nw, a, Ln, Ra},
+                                  {nw, nw, 0, Ln + Rn}};
+                // (the decrements use the same cells as their single-updater twins above)
+                for (int k = 0; k < 4; ++k) {
+                    const bool touched = (k == 0) ? (a != b && (Lb || Ra))
+                                       : (k == 1) ? (Lb || Rn)
+                                       : (k == 2) ? (Ln || Ra)
+                                                  : (Ln || Rn);
+                    if (!touched) continue;
+                    long long c;
+                    unsigned f;
+                    const bool inc = sp[k].inc != 0;
+                    const size_t s = pair_update(P, st, sp[k].p, sp[k].q, sp[k].inc - sp[k].dec, inc, &c, &f);
+                    if (consider(s, sp[k].p, sp[k].q, c, f, inc)) {
+                        // thread 0 appends its own admissions here (at most four)
+                        const unsigned idx = atomicAdd(&st->nC, 1u);
+                        if (idx < st->capC) P.C[idx] = make_uint4((unsigned)s, sp[k].p, sp[k].q, 0u);
+                        else atomicOr(&st->err, ERR_C_FULL);
+                    }
+                }
+            }
+        } else {
+            // C scan: entries untouched this round keep their counts during this launch
+            const unsigned nC = st->nC_base;
+            const unsigned stride = (gridDim.x - cell_blocks) * blockDim.x;
+            for (unsigned i = g - cell_blocks * blockDim.x; i < nC; i += stride) {
+                const uint4 e = P.C[i];
+                const unsigned p = e.y, q = e.z;
+                const unsigned f = P.flag[e.x];
+                const long long c = P.cnt[e.x];
+                const unsigned long long ka = K.key8[p], kb = K.key8[q];
+                bool touched = false;
+                if (q == a || q == nw) touched = LR[2 * (size_t)p] != 0;
+                if (!touched && (p == b || p == nw)) touched = LR[2 * (size_t)q + 1] != 0;
+                if (touched || !(f & kPresent)) continue;
+                const Cand cand{c, ka, kb, e.x, p, q};
+                if (cand_better(cand, best, K.pool, K.off, K.len)) best = cand;
             }
         }
         const unsigned idx = wave_append(add, &st->nC);
         if (add) {
-            if (idx < st->capC) P.C[idx] = make_uint4(s, a, b, 0u);
+            if (idx < st->capC) P.C[idx] = add_e;
             else atomicOr(&st->err, ERR_C_FULL);
         }
     }
+    for (int o = 32; o > 0; o >>= 1) {
+        const Cand oc = shfl_xor_cand(best, o);
+        if (cand_better(oc, best, K.pool, K.off, K.len)) best = oc;
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) sw[w] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
+            if (cand_better(sw[k], best, K.pool, K.off, K.len)) best = sw[k];
+        part[blockIdx.x] = Partial{best.cnt, best.ka, best.kb, best.slot, best.a, best.b, 0};
+        if (blockIdx.x == 0 && !st->halt) {
+            // finish the round: the new token enters the dedupe map; round/ntok advance (only
+            // k_merge reads these, in the next launch)
+            const unsigned nw = st->cur_new;
+            if (st->new_is_new) {
+                unsigned s = (unsigned)mix64(K.hash[nw]) & K.map_mask;
+                while (K.map[s] != 0) s = (s + 1) & K.map_mask;
+                K.map[s] = nw + 1;
+            }
+            st->round = st->cur_round + 1;
+            st->ntok = st->cur_ntok;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ argmax over C (rebuild)
+// After the host re-thresholds C: per-block partials of the argmax over all of C.
+__global__ void __launch_bounds__(256) k_argmax(RoundState* __restrict__ st, PairsDev P, ToksDev K,
+                                                Partial* __restrict__ part) {
+    __shared__ Cand sw[4];
+    Cand best = cand_none();
+    const unsigned nC = st->nC;
     for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < nC; i += gridDim.x * blockDim.x) {
         const uint4 e = P.C[i];
         const unsigned f = P.flag[e.x];
@@ -651,17 +733,6 @@ __global__ void __launch_bounds__(256) k_argmax(RoundState* __restrict__ st, Pai
         for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
             if (cand_better(sw[k], best, K.pool, K.off, K.len)) best = sw[k];
         part[blockIdx.x] = Partial{best.cnt, best.ka, best.kb, best.slot, best.a, best.b, 0};
-        // Advance the round only once every block has read round-dependent state: the last
-        // block to finish does it.  (Advancing from block 0 raced with blocks that had not
-        // started yet.)
-        if (advance) {
-            __threadfence();
-            if (atomicAdd(&st->k3_done, 1u) == gridDim.x - 1) {
-                st->k3_done = 0;
-                st->round += 1;
-                st->ntok += st->new_is_new;
-            }
-        }
     }
 }
 
@@ -1019,6 +1090,8 @@ class MergeLoop {
    private:
     static constexpr int kBatch = 64;
     static constexpr int kArgBlocks = 64;
+    static constexpr unsigned kCScanBlocks = 64;   // k_apply_argmax workgroups scanning C
+    unsigned nparts_ = 0;                          // argmax partials the next k_merge reduces
     static constexpr int kTimingStride = 8;   // k_merge launches timed: one in 8
     static constexpr unsigned long long kTarget = 4096;
 
@@ -1083,7 +1156,6 @@ class MergeLoop {
     DevBuf<uint32_t> ilist_, ibeg_, ilen_;
     IndexDev idev_{};
     int next_index_round_ = 256;
-    DevBuf<unsigned long long> touched_;   // per delta cell: (round + 1) << 32 | slot it incremented
 };
 
 template <class TokT>
@@ -1360,8 +1432,8 @@ int MergeLoop<TokT>::rebuild() {
     hs_.halt = HALT_NONE;
     push_state();
     hipLaunchKernelGGL(k_build_C, dim3(grid), dim3(256), 0, s_, pairs(), pcap_, T, st_.p);
-    hipLaunchKernelGGL(k_argmax, dim3(kArgBlocks), dim3(256), 0, s_, st_.p, pairs(), toks(),
-                       touched_.p, part_.p, 0);
+    hipLaunchKernelGGL(k_argmax, dim3(kArgBlocks), dim3(256), 0, s_, st_.p, pairs(), toks(), part_.p);
+    nparts_ = kArgBlocks;
     BPE_HIP(hipGetLastError());
     pull_state();
     BPE_REQUIRE(!(hs_.err & ERR_C_FULL), BPE_E_NOMEM, "candidate list overflow");
@@ -1376,11 +1448,9 @@ template <class TokT>
 void MergeLoop<TokT>::run() {
     st_.alloc(1);
     rs_.alloc(1);
-    part_.alloc(kArgBlocks);
     tok_cap_ = 256u + (unsigned)n_rounds_ + 1u;
-    LR_.alloc(2ull * tok_cap_);
-    touched_.alloc(2ull * tok_cap_);
-    BPE_HIP(hipMemsetAsync(touched_.p, 0, touched_.bytes(), s_));
+    part_.alloc(std::max<size_t>(kArgBlocks, ceil_div(4ull * tok_cap_, 256) + kCScanBlocks));
+    LR_.alloc(2 * 2ull * tok_cap_);   // two cell buffers, by round parity
     BPE_HIP(hipMemsetAsync(LR_.p, 0, LR_.bytes(), s_));
     m_a_.alloc(n_rounds_); m_b_.alloc(n_rounds_); m_new_.alloc(n_rounds_); m_mode_.alloc(n_rounds_);
     toff_.alloc(tok_cap_); tlen_.alloc(tok_cap_);
@@ -1465,19 +1535,25 @@ void MergeLoop<TokT>::run() {
             // launch in kTimingStride is timed, by events stamped from k_merge's own dispatch
             // packet (events on every launch cost ~8 us of idle per round).
             const bool timed = timing && (start_round + k) % kTimingStride == 0;
+            // the round's cells: buffer (round & 1); k_apply_argmax clears the other one
+            const long long rnd = start_round + k;
+            unsigned long long* LRc = LR_.p + (size_t)(rnd & 1) * 2 * tok_cap_;
+            unsigned long long* LRo = LR_.p + (size_t)((rnd + 1) & 1) * 2 * tok_cap_;
             hipExtLaunchKernelGGL(k_merge<TokT>, dim3(merge_grid_), dim3(256), 0, s_,
                                   timed ? ev[2 * k] : nullptr, timed ? ev[2 * k + 1] : nullptr, 0,
-                                  st_.p, (const Partial*)part_.p, (int)kArgBlocks, pairs(), toks(),
-                                  wdev_, idev_, LR_.p, m_a_.p, m_b_.p, m_new_.p, m_mode_.p);
+                                  st_.p, (const Partial*)part_.p, (int)nparts_, pairs(), toks(),
+                                  wdev_, idev_, LRc, m_a_.p, m_b_.p, m_new_.p, m_mode_.p);
             if (sharded) {   // the one collective per merge round
-                const size_t ntok_bound = 256 + (size_t)start_round + k + 1;
-                comm_->allreduce_i64(reinterpret_cast<int64_t*>(LR_.p), 2 * ntok_bound, s_);
+                const size_t ntok_bound = 256 + (size_t)rnd + 1;
+                comm_->allreduce_i64(reinterpret_cast<int64_t*>(LRc), 2 * ntok_bound, s_);
             }
-            const unsigned ntb = 256u + (unsigned)start_round + (unsigned)k + 1u;
-            hipLaunchKernelGGL(k_apply, dim3(ceil_div(4ull * ntb, 256)), dim3(256), 0, s_, st_.p,
-                               pairs(), LR_.p, touched_.p, ntb);
-            hipLaunchKernelGGL(k_argmax, dim3(kArgBlocks), dim3(256), 0, s_, st_.p, pairs(), toks(),
-                               touched_.p, part_.p, 1);
+            const unsigned ntb = 256u + (unsigned)rnd + 1u;
+            const unsigned cell_blocks = ceil_div(4ull * ntb, 256);
+            const unsigned c_blocks = std::min<unsigned>(kCScanBlocks, std::max(1u, ceil_div(hs_.c_limit, 256)));
+            hipLaunchKernelGGL(k_apply_argmax, dim3(cell_blocks + c_blocks), dim3(256), 0, s_, st_.p,
+                               pairs(), toks(), (const unsigned long long*)LRc, LRo, ntb, cell_blocks,
+                               part_.p);
+            nparts_ = cell_blocks + c_blocks;
         }
         BPE_HIP(hipGetLastError());
         pull_state();
