@@ -386,18 +386,12 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
                                                uint32_t* __restrict__ m_new, uint32_t* __restrict__ m_mode) {
     __shared__ BestShared sb;
     __shared__ unsigned long long l_lr[2 * kLdsLR];
+    __shared__ Cand s_part[4];
     const int tid = threadIdx.x;
     for (unsigned k = tid; k < 2 * kLdsLR; k += blockDim.x) l_lr[k] = 0;
-    if (tid < 64) {
-        // Every workgroup redundantly decides the round (no extra launch, no grid sync).  The
-        // loads are grouped by dependency level so the chain is ~4 memory latencies long:
-        // state + partials | token metadata, posting-list ids | map slot, list bounds | (dedupe)
-        const int halt = st->halt, round = st->round, ntok = st->ntok;
-        const int n_rounds = st->n_rounds;
-        const unsigned nC = st->nC, c_limit = st->c_limit;   // only k_argmax appends to C
-        const long long T = st->T;
+    {   // all four waves reduce the argmax partials (a few independent loads per thread)
         Cand pp = cand_none();
-        for (int i = tid; i < nparts; i += 64) {   // independent loads: one latency
+        for (int i = tid; i < nparts; i += blockDim.x) {
             const Partial q = part[i];
             const Cand c{q.cnt, q.ka, q.kb, q.slot, q.a, q.b};
             if (cand_better(c, pp, K.pool, K.off, K.len)) pp = c;
@@ -406,6 +400,20 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
             const Cand oc = shfl_xor_cand(pp, o);
             if (cand_better(oc, pp, K.pool, K.off, K.len)) pp = oc;
         }
+        if ((tid & 63) == 0) s_part[tid >> 6] = pp;
+    }
+    __syncthreads();
+    if (tid < 64) {
+        // Every workgroup redundantly decides the round (no extra launch, no grid sync).  The
+        // loads are grouped by dependency level so the chain is ~4 memory latencies long:
+        // state + partials | token metadata, posting-list ids | map slot, list bounds | (dedupe)
+        const int halt = st->halt, round = st->round, ntok = st->ntok;
+        const int n_rounds = st->n_rounds;
+        const unsigned nC = st->nC, c_limit = st->c_limit;   // only k_apply_argmax appends to C
+        const long long T = st->T;
+        Cand pp = s_part[0];
+        for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
+            if (cand_better(s_part[k], pp, K.pool, K.off, K.len)) pp = s_part[k];
         int stop = HALT_NONE;
         if (halt) stop = -1;
         else if (round >= n_rounds) stop = HALT_DONE;
@@ -586,12 +594,13 @@ __device__ __forceinline__ size_t pair_update(const PairsDev& P, RoundState* st,
     return s;
 }
 
-__global__ void __launch_bounds__(256) k_apply_argmax(RoundState* __restrict__ st, PairsDev P, ToksDev K,
+constexpr unsigned kApplyThreads = 256;    // large workgroups: fewer argmax partials for k_merge
+__global__ void __launch_bounds__(kApplyThreads) k_apply_argmax(RoundState* __restrict__ st, PairsDev P, ToksDev K,
                                                       const unsigned long long* __restrict__ LR,
                                                       unsigned long long* __restrict__ LRold,
                                                       unsigned ntb, unsigned cell_blocks,
                                                       Partial* __restrict__ part) {
-    __shared__ Cand sw[4];
+    __shared__ Cand sw[kApplyThreads / 64];
     const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
     const bool cell_thread = blockIdx.x < cell_blocks;
     const unsigned x = g >> 2, op = g & 3;
@@ -1548,9 +1557,10 @@ void MergeLoop<TokT>::run() {
                 comm_->allreduce_i64(reinterpret_cast<int64_t*>(LRc), 2 * ntok_bound, s_);
             }
             const unsigned ntb = 256u + (unsigned)rnd + 1u;
-            const unsigned cell_blocks = ceil_div(4ull * ntb, 256);
-            const unsigned c_blocks = std::min<unsigned>(kCScanBlocks, std::max(1u, ceil_div(hs_.c_limit, 256)));
-            hipLaunchKernelGGL(k_apply_argmax, dim3(cell_blocks + c_blocks), dim3(256), 0, s_, st_.p,
+            const unsigned cell_blocks = ceil_div(4ull * ntb, kApplyThreads);
+            const unsigned c_blocks = std::min<unsigned>(kCScanBlocks,
+                                                         std::max(1u, ceil_div(hs_.c_limit, kApplyThreads)));
+            hipLaunchKernelGGL(k_apply_argmax, dim3(cell_blocks + c_blocks), dim3(kApplyThreads), 0, s_, st_.p,
                                pairs(), toks(), (const unsigned long long*)LRc, LRo, ntb, cell_blocks,
                                part_.p);
             nparts_ = cell_blocks + c_blocks;
