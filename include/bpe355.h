@@ -134,7 +134,28 @@ int bpe_tok_encode(bpe_tokenizer* tok, const uint8_t* utf8, size_t n, uint32_t* 
 /* same, device-resident text and output (d_out holds >= n ids) */
 int bpe_tok_encode_device(bpe_tokenizer* tok, const uint8_t* d_utf8, size_t n, uint32_t* d_out,
                           size_t* n_out, void* hip_stream);
+/* Chunked encode: the ids of encode(text[starts[i] : starts[i+1]]) for every piece, concatenated
+ * (starts sorted byte offsets; the last piece runs to n).  A piece boundary ends every
+ * pre-token and no special token may straddle it -- exactly separate encode() calls, as the
+ * reference's encode_iterable (tokenizer.py:140-150: 2 MiB-character batches) and dataset
+ * encoder (encode.py:31-36: 1 M-character reads) make them. */
+int bpe_tok_encode_chunks(bpe_tokenizer* tok, const uint8_t* utf8, size_t n, const uint64_t* starts,
+                          size_t n_starts, uint32_t* ids_out, size_t cap, size_t* n_out);
+int bpe_tok_encode_chunks_device(bpe_tokenizer* tok, const uint8_t* d_utf8, size_t n, const uint64_t* starts,
+                                 size_t n_starts, uint32_t* d_out, size_t* n_out, void* hip_stream);
 void bpe_tok_free(bpe_tokenizer* tok);
+
+/* ---------------------------------------------------------------- bulk encode plumbing */
+/* open(path, "r", encoding="utf-8").read() on device bytes: strict UTF-8 (BPE_E_UTF8) and
+ * universal newlines.  d_out holds n bytes (may be d_in); *n_out = resulting length. */
+int bpe_text_prepare_device(const uint8_t* d_in, size_t n, uint8_t* d_out, size_t* n_out, void* hip_stream);
+/* Byte offsets of characters 0, K, 2K, ... of valid UTF-8 (K = chars_per_chunk): the pieces
+ * successive f.read(K) calls return (encode.py:31-33).  starts == NULL: count only. */
+int bpe_utf8_chunk_starts_device(const uint8_t* d_text, size_t n, size_t chars_per_chunk, uint64_t* starts,
+                                 size_t cap, size_t* n_starts, void* hip_stream);
+/* np.array(token_ids, dtype=np.uint16) (encode.py:37), on the device; BPE_E_LIMIT if an id
+ * does not fit (the reference would silently wrap it). */
+int bpe_ids_to_u16_device(const uint32_t* d_ids, size_t n, uint16_t* d_out, void* hip_stream);
 
 /* ---------------------------------------------------------------- helpers */
 /* Largest p <= pos such that splitting the text at p does not change its pre-tokenization

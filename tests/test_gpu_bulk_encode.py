@@ -1,0 +1,132 @@
+"""Bulk encode output: the reference's dataset encoder
+models/tokenizer/encode.py:31-38 and the np.memmap consumer of train.py:230-232.
+
+The device path (bpe_amd.encode) must write exactly the ids the reference's loop produces:
+text-mode read (universal newlines), 1 M-character pieces (smaller here), each piece encoded on
+its own, concatenated, as np.uint16 -- checked against the oracle encoding each piece.
+"""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+import gpt2_files
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _pieces(text: str, k: int):
+    return [text[i:i + k] for i in range(0, len(text), k)]
+
+
+def _mixed_text(seed: int, n_words: int) -> str:
+    rng = random.Random(seed)
+    words = ["the", " cat", "été", " naïve", "<|endoftext|>", "\n", "\r\n", "  ", "12", "'s", "!!",
+             " 東京", "—", " x" * 3, "\t", "ab<|end", "oftext|>cd"]
+    return "".join(rng.choice(words) for _ in range(n_words))
+
+
+def _device(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def test_chunk_starts_are_character_offsets():
+    import torch
+    from bpe_amd import _lib
+    L = _lib.lib()
+    text = _mixed_text(1, 3000)
+    data = text.encode("utf-8")
+    d = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda")
+    for k in (1, 7, 100, 4096):
+        ns = ctypes.c_size_t(0)
+        _lib.check(L.bpe_utf8_chunk_starts_device(_device(d), len(data), k, None, 0, ctypes.byref(ns), None))
+        starts = (ctypes.c_uint64 * max(ns.value, 1))()
+        _lib.check(L.bpe_utf8_chunk_starts_device(_device(d), len(data), k, starts, ns.value,
+                                                  ctypes.byref(ns), None))
+        want = [len(text[:i].encode("utf-8")) for i in range(0, len(text), k)]
+        assert list(starts[:ns.value]) == want
+
+
+def test_text_prepare_is_text_mode_read(tmp_path):
+    import torch
+    from bpe_amd import _lib
+    L = _lib.lib()
+    raw = "a\r\nb\rc\n\r\r\nd é\r".encode("utf-8")
+    p = tmp_path / "t.txt"
+    p.write_bytes(raw)
+    with open(p, "r", encoding="utf-8") as f:
+        want = f.read().encode("utf-8")
+    d = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to("cuda")
+    m = ctypes.c_size_t(0)
+    _lib.check(L.bpe_text_prepare_device(_device(d), len(raw), _device(d), ctypes.byref(m), None))
+    assert bytes(d[:m.value].cpu().numpy()) == want
+    bad = torch.tensor([0x61, 0xC3, 0x28], dtype=torch.uint8, device="cuda")
+    with pytest.raises(UnicodeDecodeError):
+        _lib.check(L.bpe_text_prepare_device(_device(bad), 3, _device(bad), ctypes.byref(m), None))
+
+
+# (the oracle re-serializes the 50k-entry vocab per call: small pieces only on a short text)
+@pytest.mark.parametrize("k,n_words", [(1, 60), (7, 400), (50, 4000), (997, 4000), (100_000, 4000)])
+def test_encode_chunks_equals_separate_encodes(k, n_words):
+    from bpe_amd import Tokenizer, _lib
+    vocab, merges = gpt2_files.load_gpt2(["<|endoftext|>"])
+    tok = Tokenizer(dict(vocab), list(merges), ["<|endoftext|>"])
+    text = _mixed_text(2, n_words).replace("\r", "")
+    pieces = _pieces(text, k)
+    want = []
+    for piece in pieces:   # specials straddling a piece boundary are NOT matched
+        want += oracle.encode(vocab, merges, ["<|endoftext|>"], piece)
+    data = text.encode("utf-8")
+    starts = []
+    off = 0
+    for piece in pieces:
+        starts.append(off)
+        off += len(piece.encode("utf-8"))
+    arr = (ctypes.c_uint64 * max(len(starts), 1))(*starts)
+    out = (ctypes.c_uint32 * max(len(data), 1))()
+    n_out = ctypes.c_size_t(0)
+    _lib.check(_lib.lib().bpe_tok_encode_chunks(tok._device(), data, len(data), arr, len(starts), out,
+                                                len(data), ctypes.byref(n_out)))
+    assert list(out[:n_out.value]) == want
+
+
+@pytest.mark.parametrize("fmt", ["pt", "bin"])
+def test_encode_file_matches_reference_loop(tmp_path, fmt):
+    import torch
+    from bpe_amd import Tokenizer
+    from bpe_amd.encode import encode_file
+    vocab, merges = gpt2_files.load_gpt2(["<|endoftext|>"])
+    tok = Tokenizer(dict(vocab), list(merges), ["<|endoftext|>"])
+    text = _mixed_text(3, 20000)
+    src = tmp_path / "split.txt"
+    src.write_bytes(text.encode("utf-8"))
+    k = 3000
+    with open(src, "r", encoding="utf-8") as f:   # encode.py:31-36, pieces of k characters
+        want = []
+        while True:
+            piece = f.read(k)
+            if not piece:
+                break
+            want += oracle.encode(vocab, merges, ["<|endoftext|>"], piece)
+    out = tmp_path / f"tokens.{fmt}"
+    got = encode_file(tok, src, out, fmt=fmt, chars_per_piece=k)
+    assert got.dtype == np.uint16 and got.tolist() == want
+    if fmt == "pt":
+        loaded = torch.load(out, weights_only=False)   # this test's own file
+        assert isinstance(loaded, np.ndarray) and loaded.dtype == np.uint16
+    else:
+        loaded = np.memmap(out, dtype=np.uint16, mode="r")   # train.py:230-232
+    assert loaded.tolist() == want
+
+
+def test_ids_above_uint16_are_refused():
+    import torch
+    from bpe_amd import _lib
+    ids = torch.tensor([1, 65535, 65536], dtype=torch.int32, device="cuda")
+    out = torch.empty(3, dtype=torch.int16, device="cuda")
+    with pytest.raises(RuntimeError, match="uint16"):
+        _lib.check(_lib.lib().bpe_ids_to_u16_device(_device(ids), 3, _device(out), None))
+    _lib.check(_lib.lib().bpe_ids_to_u16_device(_device(ids), 2, _device(out), None))
+    assert out[:2].cpu().numpy().view(np.uint16).tolist() == [1, 65535]

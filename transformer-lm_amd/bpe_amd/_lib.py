@@ -77,7 +77,12 @@ _SIGS = [
     ("bpe_tok_special_id", ctypes.c_int64, [_P, ctypes.c_int]),
     ("bpe_tok_encode", ctypes.c_int, [_P, _U8P, _SZ, _P, _SZ, ctypes.POINTER(_SZ)]),
     ("bpe_tok_encode_device", ctypes.c_int, [_P, _P, _SZ, _P, ctypes.POINTER(_SZ), _P]),
+    ("bpe_tok_encode_chunks", ctypes.c_int, [_P, _U8P, _SZ, _P, _SZ, _P, _SZ, ctypes.POINTER(_SZ)]),
+    ("bpe_tok_encode_chunks_device", ctypes.c_int, [_P, _P, _SZ, _P, _SZ, _P, ctypes.POINTER(_SZ), _P]),
     ("bpe_tok_free", None, [_P]),
+    ("bpe_text_prepare_device", ctypes.c_int, [_P, _SZ, _P, ctypes.POINTER(_SZ), _P]),
+    ("bpe_utf8_chunk_starts_device", ctypes.c_int, [_P, _SZ, _SZ, _P, _SZ, ctypes.POINTER(_SZ), _P]),
+    ("bpe_ids_to_u16_device", ctypes.c_int, [_P, _SZ, _P, _P]),
     ("bpe_safe_split", _SZ, [_U8P, _SZ, _SZ]),
     ("bpe_synth_corpus_device", ctypes.c_int, [_P, _SZ, ctypes.c_uint64, ctypes.c_int,
                                                ctypes.c_uint64, _P]),

@@ -1,0 +1,114 @@
+"""Dataset encoder -- drop-in for reference models/tokenizer/encode.py (and the memmap input of
+train.py:230-232).
+
+The reference reads the split in text mode 1 M characters at a time, encodes every piece with
+Tokenizer.encode_iterable([piece]) and saves np.array(ids, dtype=np.uint16) with
+torch.save(..., pickle_protocol=4).  Here the whole file goes to the device once:
+
+    bytes -> bpe_text_prepare_device    (strict UTF-8 + universal newlines: the text-mode read)
+          -> bpe_utf8_chunk_starts_device (where each 1 M-character piece starts)
+          -> bpe_tok_encode_chunks_device (one launch sequence for all pieces; a piece boundary
+                                          ends every pre-token and no special straddles it, so
+                                          the ids equal the per-piece encodes, concatenated)
+          -> bpe_ids_to_u16_device        (np.uint16, refusing ids > 65535 instead of wrapping)
+
+and the uint16 ids come back to the host once.  Output formats: "pt" (the reference's file,
+torch.save of the np.uint16 array) and "bin" (raw uint16, what train.py's np.memmap reads).
+
+(The reference's loop passes a one-element LIST to encode_iterable, which re-iterates it
+forever -- tokenizer.py:140-150; DESIGN.md section 7.  The ids written here are the ones the
+loop would produce if it terminated.)
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .tokenizer import Tokenizer
+
+fname = {   # encode.py:8-15
+    "tiny/train": "TinyStoriesV2-GPT4-train.txt",
+    "tiny/valid": "TinyStoriesV2-GPT4-valid.txt",
+    "owt/train": "owt_train.txt",
+    "owt/valid": "owt_valid.txt",
+    "corpus/train": "corpus.en",
+    "corpus/valid": "corpus.en",
+}
+
+CHARS_PER_PIECE = 1024 * 1024   # encode.py:33 f.read(1024 * 1024)
+
+
+def encode_bytes_u16(tokenizer: Tokenizer, data: bytes, chars_per_piece: int = CHARS_PER_PIECE) -> np.ndarray:
+    """The reference's encode.py ids for a file whose raw bytes are `data`, as np.uint16."""
+    import torch
+    L = _lib.lib()
+    n = len(data)
+    if n == 0:
+        return np.zeros(0, dtype=np.uint16)
+    raw = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda")
+    torch.cuda.synchronize()
+    m = ctypes.c_size_t(0)
+    _lib.check(L.bpe_text_prepare_device(ctypes.c_void_p(raw.data_ptr()), n, ctypes.c_void_p(raw.data_ptr()),
+                                         ctypes.byref(m), None), "read")
+    m = m.value
+    ns = ctypes.c_size_t(0)
+    _lib.check(L.bpe_utf8_chunk_starts_device(ctypes.c_void_p(raw.data_ptr()), m, chars_per_piece, None, 0,
+                                              ctypes.byref(ns), None), "chunk starts")
+    starts = (ctypes.c_uint64 * max(ns.value, 1))()
+    _lib.check(L.bpe_utf8_chunk_starts_device(ctypes.c_void_p(raw.data_ptr()), m, chars_per_piece, starts,
+                                              ns.value, ctypes.byref(ns), None), "chunk starts")
+    ids = torch.empty(max(m, 1), dtype=torch.int32, device="cuda")
+    n_ids = ctypes.c_size_t(0)
+    _lib.check(L.bpe_tok_encode_chunks_device(tokenizer._device(), ctypes.c_void_p(raw.data_ptr()), m, starts,
+                                              ns.value, ctypes.c_void_p(ids.data_ptr()), ctypes.byref(n_ids),
+                                              None), "encode")
+    k = n_ids.value
+    out16 = torch.empty(max(k, 1), dtype=torch.int16, device="cuda")
+    _lib.check(L.bpe_ids_to_u16_device(ctypes.c_void_p(ids.data_ptr()), k, ctypes.c_void_p(out16.data_ptr()),
+                                       None), "uint16 ids")
+    torch.cuda.synchronize()
+    return out16[:k].cpu().numpy().view(np.uint16)
+
+
+def encode_file(tokenizer: Tokenizer, input_path, output_path=None, fmt: str = "pt",
+                chars_per_piece: int = CHARS_PER_PIECE) -> np.ndarray:
+    """Encode a text file like encode.py:main; write it if output_path is given."""
+    with open(input_path, "rb") as f:
+        data = f.read()
+    pt = encode_bytes_u16(tokenizer, data, chars_per_piece)
+    if output_path is not None:
+        if fmt == "pt":
+            import torch
+            torch.save(pt, output_path, pickle_protocol=4)   # encode.py:38
+        elif fmt == "bin":
+            pt.tofile(output_path)                           # np.memmap(path, np.uint16, "r")
+        else:
+            raise ValueError(f"unknown format {fmt!r}")
+    return pt
+
+
+def main(dataset: str, split: str, fmt: str = "pt"):
+    """encode.py:18-38 with the same paths."""
+    if dataset == "corpus":
+        input_file = "tests/fixtures/corpus.en"
+    else:
+        input_file = f"/data/{fname[dataset + '/' + split]}"
+    tokenizer = Tokenizer.from_files(
+        vocab_filepath=f"data/tokenizer/{dataset}-vocab.pkl",
+        merges_filepath=f"data/tokenizer/{dataset}-merges.pkl",
+        special_tokens=["<|endoftext|>"],
+    )
+    ext = "pt" if fmt == "pt" else "bin"
+    encode_file(tokenizer, input_file, f"data/tokenizer/{dataset}-tokens-{split}.{ext}", fmt=fmt)
+
+
+if __name__ == "__main__":
+    parser = argparse.ArgumentParser()
+    parser.add_argument("--dataset", type=str)
+    parser.add_argument("--split", type=str)
+    parser.add_argument("--format", type=str, default="pt", choices=["pt", "bin"])
+    args = parser.parse_args()
+    main(args.dataset, args.split, args.format)

@@ -550,10 +550,16 @@ void build_tokenizer(bpe_tokenizer& T, const uint8_t* vb, size_t vn, const uint8
     BPE_HIP(hipStreamSynchronize(T.stream));
 }
 
-// encode d_text[0..n) into d_out; returns the id count
+// encode d_text[0..n) into d_out; returns the id count.  `cuts` (sorted byte offsets) make the
+// result that of separate encode() calls on the pieces between them, concatenated: a cut ends
+// every segment, and a special token may not straddle one (encode.py's 1 M-character chunks,
+// encode_iterable's 2 MiB batches).
 size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t* d_out,
-                     hipStream_t s) {
+                     hipStream_t s, const std::vector<unsigned long long>& cuts_in = {}) {
     if (n == 0) return 0;
+    std::vector<unsigned long long> cuts;
+    for (unsigned long long c : cuts_in)
+        if (c > 0 && c < n && (cuts.empty() || c > cuts.back())) cuts.push_back(c);
     EncTables E = T.tables();
     // 1. segments
     std::vector<Seg> segs;
@@ -591,14 +597,24 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
         for (size_t i = 0; i < cnt; ++i) order[i] = i;
         std::sort(order.begin(), order.end(), [&](size_t x, size_t y) { return pos[x] < pos[y]; });
         unsigned long long cur = 0;
+        size_t ci = 0;
+        auto cut_until = [&](unsigned long long upto) {   // normal segments ended by cuts <= upto
+            for (; ci < cuts.size() && cuts[ci] <= upto; ++ci) {
+                if (cuts[ci] > cur) segs.push_back(Seg{cur, cuts[ci], -1, 0});
+                cur = std::max(cur, cuts[ci]);
+            }
+        };
         for (size_t oi : order) {  // leftmost, non-overlapping (re.split)
             const unsigned long long p0 = pos[oi];
             if (p0 < cur) continue;
-            if (p0 > cur) segs.push_back(Seg{cur, p0, -1, 0});
             const unsigned long long e = p0 + T.specials[spk[oi]].size();
+            cut_until(p0);
+            if (ci < cuts.size() && cuts[ci] < e) continue;   // straddles a chunk boundary
+            if (p0 > cur) segs.push_back(Seg{cur, p0, -1, 0});
             segs.push_back(Seg{p0, e, spk[oi], 0});
             cur = e;
         }
+        cut_until(n);
         if (cur < n) segs.push_back(Seg{cur, n, -1, 0});
     }
     const int nseg = (int)segs.size();
@@ -772,6 +788,40 @@ int bpe_tok_encode_device(bpe_tokenizer* tok, const uint8_t* d_utf8, size_t n, u
         BPE_REQUIRE(tok && n_out && (n == 0 || (d_utf8 && d_out)), BPE_E_ARG, "NULL argument");
         hipStream_t s = hip_stream ? (hipStream_t)hip_stream : tok->stream;
         *n_out = bpe::encode_device(*tok, d_utf8, n, d_out, s);
+    });
+}
+
+int bpe_tok_encode_chunks_device(bpe_tokenizer* tok, const uint8_t* d_utf8, size_t n, const uint64_t* starts,
+                                 size_t n_starts, uint32_t* d_out, size_t* n_out, void* hip_stream) {
+    return bpe::guarded_enc([&] {
+        BPE_REQUIRE(tok && n_out && (n == 0 || (d_utf8 && d_out)), BPE_E_ARG, "NULL argument");
+        BPE_REQUIRE(n_starts == 0 || starts, BPE_E_ARG, "NULL starts");
+        std::vector<unsigned long long> cuts(starts, starts + n_starts);
+        for (size_t i = 1; i < cuts.size(); ++i)
+            BPE_REQUIRE(cuts[i] >= cuts[i - 1], BPE_E_ARG, "chunk starts must be sorted");
+        hipStream_t s = hip_stream ? (hipStream_t)hip_stream : tok->stream;
+        *n_out = bpe::encode_device(*tok, d_utf8, n, d_out, s, cuts);
+    });
+}
+
+int bpe_tok_encode_chunks(bpe_tokenizer* tok, const uint8_t* utf8, size_t n, const uint64_t* starts,
+                          size_t n_starts, uint32_t* ids_out, size_t cap, size_t* n_out) {
+    return bpe::guarded_enc([&] {
+        BPE_REQUIRE(tok && n_out && (n == 0 || (utf8 && ids_out)), BPE_E_ARG, "NULL argument");
+        BPE_REQUIRE(cap >= n, BPE_E_ARG, "ids_out capacity must be >= input bytes");
+        BPE_REQUIRE(n_starts == 0 || starts, BPE_E_ARG, "NULL starts");
+        *n_out = 0;
+        if (n == 0) return;
+        std::vector<unsigned long long> cuts(starts, starts + n_starts);
+        for (size_t i = 1; i < cuts.size(); ++i)
+            BPE_REQUIRE(cuts[i] >= cuts[i - 1], BPE_E_ARG, "chunk starts must be sorted");
+        bpe::DevBuf<uint8_t> d_text(n);
+        bpe::DevBuf<uint32_t> d_out(n);
+        BPE_HIP(hipMemcpyAsync(d_text.p, utf8, n, hipMemcpyHostToDevice, tok->stream));
+        const size_t m = bpe::encode_device(*tok, d_text.p, n, d_out.p, tok->stream, cuts);
+        if (m) BPE_HIP(hipMemcpyAsync(ids_out, d_out.p, m * 4, hipMemcpyDeviceToHost, tok->stream));
+        BPE_HIP(hipStreamSynchronize(tok->stream));
+        *n_out = m;
     });
 }
 
