@@ -63,6 +63,19 @@ class Tokenizer:
             merges = pickle.load(f)
         return cls(vocab, merges, special_tokens=special_tokens)
 
+    @classmethod
+    def from_gpt2_files(cls, vocab_json: str, merges_txt: str,
+                        special_tokens: List[str] | None = None) -> "Tokenizer":
+        """GPT-2 vocab.json / merges.txt (formats.py), as the reference's tests load them."""
+        from .formats import load_gpt2
+        vocab, merges = load_gpt2(vocab_json, merges_txt, special_tokens)
+        return cls(vocab, merges, special_tokens)
+
+    def save_gpt2(self, vocab_json: str, merges_txt: str) -> None:
+        from .formats import save_gpt2
+        save_gpt2({i: b for i, b in self.vocab.items() if isinstance(i, int)}, self.merges,
+                  vocab_json, merges_txt)
+
     # ------------------------------------------------------------------ device handle
     def _device(self):
         if self._handle is None:
