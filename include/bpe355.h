@@ -145,6 +145,20 @@ int bpe_tok_encode_chunks_device(bpe_tokenizer* tok, const uint8_t* d_utf8, size
                                  size_t n_starts, uint32_t* d_out, size_t* n_out, void* hip_stream);
 void bpe_tok_free(bpe_tokenizer* tok);
 
+/* ---------------------------------------------------------------- decode */
+/* Tokenizer.decode (tokenizer.py:155-157): b"".join(vocab[i] for i in ids) on the device; the
+ * caller applies .decode("utf-8", errors="replace").  vocab blob: u32 count, then (i64 id,
+ * u32 len, bytes) per entry -- the int-keyed entries of Tokenizer.vocab.  An id without an
+ * entry fails with BPE_E_KEY (message: the id), as vocab[i] raises KeyError. */
+typedef struct bpe_decoder bpe_decoder;
+int bpe_dec_create(const uint8_t* vocab_blob, size_t vocab_n, bpe_decoder** out);
+/* host ids -> host bytes; *n_out = byte count (also set when cap is too small: BPE_E_ARG) */
+int bpe_dec_decode(bpe_decoder* dec, const uint32_t* ids, size_t n, uint8_t* out, size_t cap, size_t* n_out);
+/* device ids -> device bytes */
+int bpe_dec_decode_device(bpe_decoder* dec, const uint32_t* d_ids, size_t n, uint8_t* d_out, size_t cap,
+                          size_t* n_out, void* hip_stream);
+void bpe_dec_free(bpe_decoder* dec);
+
 /* ---------------------------------------------------------------- bulk encode plumbing */
 /* open(path, "r", encoding="utf-8").read() on device bytes: strict UTF-8 (BPE_E_UTF8) and
  * universal newlines.  d_out holds n bytes (may be d_in); *n_out = resulting length. */

@@ -41,6 +41,7 @@ class Tokenizer:
                 self.vocab[b] = len(self.vocab)
                 self.vocab_inv[b] = len(self.vocab) - 1
         self._handle = None
+        self._dec = None
 
     # ------------------------------------------------------------------ constructors
     @classmethod
@@ -97,9 +98,13 @@ class Tokenizer:
 
     def __del__(self):
         h = getattr(self, "_handle", None)
-        if h is not None and _lib._lib is not None:
+        d = getattr(self, "_dec", None)
+        if _lib._lib is not None:
             try:
-                _lib._lib.bpe_tok_free(h)
+                if h is not None:
+                    _lib._lib.bpe_tok_free(h)
+                if d is not None:
+                    _lib._lib.bpe_dec_free(d)
             except Exception:  # noqa: BLE001
                 pass
 
@@ -128,9 +133,41 @@ class Tokenizer:
                 break
             yield from self.encode(text)
 
+    def _decoder(self):
+        if getattr(self, "_dec", None) is None:
+            import struct
+            ents = [(i, b) for i, b in self.vocab.items() if isinstance(i, int)]
+            blob = struct.pack("<I", len(ents)) + b"".join(
+                struct.pack("<qI", int(i), len(b)) + bytes(b) for i, b in ents)
+            h = ctypes.c_void_p()
+            _lib.check(_lib.lib().bpe_dec_create(blob, len(blob), ctypes.byref(h)), "decoder")
+            self._dec = h
+        return self._dec
+
     def decode(self, ids: List[int]) -> str:
-        raw = b"".join([self.vocab[i] for i in ids])
-        return raw.decode("utf-8", errors="replace")
+        """tokenizer.py:155-157: b"".join(self.vocab[i] for i in ids) gathered on the GPU, then
+        CPython's UTF-8 decoder with errors="replace" (its replacement rule, exactly)."""
+        ids = list(ids)
+        for i in ids:   # ids the uint32 device table cannot hold
+            if not isinstance(i, int) or i < 0 or i > 0xFFFFFFFF:
+                v = self.vocab[i]   # KeyError, as the reference's lookup raises
+                if not isinstance(v, (bytes, bytearray)):   # b"".join of a non-bytes value
+                    raise TypeError(f"sequence item: expected a bytes-like object, {type(v).__name__} found")
+                raise KeyError(i)   # (a non-int key with a bytes value: not decodable here)
+        if not ids:
+            return ""
+        arr = (ctypes.c_uint32 * len(ids))(*ids)
+        L = _lib.lib()
+        n_out = ctypes.c_size_t(0)
+        rc = L.bpe_dec_decode(self._decoder(), arr, len(ids), None, 0, ctypes.byref(n_out))
+        if rc != _lib.BPE_E_ARG or n_out.value == 0:   # size query, or KeyError / empty result
+            if rc == _lib.BPE_E_KEY:
+                raise KeyError(int((L.bpe_last_error() or b"0").decode()))
+            _lib.check(rc, "decode")
+        buf = (ctypes.c_uint8 * max(n_out.value, 1))()
+        _lib.check(L.bpe_dec_decode(self._decoder(), arr, len(ids), buf, n_out.value, ctypes.byref(n_out)),
+                   "decode")
+        return bytes(buf[:n_out.value]).decode("utf-8", errors="replace")
 
     def save(self, path: str, prefix: str = ""):
         os.makedirs(path, exist_ok=True)
