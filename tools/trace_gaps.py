@@ -43,7 +43,7 @@ def main():
     print(f"# {path}: {len(rows)} dispatches, {rnd + 1} k_merge rounds, bucket {bucket} rounds")
     print(f"{'kernel':18s} {'bucket':>6s} {'n':>7s} {'dur_med':>8s} {'dur_mean':>8s} {'dur_p90':>8s} "
           f"{'gap_med':>8s} {'gap_mean':>8s}")
-    for k in ("k_merge<unsigned short>", "k_merge<unsigned int>", "k_apply", "k_argmax"):
+    for k in ("k_merge<unsigned short>", "k_merge<unsigned int>", "k_apply", "k_apply_argmax", "k_argmax"):
         if k not in dur:
             continue
         for b in sorted(dur[k]):

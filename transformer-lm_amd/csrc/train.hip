@@ -579,11 +579,27 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
 // created (a decrement of a missing key creates it, as the reference's defaultdict does)
 __device__ __forceinline__ size_t pair_update(const PairsDev& P, RoundState* st, unsigned p, unsigned q,
                                               long long delta, bool inc, long long* c_out, unsigned* f_out) {
-    bool ins;
-    const size_t s = pair_slot(P, pair_key(p, q), st, &ins);
-    if (s == ~(size_t)0) return s;
-    const long long c = P.cnt[s] + delta;
-    unsigned f = P.flag[s];
+    const unsigned long long key = pair_key(p, q);
+    const size_t s0 = mix64(key) & P.mask;
+    // the home slot's key, count and flags in one step: at load <= 1/2 the first probe usually
+    // decides, so the usual chain is one dependent load
+    const unsigned long long k0 = P.key[s0];
+    long long c = P.cnt[s0];
+    unsigned f = P.flag[s0];
+    bool ins = false;
+    size_t s = s0;
+    if (k0 != key) {
+        s = pair_slot(P, key, st, &ins);
+        if (s == ~(size_t)0) return s;
+        if (ins) {          // a slot this call claimed was empty: count and flags are 0
+            c = 0;
+            f = 0;
+        } else {
+            c = P.cnt[s];
+            f = P.flag[s];
+        }
+    }
+    c += delta;
     P.cnt[s] = c;
     if ((inc || ins) && !(f & kPresent)) {
         f |= kPresent;
@@ -612,9 +628,10 @@ __global__ void __launch_bounds__(kApplyThreads) k_apply_argmax(RoundState* __re
         const unsigned a = st->cur_a, b = st->cur_b, nw = st->cur_new;
         const long long T = st->T;
         // a key this thread updated: candidate if present and >= T; increments may admit it
-        auto consider = [&](size_t s, unsigned p, unsigned q, long long c, unsigned f, bool inc) -> bool {
+        auto consider = [&](size_t s, unsigned p, unsigned q, unsigned long long ka, unsigned long long kb,
+                            long long c, unsigned f, bool inc) -> bool {
             if (s == ~(size_t)0 || !(f & kPresent) || c < T) return false;
-            const Cand cand{c, K.key8[p], K.key8[q], (unsigned)s, p, q};
+            const Cand cand{c, ka, kb, (unsigned)s, p, q};
             if (cand_better(cand, best, K.pool, K.off, K.len)) best = cand;
             if (inc && !(f & kInC)) {
                 P.flag[s] = f | kInC;
@@ -632,10 +649,11 @@ __global__ void __launch_bounds__(kApplyThreads) k_apply_argmax(RoundState* __re
                     const unsigned p = op == 0 ? x : op == 1 ? x : op == 2 ? b : nw;
                     const unsigned q = op == 0 ? a : op == 1 ? nw : x;
                     const bool inc = op & 1;
+                    const unsigned long long ka = K.key8[p], kb = K.key8[q];   // issued with the probe
                     long long c;
                     unsigned f;
                     const size_t s = pair_update(P, st, p, q, inc ? d : -d, inc, &c, &f);
-                    if (consider(s, p, q, c, f, inc)) { add = true; add_e = make_uint4((unsigned)s, p, q, 0u); }
+                    if (consider(s, p, q, ka, kb, c, f, inc)) { add = true; add_e = make_uint4((unsigned)s, p, q, 0u); }
                 }
             }
             if (g == 0) {   // the four keys two cells can update
@@ -657,7 +675,7 @@ __global__ void __launch_bounds__(kApplyThreads) k_apply_argmax(RoundState* __re
                     unsigned f;
                     const bool inc = sp[k].inc != 0;
                     const size_t s = pair_update(P, st, sp[k].p, sp[k].q, sp[k].inc - sp[k].dec, inc, &c, &f);
-                    if (consider(s, sp[k].p, sp[k].q, c, f, inc)) {
+                    if (consider(s, sp[k].p, sp[k].q, K.key8[sp[k].p], K.key8[sp[k].q], c, f, inc)) {
                         // thread 0 appends its own admissions here (at most four)
                         const unsigned idx = atomicAdd(&st->nC, 1u);
                         if (idx < st->capC) P.C[idx] = make_uint4((unsigned)s, sp[k].p, sp[k].q, 0u);
