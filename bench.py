@@ -8,8 +8,10 @@ merges/vocab back on the host.  OWT itself is not available offline; the corpus 
 library's deterministic generator (bpe_synth_corpus_device), `--bytes` per GPU.
 
 Multi-GPU (torchrun, one rank per GPU): each rank owns a slab of the same global corpus (weak
-scaling: per-GPU bytes fixed), trains on it, and the ranks exchange the per-round pair deltas
-with one RCCL all-reduce; every rank ends with the identical global merge list.
+scaling: per-GPU bytes fixed) and pre-tokenizes/counts it; ONE RCCL all-gather of the slabs'
+unique-word tables follows, and every rank trains on their union (no per-round collective;
+BPE355_EXCHANGE=rounds selects the per-round all-reduce of the pair deltas instead).  Every rank
+ends with the identical global merge list.
 
 Prints ONE JSON line on rank 0.  Extra fields: merges_per_s, encode MB/s (Tokenizer.encode of
 the same corpus with the trained merges), roofline of the dominant kernel (HIP events on the
@@ -69,7 +71,7 @@ def main():
     if world > 1:
         from bpe_amd.dist import Communicator
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        comm = Communicator.from_torch(local_rank)   # RCCL: one int64 all-reduce per merge round
+        comm = Communicator.from_torch(local_rank)   # RCCL: one all-gather of the word tables
 
     # ---------------------------------------------------------------- corpus slab in HBM
     blocks = max(1, int(args.bytes) // BLOCK)
@@ -199,16 +201,20 @@ def main():
                                    "special <|endoftext|> (BASELINE configs[2])",
                        "bytes_per_gpu": n, "vocab_size": args.vocab, "merges": rounds,
                        "seed": args.seed, "flavour": args.flavour,
-                       "parallelism": f"corpus slabs x{world}, RCCL all-reduce per merge round"},
+                       "parallelism": (f"corpus slabs x{world}, " + (
+                           "RCCL all-reduce of the pair deltas per merge round"
+                           if os.environ.get("BPE355_EXCHANGE") == "rounds" else
+                           "one RCCL all-gather of the unique-word tables, then every rank "
+                           "trains on their union")) if world > 1 else "1 GPU"},
             "merges_per_s": round(rounds / (merge_ms / 1e3), 1) if merge_ms else None,
             "encode": encode,
             "roofline": roofline,
             "cpu_baseline": cpu,
-            "phases_ms": {k: round(s0[k], 2) for k in ("t_prepare_ms", "t_count_ms", "t_words_ms",
-                                                        "t_merge_ms", "t_total_ms")},
-            "counters": {k: s0[k] for k in ("n_pretokens", "n_words", "n_pairs_final",
-                                            "n_rebuilds", "n_rounds_device", "n_rounds_host",
-                                            "n_index_builds")},
+            "phases_ms": {k: round(s0[k], 2) for k in ("t_prepare_ms", "t_count_ms", "t_exchange_ms",
+                                                        "t_words_ms", "t_merge_ms", "t_total_ms")},
+            "counters": {k: s0[k] for k in ("n_pretokens", "n_words", "n_exchanged_words",
+                                            "n_pairs_final", "n_rebuilds", "n_rounds_device",
+                                            "n_rounds_host", "n_index_builds")},
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -1,12 +1,16 @@
-"""World-size-2 `gloo` test of the SHARDED training protocol, on CPU (no GPU needed).
+"""`gloo` tests (world size 2 and 3) of the SHARDED training protocols, on CPU (no GPU needed).
 
-libbpe355 shards the corpus into slabs cut at safe points (one per rank), keeps each rank's
-unique words local, and per merge round all-reduces one fixed-layout int64 buffer of delta
-cells (L[x] for (x,a)-=c/(x,new)+=c and R[y] for (b,y)-=c/(new,y)+=c); every rank applies the
-global deltas to a replicated pair table and takes the same argmax.  This test restates that
-protocol in plain Python over torch.distributed/gloo and checks that the sharded run produces
-exactly the merges of the unsharded reference semantics (the oracle, pinned to the reference's
-goldens in test_oracle_golden.py).
+libbpe355 shards the corpus into slabs cut at safe points (one per rank) and has two ways to
+combine them (exchange.hip, train.hip):
+  words  (default)  each rank counts its slab's unique words; ONE all-gather of the word tables;
+                    every rank trains on the union (counts summed) with no further collective;
+  rounds            each rank keeps its unique words local and per merge round all-reduces one
+                    fixed-layout int64 buffer of delta cells (L[x] for (x,a)-=c/(x,new)+=c and
+                    R[y] for (b,y)-=c/(new,y)+=c); every rank applies the global deltas to a
+                    replicated pair table and takes the same argmax.
+These tests restate both protocols in plain Python over torch.distributed/gloo and check that
+every rank produces exactly the merges of the unsharded reference semantics (the oracle, pinned
+to the reference's goldens in test_oracle_golden.py).
 """
 import multiprocessing as mp
 import os
@@ -36,13 +40,21 @@ def safe_split(data: bytes, pos: int) -> int:
     return 0
 
 
-def sharded_train(rank, world, slab: bytes, vocab_size, specials):
+def sharded_train(rank, world, slab: bytes, vocab_size, specials, mode="rounds"):
     import torch
     import torch.distributed as dist
 
     # local unique words (train.py:16-28 on this rank's slab; single bytes carry no pairs)
     text = oracle.decode_text(slab)
     counts = oracle.word_counts(text, specials)
+    if mode == "words":
+        # the one collective: gather every rank's table, sum the counts word by word
+        gathered = [None] * world
+        dist.all_gather_object(gathered, counts)
+        counts = {}
+        for table in gathered:
+            for w, c in table.items():
+                counts[w] = counts.get(w, 0) + c
     words = [[bytes([c]) for c in w] for w in counts if len(w) >= 2]
     freq = [counts[w] for w in counts if len(w) >= 2]
 
@@ -59,6 +71,8 @@ def sharded_train(rank, world, slab: bytes, vocab_size, specials):
     W = [[tid[c] for c in w] for w in words]
 
     def allreduce(vals):
+        if mode == "words":   # the union is global already: no per-round exchange
+            return vals
         t = torch.tensor(vals, dtype=torch.int64)
         dist.all_reduce(t)
         return t.tolist()
@@ -120,24 +134,24 @@ def sharded_train(rank, world, slab: bytes, vocab_size, specials):
     return merges
 
 
-def _worker(rank, world, port, slabs, vocab_size, specials, q):
+def _worker(rank, world, port, slabs, vocab_size, specials, q, mode):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank, sharded_train(rank, world, slabs[rank], vocab_size, specials)))
+        q.put((rank, sharded_train(rank, world, slabs[rank], vocab_size, specials, mode)))
     finally:
         dist.destroy_process_group()
 
 
-def run_sharded(data: bytes, world: int, vocab_size: int, specials):
+def run_sharded(data: bytes, world: int, vocab_size: int, specials, mode="rounds"):
     cuts = [0] + [safe_split(data, len(data) * r // world) for r in range(1, world)] + [len(data)]
     slabs = [data[cuts[r]:cuts[r + 1]] for r in range(world)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, slabs, vocab_size, specials, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, slabs, vocab_size, specials, q, mode))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -148,11 +162,12 @@ def run_sharded(data: bytes, world: int, vocab_size: int, specials):
     return out
 
 
+@pytest.mark.parametrize("mode", ["words", "rounds"])
 @pytest.mark.parametrize("name,world", [("corpus_en_500", 2), ("tiny_1200", 2),
                                         ("synth_mixed_200k", 2), ("corpus_en_1000", 3)])
-def test_sharded_protocol_matches_reference(name, world):
+def test_sharded_protocol_matches_reference(name, world, mode):
     o, _vocab, merges = G.train_expect(name)
     data = G.input_bytes(o["input"])   # raw bytes: slabs are cut at safe points, then decoded
-    out = run_sharded(data, world, o["vocab_size"], o["special_tokens"])
+    out = run_sharded(data, world, o["vocab_size"], o["special_tokens"], mode)
     for r in range(world):   # every rank holds the identical, global merge list
         assert out[r] == merges

@@ -13,6 +13,9 @@ import pathlib
 import struct
 
 LIB_PATH = pathlib.Path(__file__).resolve().parent.parent / "lib" / "libbpe355.so"
+# experiment knob: an alternative build of the same library (A/B timing of kernel variants)
+if os.environ.get("BPE355_LIB"):
+    LIB_PATH = pathlib.Path(os.environ["BPE355_LIB"]).resolve()
 
 BPE_OK, BPE_E_IO, BPE_E_UTF8, BPE_E_KEY, BPE_E_HIP, BPE_E_ARG, BPE_E_NOMEM, BPE_E_RCCL, \
     BPE_E_LIMIT = 0, -1, -2, -3, -4, -5, -6, -7, -8
@@ -33,6 +36,7 @@ class TrainStats(ctypes.Structure):
         ("n_word_tokens", ctypes.c_int64), ("n_pairs_final", ctypes.c_int64),
         ("n_rebuilds", ctypes.c_int64), ("n_rounds_device", ctypes.c_int64),
         ("n_rounds_host", ctypes.c_int64), ("n_index_builds", ctypes.c_int64),
+        ("t_exchange_ms", ctypes.c_double), ("n_exchanged_words", ctypes.c_int64),
     ]
 
     def as_dict(self):

@@ -1,6 +1,7 @@
-// Communicators for the sharded trainer: one process per GPU, corpus slabs per rank, one
-// sum all-reduce of the per-round pair deltas (and once of the initial byte-pair
-// histogram).  RCCL over xGMI in production; a host-staged variant lets the sharded path be
+// Communicators for the sharded trainer: one process per GPU, corpus slabs per rank.  The
+// default exchange is one all-gather of the ranks' unique-word tables (exchange.hip); the
+// per-round exchange (BPE355_EXCHANGE=rounds) is one sum all-reduce of the pair deltas per
+// merge round (and once of the initial byte-pair histogram).  RCCL over xGMI in production; a host-staged variant lets the sharded path be
 // exercised by several processes that share one GPU (tests).
 #include <rccl/rccl.h>
 
@@ -39,6 +40,10 @@ struct RcclComm final : Comm {
     void allreduce_i64(int64_t* d_buf, size_t count, hipStream_t stream) override {
         if (count == 0) return;
         BPE_NCCL(ncclAllReduce(d_buf, d_buf, count, ncclInt64, ncclSum, comm, stream));
+    }
+    void allgather_bytes(const void* d_send, size_t bytes, void* d_recv, hipStream_t stream) override {
+        if (bytes == 0) return;
+        BPE_NCCL(ncclAllGather(d_send, d_recv, bytes, ncclUint8, comm, stream));
     }
 };
 

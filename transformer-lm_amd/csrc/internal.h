@@ -18,6 +18,9 @@ struct Comm {
     virtual ~Comm() = default;
     // in-place sum over ranks of d_buf[0..count) (device memory), ordered on `stream`
     virtual void allreduce_i64(int64_t* d_buf, size_t count, hipStream_t stream) = 0;
+    // d_recv[r * bytes .. (r + 1) * bytes) = rank r's d_send[0 .. bytes) (default: through
+    // allreduce_i64; RCCL overrides it with ncclAllGather)
+    virtual void allgather_bytes(const void* d_send, size_t bytes, void* d_recv, hipStream_t stream);
 };
 
 // ---------------------------------------------------------------- text preparation
@@ -38,6 +41,12 @@ struct WordCounts {
 // (Single-byte words carry no pairs and cannot affect training.)
 void count_words(const uint8_t* d_text, size_t n, WordCounts& wc, hipStream_t stream,
                  float* kernel_ms);
+
+// ---------------------------------------------------------------- multi-GPU word exchange
+// Replace this rank's word table by the union of every rank's (counts summed), whose words'
+// bytes live in `all` (exchange.hip).  One all-gather; afterwards no rank needs the others.
+void union_word_tables(const uint8_t* text, WordCounts& wc, Comm* comm, hipStream_t stream,
+                       DevBuf<uint8_t>& all, uint64_t* union_words);
 
 // ---------------------------------------------------------------- training driver
 struct TrainOutput {

@@ -1721,10 +1721,27 @@ void train_on_device(const uint8_t* d_raw, size_t n, int vocab_size,
         return;
     }
     BPE_REQUIRE(rounds < (1LL << 31) - 512, BPE_E_LIMIT, "vocab_size too large");
+    // several ranks: by default exchange the word tables once and train on their union with no
+    // per-round collective (exchange.hip); BPE355_EXCHANGE=rounds keeps the slabs' words local and
+    // all-reduces the pair deltas every round.  BPE355_FORCE_EXCHANGE=1 runs the word exchange
+    // on a 1-rank communicator too (tests the collective on a single-GPU box).
+    DevBuf<uint8_t> union_text;
+    Comm* loop_comm = comm;
+    const char* ex = std::getenv("BPE355_EXCHANGE");
+    const bool per_round = ex && std::string(ex) == "rounds";
+    if (comm && !per_round && (comm->nranks > 1 || std::getenv("BPE355_FORCE_EXCHANGE"))) {
+        auto te = std::chrono::steady_clock::now();
+        uint64_t uw = 0;
+        union_word_tables(text, wc, comm, stream, union_text, &uw);
+        text = union_text.p;
+        loop_comm = nullptr;
+        out.stats.t_exchange_ms = ms_since(te);
+        out.stats.n_exchanged_words = (int64_t)uw;
+    }
     auto go = [&](auto tag) {
         using TokT = decltype(tag);
         auto t2 = std::chrono::steady_clock::now();
-        MergeLoop<TokT> loop(stream, comm, text, (int)rounds, out);
+        MergeLoop<TokT> loop(stream, loop_comm, text, (int)rounds, out);
         loop.build_words(wc, specials);
         { WordCounts drop = std::move(wc); }
         out.stats.t_words_ms = ms_since(t2);
