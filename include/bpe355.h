@@ -111,6 +111,8 @@ typedef struct {
     int64_t n_rounds_device;  /* merges decided on the device */
     int64_t n_rounds_host;    /* zero-count merges emitted after exhaustion */
     int64_t n_index_builds;   /* word-table compactions + posting-list builds */
+    int64_t n_trips;          /* merge-loop round trips (several exact merges each when batched) */
+    int64_t n_rounds_batched; /* rounds taken in trips of more than one merge */
     double t_exchange_ms;     /* multi-GPU word-table exchange (0 on one rank) */
     int64_t n_exchanged_words; /* local unique words of all ranks gathered (before dedupe) */
 } bpe_train_stats;

@@ -36,6 +36,7 @@ class TrainStats(ctypes.Structure):
         ("n_word_tokens", ctypes.c_int64), ("n_pairs_final", ctypes.c_int64),
         ("n_rebuilds", ctypes.c_int64), ("n_rounds_device", ctypes.c_int64),
         ("n_rounds_host", ctypes.c_int64), ("n_index_builds", ctypes.c_int64),
+        ("n_trips", ctypes.c_int64), ("n_rounds_batched", ctypes.c_int64),
         ("t_exchange_ms", ctypes.c_double), ("n_exchanged_words", ctypes.c_int64),
     ]
 

@@ -171,7 +171,7 @@ __global__ void __launch_bounds__(256, 3) k_count_words(const uint8_t* __restric
                                                      unsigned long long* __restrict__ pos, size_t mask, unsigned long long max_fill,
                                                      unsigned long long* __restrict__ fill,
                                                      unsigned* __restrict__ status,
-                                                     unsigned long long* __restrict__ n_tok) {
+                                                     unsigned long long* __restrict__ n_tok, int mode) {
     __shared__ unsigned long long c_key[kCache];
     __shared__ uint64_t c_lo[kCache], c_hi[kCache];
     __shared__ unsigned c_cnt[kCache];
@@ -188,6 +188,7 @@ __global__ void __launch_bounds__(256, 3) k_count_words(const uint8_t* __restric
     auto count_token = [&](const auto& src, auto r, size_t len, size_t gpos) {
         if (len < 2) return;
         ++ntok;
+        if (mode == 1) return;   // analysis knob (BPE355_COUNT_MODE=1): the scan alone
         if (len >= (1ULL << 24)) {
             atomicOr(status, 2u);
         } else if (len <= kInline) {
@@ -223,9 +224,11 @@ __global__ void __launch_bounds__(256, 3) k_count_words(const uint8_t* __restric
                 }
             }
             ++n_miss;
+            if (mode == 2) return;   // analysis knob: LDS cache only, misses dropped
             inserted += global_add(s, s, gpos, len, wl, wh, h, 1, kv, pos, mask, status);
         } else {
             ++n_long;
+            if (mode == 2) return;
             inserted += global_add(s, s, gpos, len, 0, 0, hash_word(s, gpos, len), 1, kv, pos, mask, status);
         }
     };
@@ -375,6 +378,8 @@ void count_words(const uint8_t* d_text, size_t n, WordCounts& wc, hipStream_t st
                                                (size_t)std::max(1, per_cu) * std::max(1, n_cu));
     if (const char* e = std::getenv("BPE355_STREAM_WG"))   // test knob: fewer workgroups, each
         grid = std::max(1u, std::min(grid, (unsigned)std::atoi(e)));   // streaming many chunks
+    // analysis knob: 1 = scan only, 2 = LDS word cache only (counts incomplete: timing only)
+    static const int count_mode = std::getenv("BPE355_COUNT_MODE") ? std::atoi(std::getenv("BPE355_COUNT_MODE")) : 0;
     for (int attempt = 0;; ++attempt) {
         wc.kv.alloc(2 * cap);
         wc.pos.alloc(cap);
@@ -389,7 +394,7 @@ void count_words(const uint8_t* d_text, size_t n, WordCounts& wc, hipStream_t st
             hipExtLaunchKernelGGL(kern, dim3(grid), dim3(256), kPadded, stream,
                                   kernel_ms ? e0 : nullptr, kernel_ms ? e1 : nullptr, 0,
                                   d_text, n, n_chunks, wc.kv.p, wc.pos.p, cap - 1,
-                                  (unsigned long long)(cap / 2), fill.p, status.p, ntok.p);
+                                  (unsigned long long)(cap / 2), fill.p, status.p, ntok.p, count_mode);
             BPE_HIP(hipGetLastError());
         }
         unsigned st = 0;

@@ -54,7 +54,7 @@ namespace bpe {
 namespace {
 
 constexpr unsigned kPresent = 1u, kInC = 2u;
-enum : int { HALT_NONE = 0, HALT_REBUILD = 1, HALT_DONE = 2 };
+enum : int { HALT_NONE = 0, HALT_REBUILD = 1, HALT_DONE = 2, HALT_HOST = 3 };
 enum : unsigned { ERR_PAIRS_FULL = 1u, ERR_C_FULL = 2u, ERR_POOL = 4u };
 constexpr unsigned long long kPolyP = 0x100000001B3ULL * 0x9E3779B97F4A7C15ULL | 1ULL;
 constexpr int kNumCls = 4;
@@ -77,6 +77,14 @@ struct RoundState {
     unsigned pool_used, pool_cap;
     unsigned long long pair_used;
     unsigned long long scan_slots;
+    int nparts;                 // batched: apply workgroups whose top-M lists part[] holds
+    int pad1;
+    // batched rounds (k_select): the host's limits, checked before every trip
+    int host_round;             // hand back to the host at this round (compaction schedule)
+    unsigned single_limit;      // ... or when this many words became one token (compaction)
+    unsigned max_len;           // longest word (bytes): the most one new token adds to the pool
+    int max_batch;              // merges allowed per trip (1: one merge per trip)
+    unsigned long long pair_limit;   // ... or when the pair table could pass this many keys
 };
 
 struct Partial {
@@ -146,7 +154,7 @@ struct IndexDev {
 template <class TokT> __host__ __device__ constexpr TokT sentinel() { return (TokT)~(TokT)0; }
 
 // bytes(x) vs bytes(y) for tokens whose 8-byte prefixes are equal: -1 / 0 / +1
-__device__ __noinline__ int cmp_tok_tail(const uint8_t* __restrict__ pool, const uint32_t* __restrict__ off,
+__device__ __forceinline__ int cmp_tok_tail(const uint8_t* __restrict__ pool, const uint32_t* __restrict__ off,
                                          const uint32_t* __restrict__ len, unsigned x, unsigned y) {
     const unsigned lx = len[x], ly = len[y], m = lx < ly ? lx : ly;
     const uint8_t* px = pool + off[x];
@@ -383,7 +391,8 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
                                                PairsDev P, ToksDev K, WordsDev<TokT> W,
                                                IndexDev X, unsigned long long* __restrict__ LR,
                                                uint32_t* __restrict__ m_a, uint32_t* __restrict__ m_b,
-                                               uint32_t* __restrict__ m_new, uint32_t* __restrict__ m_mode) {
+                                               uint32_t* __restrict__ m_new, uint32_t* __restrict__ m_mode,
+                                               long long* __restrict__ m_cnt) {
     __shared__ BestShared sb;
     __shared__ unsigned long long l_lr[2 * kLdsLR];
     __shared__ Cand s_part[4];
@@ -494,6 +503,7 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
             st->cur_a = a; st->cur_b = b; st->cur_new = nw; st->cur_slot = sb.slot;
             st->cur_cnt = sb.cnt; st->new_is_new = (int)sb.isnew;
             m_a[sb.round] = a; m_b[sb.round] = b; m_new[sb.round] = nw;
+            if (m_cnt) m_cnt[sb.round] = sb.cnt;
             m_mode[sb.round] = sb.use_list ? sb.list_len : 0xffffffffu;
             X.beg[nw] = sb.cov_beg;
             X.len[nw] = sb.cov_len;
@@ -760,6 +770,609 @@ __global__ void __launch_bounds__(256) k_argmax(RoundState* __restrict__ st, Pai
         for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
             if (cand_better(sw[k], best, K.pool, K.off, K.len)) best = sw[k];
         part[blockIdx.x] = Partial{best.cnt, best.ka, best.kb, best.slot, best.a, best.b, 0};
+    }
+}
+
+// ------------------------------------------------------------------ batched rounds
+// Several merges per round trip, exactly.  At a state S, let P1 > P2 > ... be the candidates in
+// the reference's order (count, then bytes; train.py:187-189).  The top k form a batch when
+//   (1) their tokens are pairwise disjoint and (2) a != b for each (k > 1),
+//   (3) each a + b is new bytes: not an existing token, not another member's (vocab.py:29),
+//   (4) count(Pk) >= T and count(Pk) > count of the next candidate in C (keys outside C are
+//       below T), so every pair outside the batch has a count strictly below count(Pk).
+// Then the reference takes P1, ..., Pk in exactly that order:
+//   * disjoint tokens: merging Pi never touches an occurrence of Pj (j != i), so Pj's count is
+//     unchanged until its turn; with a != b every occurrence of Pi is merged;
+//   * an occurrence of a pair created by the batch sits where, before the batch, two original
+//     tokens met -- an occurrence of an old pair that is not a member (members' occurrences are
+//     all merged) -- so its count is below count(Pk); old non-members only lose counts.
+// The rewrite applies the members in order to each word (the deltas of member j see the word
+// after members < j, as the reference's sequence of rounds does), so counts, present keys and
+// words after the trip equal the state after k rounds.
+constexpr int kMaxBatch = 8;
+constexpr int kTopM = kMaxBatch + 1;
+constexpr unsigned kLdsB = 256;          // LDS-summed cells per member (ids below kLdsB)
+
+struct BatchMember {
+    unsigned a, b, nw, slot;
+    long long cnt;
+    unsigned long long hash, k8, pw;
+    unsigned ln, list_beg, list_len, use_list, cov_beg, cov_len, pool_off, isnew;
+};
+struct Batch {
+    int stop;            // 0 run, -1 nothing to do
+    int k;               // members
+    int round, ntok;     // round of member 0, token count before the batch
+    int trip, prev_k;    // trip number (cell parity), members of the previous trip
+    unsigned batch_id;   // word claims of this batch
+    unsigned full_scan;  // a member has no usable posting list: scan every word once
+    unsigned n_fresh;    // members that create a token
+    unsigned nC_base;    // C entries before this trip's admissions (the apply scans them)
+    unsigned list_pre[kMaxBatch + 1];   // prefix sums of the members' list lengths
+    BatchMember m[kMaxBatch];
+};
+
+// device-owned batch state (the host only initializes it; its limits live in RoundState)
+struct BatchState {
+    unsigned pend_insert;    // the last batch's new tokens still have to enter the dedupe map
+    unsigned batch_seq;      // last batch_id handed out
+    int trip;                // trips completed
+    int prev_k;              // members of the last trip (its cells are cleared by the next apply)
+    unsigned long long rounds_batched;   // statistics: rounds taken in batches of k > 1
+    unsigned long long trips_batched;
+};
+
+struct TokMetaS {
+    unsigned long long ha, pb, hb, pa;   // hash(a), P^len(b), hash(b), P^len(a)
+    unsigned la, lb, za, zb, ba, bb;     // lengths; posting lists of a and b (len, begin)
+};
+
+template <unsigned N>
+struct DeltaSinkN {
+    unsigned long long* LR;     // this member's global cells
+    unsigned long long* lds;    // this member's LDS cells (ids below N)
+    __device__ __forceinline__ void add(unsigned cell, unsigned long long c) const {
+        if (cell < 2 * N) atomicAdd(&lds[cell], c);
+        else atomicAdd(&LR[cell], c);
+    }
+};
+
+// A wave's sorted top-M candidates, distributed: lane i < M holds the i-th best (cand_none
+// padding), so no lane keeps an array.
+__device__ __forceinline__ Cand shfl_cand(const Cand& c, int src) {
+    Cand r;
+    r.cnt = __shfl(c.cnt, src);
+    r.ka = __shfl(c.ka, src);
+    r.kb = __shfl(c.kb, src);
+    r.slot = __shfl(c.slot, src);
+    r.a = __shfl(c.a, src);
+    r.b = __shfl(c.b, src);
+    return r;
+}
+// every lane of the wave calls; lanes with `has` offer c
+template <int M>
+__device__ __forceinline__ void wave_top_offer(Cand& mine, bool has, const Cand& c, const ToksDev& K) {
+    const int lane = threadIdx.x & 63;
+    const Cand last = shfl_cand(mine, M - 1);
+    unsigned long long pend = __ballot(has && cand_better(c, last, K.pool, K.off, K.len));
+    while (pend) {
+        const int src = __ffsll((long long)pend) - 1;
+        pend &= pend - 1;
+        const Cand x = shfl_cand(c, src);
+        const bool ahead = lane < M && cand_better(mine, x, K.pool, K.off, K.len);
+        const int pos = __popcll(__ballot(ahead));   // entries that stay ahead of x
+        if (pos < M) {
+            const Cand up = shfl_cand(mine, lane > 0 ? lane - 1 : 0);
+            if (lane > pos && lane < M) mine = up;
+            if (lane == pos) mine = x;
+        }
+    }
+}
+// a workgroup's top-M from its waves' lists (every thread calls; out[0..M) valid after return)
+template <int M, int NW>
+__device__ __forceinline__ void block_top(const Cand& mine, Cand (*s_wave)[M], Cand* out, const ToksDev& K) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane < M) s_wave[wv][lane] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int head[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) head[w] = 0;
+        for (int t = 0; t < M; ++t) {
+            int bw = -1;
+            Cand bc = cand_none();
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                if (head[w] >= M) continue;
+                const Cand x = s_wave[w][head[w]];
+                if (x.cnt != LLONG_MIN && (bw < 0 || cand_better(x, bc, K.pool, K.off, K.len))) { bw = w; bc = x; }
+            }
+            out[t] = bc;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) head[w] += (w == bw);
+        }
+    }
+    __syncthreads();
+}
+
+constexpr int kSelThreads = 512;
+// One workgroup: the top-(kMaxBatch + 1) candidates of C, the batch rule, the batch record, and
+// the merge records of its rounds.  Also puts the previous batch's new tokens into the dedupe
+// map first (single writer of the map).
+__global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__ st, BatchState* __restrict__ bs,
+                                                        PairsDev P, ToksDev K, IndexDev X, Batch* __restrict__ bt,
+                                                        const Partial* __restrict__ part,
+                                                        uint32_t* __restrict__ m_a, uint32_t* __restrict__ m_b,
+                                                        uint32_t* __restrict__ m_new, uint32_t* __restrict__ m_mode,
+                                                        long long* __restrict__ m_cnt, int* __restrict__ trip_info,
+                                                        int trip_slot) {
+    __shared__ Cand s_wave[kSelThreads / 64][kTopM];
+    __shared__ Cand s_fin[kTopM];
+    __shared__ int s_nfin, s_stop;
+    __shared__ unsigned s_fresh[kTopM], s_nw_old[kTopM];
+    __shared__ TokMetaS s_meta[kTopM];
+    const int tid = threadIdx.x;
+    // ---- the previous batch's tokens enter the dedupe map
+    if (bs->pend_insert) {
+        const int pk = bt->k;
+        if (tid < pk && bt->m[tid].isnew) {
+            const unsigned nw = bt->m[tid].nw;
+            unsigned s = (unsigned)mix64(bt->m[tid].hash) & K.map_mask;
+            while (atomicCAS(&K.map[s], 0u, nw + 1) != 0u) s = (s + 1) & K.map_mask;
+        }
+        __syncthreads();
+        if (tid == 0) bs->pend_insert = 0;
+    }
+    const int halt = st->halt;
+    if (halt) {
+        if (tid == 0) {
+            bt->stop = -1;
+            if (trip_info) { trip_info[2 * trip_slot] = -1; trip_info[2 * trip_slot + 1] = 0; }
+        }
+        return;
+    }
+    // ---- the top-M of the apply workgroups' top-M lists
+    const unsigned nC = st->nC;
+    const long long T = st->T;
+    const int nlists = st->nparts;
+    Cand mine = cand_none();
+    for (int base = tid & ~63; base < nlists * kTopM; base += kSelThreads) {
+        const int i = base + (tid & 63);
+        Cand c = cand_none();
+        if (i < nlists * kTopM) {
+            const Partial q = part[i];
+            c = Cand{q.cnt, q.ka, q.kb, q.slot, q.a, q.b};
+        }
+        wave_top_offer<kTopM>(mine, c.cnt != LLONG_MIN, c, K);
+    }
+    block_top<kTopM, kSelThreads / 64>(mine, s_wave, s_fin, K);
+    if (tid == 0) {
+        int nf = 0;
+        while (nf < kTopM && s_fin[nf].cnt != LLONG_MIN) ++nf;
+        s_nfin = nf;
+        const int round = st->round;
+        int stop = HALT_NONE;
+        if (round >= st->n_rounds) stop = HALT_DONE;
+        else if (nC > st->c_limit) stop = HALT_REBUILD;               // C bloated: re-threshold
+        else if (nf == 0 || s_fin[0].cnt < T) stop = HALT_REBUILD;    // max(C) < T: re-threshold
+        else if (round >= st->host_round || st->n_single > st->single_limit ||
+                 st->pair_used + 2ull * (unsigned)(st->ntok + kMaxBatch) * kMaxBatch > st->pair_limit ||
+                 st->pool_used + (unsigned long long)kMaxBatch * st->max_len > st->pool_cap)
+            stop = HALT_HOST;
+        s_stop = stop;
+        if (stop) {
+            st->halt = stop;
+            bt->stop = -1;
+            if (trip_info) { trip_info[2 * trip_slot] = -1; trip_info[2 * trip_slot + 1] = 0; }
+        }
+    }
+    __syncthreads();
+    if (s_stop) return;
+    // ---- the candidates' token metadata and dedupe lookups (one thread each)
+    const int nf = s_nfin;
+    const int ntok = st->ntok;
+    if (tid < nf && tid < kMaxBatch) {
+        const Cand c = s_fin[tid];
+        const unsigned a = c.a, b = c.b;
+        TokMetaS m;
+        m.ha = K.hash[a]; m.pb = K.pw[b]; m.hb = K.hash[b]; m.pa = K.pw[a];
+        m.la = K.len[a]; m.lb = K.len[b];
+        m.za = X.len[a]; m.zb = X.len[b]; m.ba = X.beg[a]; m.bb = X.beg[b];
+        const unsigned long long h = m.ha * m.pb + m.hb;
+        const unsigned ln = m.la + m.lb;
+        unsigned s = (unsigned)mix64(h) & K.map_mask;
+        unsigned old = ~0u;
+        for (unsigned mm = K.map[s]; mm != 0; s = (s + 1) & K.map_mask, mm = K.map[s]) {
+            const unsigned id = mm - 1;
+            if (K.hash[id] == h && K.len[id] == ln && equals_concat(K, id, a, b)) { old = id; break; }
+        }
+        s_meta[tid] = m;
+        s_fresh[tid] = old == ~0u;
+        s_nw_old[tid] = old;
+    }
+    __syncthreads();
+    if (tid != 0) return;
+    // ---- the batch rule
+    const int maxb = min(st->max_batch, kMaxBatch);
+    int k = 1;
+    {
+        unsigned used[2 * kMaxBatch];
+        int nu = 0;
+        const Cand& p0 = s_fin[0];
+        const bool first_ok = p0.a != p0.b && s_fresh[0];
+        used[nu++] = p0.a;
+        used[nu++] = p0.b;
+        while (first_ok && k < maxb && k < nf) {
+            const Cand& c = s_fin[k];
+            if (c.cnt < T || c.a == c.b || !s_fresh[k]) break;
+            bool clash = false;
+            for (int u = 0; u < nu; ++u) clash |= used[u] == c.a || used[u] == c.b;
+            if (clash) break;
+            // new bytes must differ from every earlier member's new bytes
+            const unsigned long long h = s_meta[k].ha * s_meta[k].pb + s_meta[k].hb;
+            for (int j = 0; j < k && !clash; ++j) {
+                const unsigned long long hj = s_meta[j].ha * s_meta[j].pb + s_meta[j].hb;
+                if (hj != h || s_meta[j].la + s_meta[j].lb != s_meta[k].la + s_meta[k].lb) continue;
+                const unsigned ln = s_meta[k].la + s_meta[k].lb;
+                bool eq = true;
+                for (unsigned i = 0; i < ln && eq; ++i)
+                    eq = concat_byte(K, s_fin[j].a, s_meta[j].la, s_fin[j].b, i) ==
+                         concat_byte(K, c.a, s_meta[k].la, c.b, i);
+                clash = eq;
+            }
+            if (clash) break;
+            used[nu++] = c.a;
+            used[nu++] = c.b;
+            ++k;
+        }
+        // (4) strictly above the next candidate (keys outside C are below T <= count(Pk))
+        while (k > 1 && k < nf && !(s_fin[k - 1].cnt > s_fin[k].cnt)) --k;
+    }
+    const int round = st->round;
+    k = min(k, st->n_rounds - round);
+    // ---- the batch record
+    Batch& B = *bt;
+    B.stop = 0;
+    B.k = k;
+    B.round = round;
+    B.ntok = ntok;
+    B.trip = bs->trip;
+    B.prev_k = bs->prev_k;
+    B.batch_id = ++bs->batch_seq;
+    B.nC_base = nC;
+    unsigned pool = st->pool_used, fresh = 0, full = 0, pre = 0;
+    for (int j = 0; j < k; ++j) {
+        const Cand& c = s_fin[j];
+        const TokMetaS& m = s_meta[j];
+        BatchMember& M = B.m[j];
+        const bool isnew = s_fresh[j];
+        M.a = c.a; M.b = c.b; M.slot = c.slot; M.cnt = c.cnt;
+        M.nw = isnew ? (unsigned)ntok + fresh : s_nw_old[j];
+        M.isnew = isnew;
+        M.hash = m.ha * m.pb + m.hb;
+        M.pw = m.pa * m.pb;
+        M.ln = m.la + m.lb;
+        M.k8 = m.la >= 8 ? c.ka : (c.ka | (c.kb >> (8 * m.la)));
+        const bool pick_a = m.za <= m.zb;
+        const unsigned lu = pick_a ? m.za : m.zb, bu = pick_a ? m.ba : m.bb;
+        M.use_list = lu != kNoAnc && lu <= X.full_threshold;
+        M.list_beg = M.use_list ? bu : 0;
+        M.list_len = M.use_list ? lu : 0;
+        M.cov_beg = bu;
+        M.cov_len = isnew ? lu : kNoAnc;   // dedupe: uncovered until the next index build
+        M.pool_off = pool;
+        if (isnew) { pool += M.ln; ++fresh; }
+        full |= !M.use_list;
+        B.list_pre[j] = pre;
+        pre += M.list_len;
+        m_a[round + j] = c.a; m_b[round + j] = c.b; m_new[round + j] = M.nw;
+        m_mode[round + j] = M.use_list ? M.list_len : 0xffffffffu;
+        if (m_cnt) m_cnt[round + j] = c.cnt;
+    }
+    B.list_pre[k] = pre;
+    B.full_scan = full;
+    B.n_fresh = fresh;
+    st->pool_used = pool;
+    bs->pend_insert = fresh != 0;
+    if (k > 1) { bs->rounds_batched += k; bs->trips_batched += 1; }
+    if (trip_info) { trip_info[2 * trip_slot] = round; trip_info[2 * trip_slot + 1] = k; }
+}
+
+// the slot word of class C addressed directly, every member applied in order
+template <class TokT, int C>
+__device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigned i, const Batch& B,
+                                                 unsigned long long* LRt, size_t lr_member,
+                                                 unsigned long long* lds, unsigned& singles) {
+    constexpr int W = slot_w(C);
+    constexpr int V = W * (int)sizeof(TokT) / 16;
+    TokT* s = S.slot + (size_t)i * W;
+    uint4 r[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) r[v] = reinterpret_cast<const uint4*>(s)[v];
+    const unsigned long long c = S.cnt[i];   // issued with the slot
+    TokT e[W];
+    __builtin_memcpy(e, r, sizeof(e));
+    for (int j = 0; j < B.k; ++j) {
+        const TokT ta = (TokT)B.m[j].a, tb = (TokT)B.m[j].b;
+        bool hit = false;
+#pragma unroll
+        for (int q = 1; q + 1 < W; ++q) hit |= (e[q] == ta) & (e[q + 1] == tb);
+        if (!hit) continue;
+        // rewrite in memory; the next member tests the rewritten word (this thread's own stores)
+        const DeltaSinkN<kLdsB> D{LRt + (size_t)j * lr_member, lds + 2 * kLdsB * j};
+        const uint32_t nl = rewrite_word(s + 1, (uint32_t)e[0], ta, tb, (TokT)B.m[j].nw, c, D, true);
+        s[0] = (TokT)nl;
+        if (nl < 2) { ++singles; break; }
+#pragma unroll
+        for (int v = 0; v < V; ++v) r[v] = reinterpret_cast<const uint4*>(s)[v];
+        __builtin_memcpy(e, r, sizeof(e));
+    }
+}
+
+template <class TokT>
+__global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st, const Batch* __restrict__ bt,
+                                                     PairsDev P, ToksDev K, WordsDev<TokT> W, IndexDev X,
+                                                     unsigned long long* __restrict__ LRbase, size_t lr_member,
+                                                     size_t lr_parity, uint32_t* __restrict__ tags) {
+    __shared__ unsigned long long l_lr[2 * kLdsB * kMaxBatch];
+    const int tid = threadIdx.x;
+    const Batch& B = *bt;
+    if (B.stop) return;
+    const int k = B.k;
+    for (unsigned q = tid; q < 2 * kLdsB * (unsigned)k; q += blockDim.x) l_lr[q] = 0;
+    unsigned long long* LRt = LRbase + (size_t)(B.trip & 1) * lr_parity;   // member j at + j * lr_member
+
+    if (blockIdx.x == 0) {   // pop the members, cover and register their new tokens
+        if (tid < k) {
+            const BatchMember& M = B.m[tid];
+            P.cnt[M.slot] = 0;                       // byte_pair_frequencies.pop(best_pair)
+            atomicAnd(&P.flag[M.slot], ~kPresent);
+            X.beg[M.nw] = M.cov_beg;
+            X.len[M.nw] = M.cov_len;
+            if (M.isnew) {
+                K.off[M.nw] = M.pool_off; K.len[M.nw] = M.ln;
+                K.hash[M.nw] = M.hash; K.pw[M.nw] = M.pw; K.key8[M.nw] = M.k8;
+            }
+        }
+        for (int j = 0; j < k; ++j) {
+            const BatchMember& M = B.m[j];
+            if (!M.isnew || M.pool_off + M.ln > st->pool_cap) continue;
+            const unsigned la = K.len[M.a];
+            for (unsigned i = tid; i < M.ln; i += blockDim.x) K.pool[M.pool_off + i] = concat_byte(K, M.a, la, M.b, i);
+        }
+        if (tid == 0)
+            for (int j = 0; j < k; ++j)
+                if (B.m[j].isnew && B.m[j].pool_off + B.m[j].ln > st->pool_cap) atomicOr(&st->err, ERR_POOL);
+    }
+    __syncthreads();   // l_lr cleared
+
+    unsigned singles = 0;
+    const unsigned bid = blockIdx.x;
+    if (k == 1) {
+        // one member: the per-round rewrite (index list or a scan of every slot)
+        const BatchMember& M = B.m[0];
+        const TokT ta = (TokT)M.a, tb = (TokT)M.b, tn = (TokT)M.nw;
+        const DeltaSinkN<kLdsB> D{LRt, l_lr};
+        if (M.use_list && bid < W.lblk0) {
+            const uint32_t* L = X.list + M.list_beg;
+            for (unsigned i = bid * blockDim.x + tid; i < M.list_len; i += W.lblk0 * blockDim.x) {
+                const unsigned f = L[i];
+                if (f < W.off[1]) merge_one<TokT, 0>(W.c[0], f, ta, tb, tn, D, singles);
+                else if (f < W.off[2]) merge_one<TokT, 1>(W.c[1], f - W.off[1], ta, tb, tn, D, singles);
+                else if (f < W.off[3]) merge_one<TokT, 2>(W.c[2], f - W.off[2], ta, tb, tn, D, singles);
+                else merge_one<TokT, 3>(W.c[3], f - W.off[3], ta, tb, tn, D, singles);
+            }
+        } else if (!M.use_list) {
+            if (bid < W.c[1].blk0) {
+                if (bid < W.c[0].blk0 + W.c[0].nblk)
+                    scan_class<TokT, 0>(W.c[0], bid - W.c[0].blk0, ta, tb, tn, D, singles);
+            } else if (bid < W.c[2].blk0) {
+                scan_class<TokT, 1>(W.c[1], bid - W.c[1].blk0, ta, tb, tn, D, singles);
+            } else if (bid < W.c[3].blk0) {
+                scan_class<TokT, 2>(W.c[2], bid - W.c[2].blk0, ta, tb, tn, D, singles);
+            } else if (bid < W.lblk0) {
+                scan_class<TokT, 3>(W.c[3], bid - W.c[3].blk0, ta, tb, tn, D, singles);
+            }
+        }
+    } else if (bid < W.lblk0) {
+        // several members: every word that can contain one of them, once, all members in order
+        if (B.full_scan) {
+            const unsigned total = W.off[kNumCls];
+            for (unsigned f = bid * blockDim.x + tid; f < total; f += W.lblk0 * blockDim.x) {
+                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f, B, LRt, lr_member, l_lr, singles);
+                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1], B, LRt, lr_member, l_lr, singles);
+                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2], B, LRt, lr_member, l_lr, singles);
+                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3], B, LRt, lr_member, l_lr, singles);
+            }
+        } else {
+            const unsigned total = B.list_pre[k];
+            for (unsigned i = bid * blockDim.x + tid; i < total; i += W.lblk0 * blockDim.x) {
+                int j = 0;
+                while (j + 1 < k && i >= B.list_pre[j + 1]) ++j;
+                const unsigned f = X.list[B.m[j].list_beg + (i - B.list_pre[j])];
+                // a word on several members' lists is rewritten by the first thread to claim it
+                if (atomicMax(&tags[f], B.batch_id) >= B.batch_id) continue;
+                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f, B, LRt, lr_member, l_lr, singles);
+                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1], B, LRt, lr_member, l_lr, singles);
+                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2], B, LRt, lr_member, l_lr, singles);
+                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3], B, LRt, lr_member, l_lr, singles);
+            }
+        }
+    }
+    if (bid >= W.lblk0 && bid < W.lblk0 + W.lnblk) {   // long words: every member in order
+        for (unsigned i = (bid - W.lblk0) * blockDim.x + tid; i < W.ln; i += W.lnblk * blockDim.x) {
+            uint32_t len = W.llen[i];
+            if (len < 2) continue;
+            TokT* t = W.ltok + W.lbeg[i];
+            for (int j = 0; j < k && len >= 2; ++j) {
+                const TokT ta = (TokT)B.m[j].a, tb = (TokT)B.m[j].b;
+                bool hit = false;
+                for (uint32_t q = 0; q + 1 < len && !hit; ++q) hit = (t[q] == ta) & (t[q + 1] == tb);
+                if (!hit) continue;
+                const DeltaSinkN<kLdsB> D{LRt + (size_t)j * lr_member, l_lr + 2 * kLdsB * j};
+                len = rewrite_word(t, len, ta, tb, (TokT)B.m[j].nw, W.lcnt[i], D, false);
+                W.llen[i] = len;
+                singles += (len < 2);
+            }
+        }
+    }
+    singles = wave_sum(singles);   // words that became one token (rare: no contention)
+    if ((tid & 63) == 0 && singles) atomicAdd(&st->n_single, singles);
+    __syncthreads();
+    for (unsigned q = tid; q < 2 * kLdsB * (unsigned)k; q += blockDim.x) {
+        const unsigned long long v = l_lr[q];
+        if (v) atomicAdd(&LRt[(size_t)(q / (2 * kLdsB)) * lr_member + q % (2 * kLdsB)], v);
+    }
+}
+
+// Apply the trip's deltas and list the next trip's candidates.  Items:
+//   v < k * 4 * ntb        member j = v / (4 ntb), token x, op as in k_apply_argmax; its key has
+//                          ONE updater unless x is one of the batch's tokens S = {a_j, b_j, new_j};
+//   next |S|^2 items       every key with both tokens in S: one item sums all the members'
+//                          contributions to it;
+//   next nC_base items     C entries: untouched ones keep their counts during the apply, touched
+//                          ones are evaluated by their updater (final count).
+// Every present key >= T among them is a candidate; each workgroup writes its exact top-kTopM
+// (sorted) to part[blockIdx.x * kTopM ...] and k_select merges the lists.  scan_only: the C
+// entries alone (after a rebuild of C).
+constexpr unsigned kBatchApplyItems = 4;
+constexpr unsigned kApplyBatchThreads = 256;
+__global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* __restrict__ st,
+                                                                    BatchState* __restrict__ bs,
+                                                                    const Batch* __restrict__ bt, PairsDev P, ToksDev K,
+                                                                    unsigned long long* __restrict__ LRbase,
+                                                                    size_t lr_member, size_t lr_parity, unsigned ntb,
+                                                                    Partial* __restrict__ part, int scan_only) {
+    __shared__ unsigned s_tok[3 * kMaxBatch];
+    __shared__ int s_ns;
+    __shared__ Cand s_wave[kApplyBatchThreads / 64][kTopM];
+    __shared__ Cand s_out[kTopM];
+    const Batch& B = *bt;
+    if (!scan_only && B.stop) return;   // halted: part[] keeps the lists the next select reads
+    const int k = scan_only ? 0 : B.k;
+    const int tid = threadIdx.x;
+    if (tid == 0) {   // S, deduplicated (a == b is possible only when k == 1)
+        int ns = 0;
+        for (int j = 0; j < k; ++j) {
+            const unsigned t3[3] = {B.m[j].a, B.m[j].b, B.m[j].nw};
+            for (int q = 0; q < 3; ++q) {
+                bool dup = false;
+                for (int u = 0; u < ns; ++u) dup |= s_tok[u] == t3[q];
+                if (!dup) s_tok[ns++] = t3[q];
+            }
+        }
+        s_ns = ns;
+    }
+    __syncthreads();
+    const int ns = s_ns;
+    const long long T = st->T;
+    const unsigned long long* LRc = LRbase + (size_t)(B.trip & 1) * lr_parity;
+    unsigned long long* LRo = LRbase + (size_t)((B.trip + 1) & 1) * lr_parity;
+    if (!scan_only) ntb = min(ntb, (unsigned)B.ntok + B.n_fresh);   // token ids after this trip
+    const unsigned per_member = 4 * ntb;
+    const unsigned n_cell = (unsigned)k * per_member;
+    const unsigned n_sp = (unsigned)(ns * ns);
+    const unsigned nC0 = scan_only ? st->nC : B.nC_base;
+    const unsigned n_items = n_cell + n_sp + nC0;
+    const unsigned g = blockIdx.x * blockDim.x + tid;
+    const unsigned S = gridDim.x * blockDim.x;
+    if (!scan_only) {   // clear the previous trip's cells (its prev_k members; ids below this trip's start)
+        const unsigned nprev = 2 * (unsigned)B.ntok;
+        for (unsigned q = g; q < (unsigned)B.prev_k * nprev; q += S)
+            LRo[(size_t)(q / nprev) * lr_member + q % nprev] = 0;
+    }
+    auto in_S = [&](unsigned x) {
+        bool r = false;
+        for (int u = 0; u < ns; ++u) r |= s_tok[u] == x;
+        return r;
+    };
+    Cand mine = cand_none();   // this wave's top-kTopM, distributed over its lanes
+    Cand cand = cand_none();   // this lane's candidate of the current item
+    // an updated key: a candidate if present and >= T; an increment across T admits it to C
+    auto consider = [&](size_t s, unsigned p, unsigned q, long long c, unsigned f, bool inc) -> bool {
+        if (s == ~(size_t)0 || !(f & kPresent) || c < T) return false;
+        cand = Cand{c, K.key8[p], K.key8[q], (unsigned)s, p, q};
+        if (!inc || (f & kInC)) return false;
+        P.flag[s] = f | kInC;
+        return true;
+    };
+    for (unsigned base = (blockIdx.x * blockDim.x + (tid & ~63u)) * kBatchApplyItems; base < n_items;
+         base += S * kBatchApplyItems) {
+        for (unsigned u = 0; u < kBatchApplyItems; ++u) {
+            const unsigned v = base + u * 64 + (tid & 63);
+            bool add = false;
+            uint4 add_e = make_uint4(0, 0, 0, 0);
+            cand = cand_none();
+            if (v < n_cell) {
+                const unsigned j = v / per_member, r = v % per_member, x = r >> 2, op = r & 3;
+                const BatchMember& M = B.m[j];
+                const long long d = (long long)LRc[(size_t)j * lr_member + 2 * (size_t)x + (op >> 1)];
+                if (d && !in_S(x)) {
+                    const unsigned p = op <= 1 ? x : (op == 2 ? M.b : M.nw);
+                    const unsigned q = op == 0 ? M.a : (op == 1 ? M.nw : x);
+                    const bool inc = op & 1;
+                    long long c;
+                    unsigned f;
+                    const size_t s = pair_update(P, st, p, q, inc ? d : -d, inc, &c, &f);
+                    if (consider(s, p, q, c, f, inc)) { add = true; add_e = make_uint4((unsigned)s, p, q, 0u); }
+                }
+            } else if (v < n_cell + n_sp) {
+                const unsigned sp = v - n_cell;
+                const unsigned p = s_tok[sp / ns], q = s_tok[sp % ns];
+                bool popped = false;
+                long long inc = 0, dec = 0;
+                for (int j = 0; j < k; ++j) {
+                    const BatchMember& M = B.m[j];
+                    popped |= p == M.a && q == M.b;
+                    const unsigned long long* L = LRc + (size_t)j * lr_member;
+                    if (q == M.a) dec += (long long)L[2 * (size_t)p];
+                    if (q == M.nw) inc += (long long)L[2 * (size_t)p];
+                    if (p == M.b) dec += (long long)L[2 * (size_t)q + 1];
+                    if (p == M.nw) inc += (long long)L[2 * (size_t)q + 1];
+                }
+                if (!popped && (inc || dec)) {
+                    long long c;
+                    unsigned f;
+                    const size_t s = pair_update(P, st, p, q, inc - dec, inc != 0, &c, &f);
+                    if (consider(s, p, q, c, f, inc != 0)) { add = true; add_e = make_uint4((unsigned)s, p, q, 0u); }
+                }
+            } else if (v < n_items) {
+                const uint4 e = P.C[v - n_cell - n_sp];
+                const unsigned p = e.y, q = e.z;
+                const unsigned f = P.flag[e.x];
+                const long long c = P.cnt[e.x];
+                bool touched = false;
+                if (in_S(p) || in_S(q)) {   // does an item of this trip update the key?
+                    for (int j = 0; j < k && !touched; ++j) {
+                        const BatchMember& M = B.m[j];
+                        const unsigned long long* L = LRc + (size_t)j * lr_member;
+                        if ((q == M.a || q == M.nw) && L[2 * (size_t)p] != 0) touched = true;
+                        if ((p == M.b || p == M.nw) && L[2 * (size_t)q + 1] != 0) touched = true;
+                    }
+                }
+                if (!touched && (f & kPresent) && c >= T) cand = Cand{c, K.key8[p], K.key8[q], e.x, p, q};
+            }
+            wave_top_offer<kTopM>(mine, cand.cnt != LLONG_MIN, cand, K);
+            const unsigned idx = wave_append(add, &st->nC);
+            if (add) {
+                if (idx < st->capC) P.C[idx] = add_e;
+                else atomicOr(&st->err, ERR_C_FULL);
+            }
+        }
+    }
+    block_top<kTopM, kApplyBatchThreads / 64>(mine, s_wave, s_out, K);
+    if (tid < kTopM) {
+        const Cand c = s_out[tid];
+        part[blockIdx.x * kTopM + tid] = Partial{c.cnt, c.ka, c.kb, c.slot, c.a, c.b, 0};
+    }
+    if (blockIdx.x == 0 && tid == 0) {
+        st->nparts = gridDim.x;
+        if (!scan_only) {   // finish the trip: k rounds done
+            st->round = B.round + k;
+            st->ntok = B.ntok + (int)B.n_fresh;
+            bs->trip = B.trip + 1;
+            bs->prev_k = k;
+        }
     }
 }
 
@@ -1116,6 +1729,7 @@ class MergeLoop {
 
    private:
     static constexpr int kBatch = 64;
+    static constexpr int kTrips = 64;   // batched mode: [k_select][k_merge_batch][k_apply_batch] per host sync
     static constexpr int kArgBlocks = 64;
     static constexpr unsigned kCScanBlocks = 64;   // k_apply_argmax workgroups scanning C
     unsigned nparts_ = 0;                          // argmax partials the next k_merge reduces
@@ -1178,6 +1792,20 @@ class MergeLoop {
     DevBuf<unsigned long long> LR_;
     DevBuf<Partial> part_;
     DevBuf<uint32_t> m_a_, m_b_, m_new_, m_mode_;
+    // batched rounds (single rank): several exact merges per trip (k_select)
+    bool batched_ = false;
+    int max_batch_ = kMaxBatch;
+    long long trips_launched_ = 0, trips_run_ = 0;
+    DevBuf<BatchState> bs_;
+    DevBuf<Batch> batch_;
+    DevBuf<uint32_t> tags_;      // per slot word: the last batch that claimed it
+    DevBuf<int> trip_info_;      // per trip of a host batch: first round, members
+    DevBuf<Partial> lists_;      // per apply workgroup: its top-kTopM candidates
+    static constexpr unsigned kApplyBatchBlocks = 256;
+    void reset_tags();
+    void run_trips(bool timing, std::vector<hipEvent_t>& ev, double& k1_ms, double& k1_bytes,
+                   long long& k1_launches);
+    DevBuf<long long> m_cnt_;   // BPE355_ROUND_LOG: each round's winning count (else unallocated)
     DevBuf<RebuildStats> rs_;
     // posting index
     DevBuf<uint32_t> ilist_, ibeg_, ilen_;
@@ -1459,7 +2087,12 @@ int MergeLoop<TokT>::rebuild() {
     hs_.halt = HALT_NONE;
     push_state();
     hipLaunchKernelGGL(k_build_C, dim3(grid), dim3(256), 0, s_, pairs(), pcap_, T, st_.p);
-    hipLaunchKernelGGL(k_argmax, dim3(kArgBlocks), dim3(256), 0, s_, st_.p, pairs(), toks(), part_.p);
+    if (batched_)   // the candidates of the rebuilt C as the apply workgroups' top-M lists
+        hipLaunchKernelGGL(k_apply_batch, dim3(kApplyBatchBlocks), dim3(kApplyBatchThreads), 0, s_, st_.p, bs_.p,
+                           (const Batch*)batch_.p, pairs(), toks(), LR_.p, 2ull * tok_cap_,
+                           (size_t)kMaxBatch * 2ull * tok_cap_, tok_cap_, lists_.p, 1);
+    else
+        hipLaunchKernelGGL(k_argmax, dim3(kArgBlocks), dim3(256), 0, s_, st_.p, pairs(), toks(), part_.p);
     nparts_ = kArgBlocks;
     BPE_HIP(hipGetLastError());
     pull_state();
@@ -1477,9 +2110,27 @@ void MergeLoop<TokT>::run() {
     rs_.alloc(1);
     tok_cap_ = 256u + (unsigned)n_rounds_ + 1u;
     part_.alloc(std::max<size_t>(kArgBlocks, ceil_div(4ull * tok_cap_, 256) + kCScanBlocks));
-    LR_.alloc(2 * 2ull * tok_cap_);   // two cell buffers, by round parity
+    // single rank: batched rounds (BPE355_BATCH = members per trip, 1..8; 0 = the per-round
+    // kernels); sharded per-round exchange: the per-round kernels
+    {
+        const char* e = std::getenv("BPE355_BATCH");
+        max_batch_ = e ? std::min(std::atoi(e), kMaxBatch) : kMaxBatch;
+        batched_ = !sharded() && max_batch_ >= 1;
+    }
+    // cells: two buffers by round (trip) parity; batched: kMaxBatch members each
+    LR_.alloc(2 * (batched_ ? (size_t)kMaxBatch : 1) * 2ull * tok_cap_);
     BPE_HIP(hipMemsetAsync(LR_.p, 0, LR_.bytes(), s_));
+    if (batched_) {
+        bs_.alloc(1);
+        BPE_HIP(hipMemsetAsync(bs_.p, 0, sizeof(BatchState), s_));
+        batch_.alloc(1);
+        BPE_HIP(hipMemsetAsync(batch_.p, 0, sizeof(Batch), s_));
+        trip_info_.alloc(2 * kTrips);
+        lists_.alloc((size_t)kApplyBatchBlocks * kTopM);
+    }
     m_a_.alloc(n_rounds_); m_b_.alloc(n_rounds_); m_new_.alloc(n_rounds_); m_mode_.alloc(n_rounds_);
+    const char* round_log = std::getenv("BPE355_ROUND_LOG");   // analysis knob: per-round records
+    if (round_log) m_cnt_.alloc(n_rounds_);
     toff_.alloc(tok_cap_); tlen_.alloc(tok_cap_);
     thash_.alloc(tok_cap_); tpw_.alloc(tok_cap_); tkey8_.alloc(tok_cap_);
     tmap_.alloc(next_pow2(4ull * tok_cap_));
@@ -1516,7 +2167,10 @@ void MergeLoop<TokT>::run() {
     BPE_HIP(hipGetLastError());
     pull_state();
     build_index();
+    if (batched_) reset_tags();
     hs_.halt = HALT_REBUILD;
+    hs_.max_len = std::max(max_len_, 1u);
+    hs_.max_batch = max_batch_;
 
     const bool timing = timing_enabled();
     std::vector<hipEvent_t> ev;
@@ -1540,6 +2194,34 @@ void MergeLoop<TokT>::run() {
             const int r = rebuild();
             if (r == 1) { exhaustion(); break; }
             if (r == 2) break;   // no keys left: `if len(byte_pair_frequencies) == 0: break`
+        }
+        if (batched_) {
+            // k_select checks the pair table, the token pool and the compaction schedule before
+            // every trip and hands back to the host (HALT_HOST); here the host makes room
+            if (hs_.pair_used + 4ull * (hs_.ntok + kMaxBatch) * kMaxBatch > pcap_ / 2) {
+                grow_pairs();
+                hs_.halt = HALT_REBUILD;   // C holds slot indices: rebuild it
+                continue;
+            }
+            ensure_pool((unsigned)(4 * kMaxBatch) * std::max(max_len_, 1u));
+            if (hs_.halt == HALT_HOST) hs_.halt = HALT_NONE;
+            hs_.host_round = next_index_round_;
+            hs_.single_limit = n_live_ / 4 + 1024;
+            hs_.pair_limit = pcap_ / 2;
+            push_state();
+            run_trips(timing, ev, k1_ms, k1_bytes, k1_launches);
+            BPE_REQUIRE(!(hs_.err & ERR_PAIRS_FULL), BPE_E_NOMEM, "pair table overflow");
+            BPE_REQUIRE(!(hs_.err & ERR_C_FULL), BPE_E_NOMEM, "candidate list overflow");
+            BPE_REQUIRE(!(hs_.err & ERR_POOL), BPE_E_NOMEM, "token pool overflow");
+            if (hs_.halt == HALT_DONE) break;
+            if (hs_.n_single > n_live_ / 4 + 1024 || hs_.round >= next_index_round_) {
+                compact();
+                build_index();
+                reset_tags();
+                push_state();
+                next_index_round_ = std::max(hs_.round + 512, (int)(hs_.round * 2.5));
+            }
+            continue;
         }
         // capacity headroom for one batch (worst case: 2 new keys per token per round)
         int R = std::min(kBatch, n_rounds_ - hs_.round);
@@ -1569,7 +2251,7 @@ void MergeLoop<TokT>::run() {
             hipExtLaunchKernelGGL(k_merge<TokT>, dim3(merge_grid_), dim3(256), 0, s_,
                                   timed ? ev[2 * k] : nullptr, timed ? ev[2 * k + 1] : nullptr, 0,
                                   st_.p, (const Partial*)part_.p, (int)nparts_, pairs(), toks(),
-                                  wdev_, idev_, LRc, m_a_.p, m_b_.p, m_new_.p, m_mode_.p);
+                                  wdev_, idev_, LRc, m_a_.p, m_b_.p, m_new_.p, m_mode_.p, m_cnt_.p);
             if (sharded) {   // the one collective per merge round
                 const size_t ntok_bound = 256 + (size_t)rnd + 1;
                 comm_->allreduce_i64(reinterpret_cast<int64_t*>(LRc), 2 * ntok_bound, s_);
@@ -1617,6 +2299,29 @@ void MergeLoop<TokT>::run() {
         }
     }
     for (auto& e : ev) (void)hipEventDestroy(e);
+    if (round_log && hs_.round) {   // a, b, new, list length (~0: full scan), count per round
+        const int rd = hs_.round;
+        std::vector<uint32_t> va(rd), vb(rd), vn(rd), vm(rd);
+        std::vector<long long> vc(rd);
+        BPE_HIP(hipMemcpy(va.data(), m_a_.p, rd * 4ull, hipMemcpyDeviceToHost));
+        BPE_HIP(hipMemcpy(vb.data(), m_b_.p, rd * 4ull, hipMemcpyDeviceToHost));
+        BPE_HIP(hipMemcpy(vn.data(), m_new_.p, rd * 4ull, hipMemcpyDeviceToHost));
+        BPE_HIP(hipMemcpy(vm.data(), m_mode_.p, rd * 4ull, hipMemcpyDeviceToHost));
+        BPE_HIP(hipMemcpy(vc.data(), m_cnt_.p, rd * 8ull, hipMemcpyDeviceToHost));
+        if (FILE* f = std::fopen(round_log, "wb")) {
+            for (int r = 0; r < rd; ++r) {
+                std::fwrite(&va[r], 4, 1, f); std::fwrite(&vb[r], 4, 1, f); std::fwrite(&vn[r], 4, 1, f);
+                std::fwrite(&vm[r], 4, 1, f); std::fwrite(&vc[r], 8, 1, f);
+            }
+            std::fclose(f);
+        }
+    }
+    if (batched_) {
+        BatchState b{};
+        BPE_HIP(hipMemcpy(&b, bs_.p, sizeof(b), hipMemcpyDeviceToHost));
+        out_.stats.n_trips = trips_run_;
+        out_.stats.n_rounds_batched = (int64_t)b.rounds_batched;
+    }
     out_.stats.merge_kernel_ms = k1_ms;
     out_.stats.merge_kernel_launches = k1_launches;
     out_.stats.merge_kernel_bytes = k1_bytes;
@@ -1646,6 +2351,63 @@ void MergeLoop<TokT>::run() {
         out_.merges.emplace_back(tb[ma[r]], tb[mb[r]]);
     }
     for (auto& m : tail) out_.merges.push_back(std::move(m));
+}
+
+template <class TokT>
+void MergeLoop<TokT>::reset_tags() {
+    tags_.alloc(std::max(idev_.n_slot_words, 1u));
+    BPE_HIP(hipMemsetAsync(tags_.p, 0, tags_.bytes(), s_));
+}
+
+// kTrips x [k_select][k_merge_batch][k_apply_batch], then one host sync.  A trip after a halt
+// finds nothing to do.  With timing on, k_merge_batch is event-timed on one trip in
+// kTimingStride (events stamped by its own dispatch packet).
+template <class TokT>
+void MergeLoop<TokT>::run_trips(bool timing, std::vector<hipEvent_t>& ev, double& k1_ms, double& k1_bytes,
+                                long long& k1_launches) {
+    const size_t lr_member = 2ull * tok_cap_, lr_parity = (size_t)kMaxBatch * lr_member;
+    const unsigned ntb = tok_cap_;
+    const unsigned apply_blocks = kApplyBatchBlocks;
+    for (int t = 0; t < kTrips; ++t) {
+        const bool timed = timing && (trips_launched_ + t) % kTimingStride == 0;
+        hipLaunchKernelGGL(k_select, dim3(1), dim3(kSelThreads), 0, s_, st_.p, bs_.p, pairs(), toks(), idev_,
+                           batch_.p, (const Partial*)lists_.p, m_a_.p, m_b_.p, m_new_.p, m_mode_.p, m_cnt_.p,
+                           trip_info_.p, t);
+        hipExtLaunchKernelGGL(k_merge_batch<TokT>, dim3(merge_grid_), dim3(256), 0, s_,
+                              timed ? ev[2 * t] : nullptr, timed ? ev[2 * t + 1] : nullptr, 0,
+                              st_.p, (const Batch*)batch_.p, pairs(), toks(), wdev_, idev_, LR_.p, lr_member,
+                              lr_parity, tags_.p);
+        hipLaunchKernelGGL(k_apply_batch, dim3(apply_blocks), dim3(kApplyBatchThreads), 0, s_, st_.p, bs_.p,
+                           (const Batch*)batch_.p, pairs(), toks(), LR_.p, lr_member, lr_parity, ntb, lists_.p, 0);
+    }
+    BPE_HIP(hipGetLastError());
+    pull_state();
+    std::vector<int> ti(2 * kTrips);
+    BPE_HIP(hipMemcpy(ti.data(), trip_info_.p, ti.size() * 4, hipMemcpyDeviceToHost));
+    for (int t = 0; t < kTrips; ++t) trips_run_ += ti[2 * t + 1] > 0;
+    if (timing) {
+        const double slot_avg = scan_bytes_ / std::max(1u, idev_.n_slot_words + words_.ln);
+        for (int t = 0; t < kTrips; ++t) {
+            if ((trips_launched_ + t) % kTimingStride || ti[2 * t + 1] <= 0) continue;
+            float ms = 0;
+            BPE_HIP(hipEventElapsedTime(&ms, ev[2 * t], ev[2 * t + 1]));
+            const int r0 = ti[2 * t], k = ti[2 * t + 1];
+            std::vector<uint32_t> mode(k);
+            BPE_HIP(hipMemcpy(mode.data(), m_mode_.p + r0, k * 4ull, hipMemcpyDeviceToHost));
+            // algorithmic bytes: every slot on a full scan, else the members' list entries and
+            // their slots (at the table's mean slot size); every long word once per trip
+            bool full = false;
+            double b = long_bytes_;
+            for (uint32_t m : mode) {
+                if (m == 0xffffffffu) full = true;
+                else b += m * (4.0 + slot_avg);
+            }
+            k1_ms += ms;
+            k1_bytes += full ? scan_bytes_ : b;
+            ++k1_launches;
+        }
+    }
+    trips_launched_ += kTrips;
 }
 
 // Every word is one token: the reference keeps popping the remaining zero-count keys,
