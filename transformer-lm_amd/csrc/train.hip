@@ -79,6 +79,7 @@ struct RoundState {
     unsigned long long scan_slots;
     int nparts;                 // batched: apply workgroups whose top-M lists part[] holds
     int pad1;
+    unsigned long long* probe;  // BPE355_PROBE: phase stamps of sampled trips (else null)
     // batched rounds (k_select): the host's limits, checked before every trip
     int host_round;             // hand back to the host at this round (compaction schedule)
     unsigned single_limit;      // ... or when this many words became one token (compaction)
@@ -820,7 +821,12 @@ struct BatchState {
     int prev_k;              // members of the last trip (its cells are cleared by the next apply)
     unsigned long long rounds_batched;   // statistics: rounds taken in batches of k > 1
     unsigned long long trips_batched;
+    long long T2;            // candidate-list threshold (>= T): every present key >= T2 is listed
+    unsigned list_n;         // keys the apply appended to the list (> kListCap: overflow)
+    unsigned pad;
+    unsigned long long n_overflow, n_headmiss, n_short, k_hist[kMaxBatch + 1];   // diagnostics
 };
+constexpr unsigned kListCap = 64;   // the candidate list k_select sorts (one wave)
 
 struct TokMetaS {
     unsigned long long ha, pb, hb, pa;   // hash(a), P^len(b), hash(b), P^len(a)
@@ -836,6 +842,29 @@ struct DeltaSinkN {
         else atomicAdd(&LR[cell], c);
     }
 };
+
+// BPE355_PROBE: 100 MHz stamps of one trip in kProbeTrip, 16 per sampled trip (MergeLoop::report_probe)
+constexpr int kProbeTrip = 8;
+__device__ __forceinline__ void probe_stamp(const RoundState* st, int trip, int k) {
+    if (st->probe && (trip % kProbeTrip) == 0) st->probe[16 * (size_t)(trip / kProbeTrip) + k] = __builtin_amdgcn_s_memrealtime();
+}
+
+__device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int j) {
+    const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)v, j);
+    const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(v >> 32), j);
+    return ((unsigned long long)hi << 32) | lo;
+}
+// lane j's candidate, in every lane (scalar broadcast)
+__device__ __forceinline__ Cand readlane_cand(const Cand& c, int j) {
+    Cand r;
+    r.cnt = (long long)readlane64((unsigned long long)c.cnt, j);
+    r.ka = readlane64(c.ka, j);
+    r.kb = readlane64(c.kb, j);
+    r.slot = __builtin_amdgcn_readlane((int)c.slot, j);
+    r.a = __builtin_amdgcn_readlane((int)c.a, j);
+    r.b = __builtin_amdgcn_readlane((int)c.b, j);
+    return r;
+}
 
 // A wave's sorted top-M candidates, distributed: lane i < M holds the i-th best (cand_none
 // padding), so no lane keeps an array.
@@ -868,28 +897,39 @@ __device__ __forceinline__ void wave_top_offer(Cand& mine, bool has, const Cand&
         }
     }
 }
-// a workgroup's top-M from its waves' lists (every thread calls; out[0..M) valid after return)
+// a workgroup's top-M from its waves' lists (every thread calls; out[0..M) valid after return):
+// the NW * M entries go to LDS, then wave 0 extracts the best M (each lane scans its share)
 template <int M, int NW>
 __device__ __forceinline__ void block_top(const Cand& mine, Cand (*s_wave)[M], Cand* out, const ToksDev& K) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (lane < M) s_wave[wv][lane] = mine;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int head[NW];
-#pragma unroll
-        for (int w = 0; w < NW; ++w) head[w] = 0;
+    if (wv == 0) {
+        constexpr int E = NW * M, PER = (E + 63) / 64;
+        Cand* flat = &s_wave[0][0];
+        unsigned taken = 0;   // bit i: this lane's entry i was extracted
         for (int t = 0; t < M; ++t) {
-            int bw = -1;
-            Cand bc = cand_none();
+            Cand best = cand_none();
+            int bi = -1;
 #pragma unroll
-            for (int w = 0; w < NW; ++w) {
-                if (head[w] >= M) continue;
-                const Cand x = s_wave[w][head[w]];
-                if (x.cnt != LLONG_MIN && (bw < 0 || cand_better(x, bc, K.pool, K.off, K.len))) { bw = w; bc = x; }
+            for (int i = 0; i < PER; ++i) {
+                const int e = lane + 64 * i;
+                if (e >= E || ((taken >> i) & 1)) continue;
+                const Cand x = flat[e];
+                if (x.cnt != LLONG_MIN && (bi < 0 || cand_better(x, best, K.pool, K.off, K.len))) { best = x; bi = i; }
             }
-            out[t] = bc;
-#pragma unroll
-            for (int w = 0; w < NW; ++w) head[w] += (w == bw);
+            int from = lane;
+            for (int o = 32; o > 0; o >>= 1) {
+                const Cand oc = shfl_xor_cand(best, o);
+                const int of = __shfl_xor(from, o);
+                if (cand_better(oc, best, K.pool, K.off, K.len) ||
+                    (!cand_better(best, oc, K.pool, K.off, K.len) && of < from)) {
+                    best = oc;
+                    from = of;
+                }
+            }
+            if (lane == from && bi >= 0) taken |= 1u << bi;
+            if (lane == 0) out[t] = best;
         }
     }
     __syncthreads();
@@ -902,16 +942,27 @@ constexpr int kSelThreads = 512;
 __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__ st, BatchState* __restrict__ bs,
                                                         PairsDev P, ToksDev K, IndexDev X, Batch* __restrict__ bt,
                                                         const Partial* __restrict__ part,
+                                                        const Partial* __restrict__ list,
                                                         uint32_t* __restrict__ m_a, uint32_t* __restrict__ m_b,
                                                         uint32_t* __restrict__ m_new, uint32_t* __restrict__ m_mode,
                                                         long long* __restrict__ m_cnt, int* __restrict__ trip_info,
                                                         int trip_slot) {
     __shared__ Cand s_wave[kSelThreads / 64][kTopM];
-    __shared__ Cand s_fin[kTopM];
+    __shared__ Cand s_fin[kTopM], s_list[kTopM];
+    __shared__ long long s_rankcnt[kListCap];
     __shared__ int s_nfin, s_stop;
     __shared__ unsigned s_fresh[kTopM], s_nw_old[kTopM];
     __shared__ TokMetaS s_meta[kTopM];
+    __shared__ unsigned s_off[kMaxBatch], s_newid[kMaxBatch], s_pre[kMaxBatch + 1];
+    __shared__ int s_k, s_round, s_nrounds, s_trip, s_prevk;
+    __shared__ unsigned s_pool, s_bid;
     const int tid = threadIdx.x;
+    const int ptrip = bs->trip;
+    if (tid == 0) {   // scalars the rule needs, loaded together
+        s_round = st->round; s_nrounds = st->n_rounds; s_trip = bs->trip; s_prevk = bs->prev_k;
+        s_pool = st->pool_used; s_bid = bs->batch_seq + 1;
+    }
+    if (tid == 0) probe_stamp(st, ptrip, 0);
     // ---- the previous batch's tokens enter the dedupe map
     if (bs->pend_insert) {
         const int pk = bt->k;
@@ -923,6 +974,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         __syncthreads();
         if (tid == 0) bs->pend_insert = 0;
     }
+    if (tid == 0) probe_stamp(st, ptrip, 1);
     const int halt = st->halt;
     if (halt) {
         if (tid == 0) {
@@ -931,24 +983,59 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         }
         return;
     }
-    // ---- the top-M of the apply workgroups' top-M lists
+    // ---- the best candidate: the apply workgroups' partials (exact); the next ones: the
+    // candidate list, which holds every present key >= T2 (exact top-M among them)
     const unsigned nC = st->nC;
     const long long T = st->T;
-    const int nlists = st->nparts;
-    Cand mine = cand_none();
-    for (int base = tid & ~63; base < nlists * kTopM; base += kSelThreads) {
-        const int i = base + (tid & 63);
-        Cand c = cand_none();
-        if (i < nlists * kTopM) {
+    const int nparts = st->nparts;
+    {
+        Cand best = cand_none();
+        for (int i = tid; i < nparts; i += kSelThreads) {
             const Partial q = part[i];
-            c = Cand{q.cnt, q.ka, q.kb, q.slot, q.a, q.b};
+            const Cand c{q.cnt, q.ka, q.kb, q.slot, q.a, q.b};
+            if (cand_better(c, best, K.pool, K.off, K.len)) best = c;
         }
-        wave_top_offer<kTopM>(mine, c.cnt != LLONG_MIN, c, K);
+        for (int o = 32; o > 0; o >>= 1) {
+            const Cand oc = shfl_xor_cand(best, o);
+            if (cand_better(oc, best, K.pool, K.off, K.len)) best = oc;
+        }
+        if ((tid & 63) == 0) s_wave[tid >> 6][0] = best;
     }
-    block_top<kTopM, kSelThreads / 64>(mine, s_wave, s_fin, K);
+    const unsigned ln = bs->list_n;
+    if (tid < kTopM) s_list[tid] = cand_none();
+    __syncthreads();
+    if (tid < 64) {   // wave 0: each listed key's rank = the listed keys better than it
+        const bool usable = ln <= kListCap;
+        Cand x = cand_none();
+        if (usable && (unsigned)tid < ln) {
+            const Partial q = list[tid];
+            x = Cand{q.cnt, q.ka, q.kb, q.slot, q.a, q.b};
+        }
+        const int nl = usable ? (int)ln : 0;
+        int rank = 0;
+        for (int j = 0; j < nl; ++j) {
+            const Cand y = readlane_cand(x, j);
+            rank += cand_better(y, x, K.pool, K.off, K.len) ? 1 : 0;
+        }
+        if (x.cnt != LLONG_MIN && rank < kTopM) s_list[rank] = x;
+        if (x.cnt != LLONG_MIN) s_rankcnt[rank] = x.cnt;
+    }
+    __syncthreads();
+    if (tid == 0) probe_stamp(st, ptrip, 2);
     if (tid == 0) {
-        int nf = 0;
-        while (nf < kTopM && s_fin[nf].cnt != LLONG_MIN) ++nf;
+        Cand p1 = s_wave[0][0];
+        for (int w = 1; w < kSelThreads / 64; ++w)
+            if (cand_better(s_wave[w][0], p1, K.pool, K.off, K.len)) p1 = s_wave[w][0];
+        // the list's head is the global best whenever the best is >= T2 and nothing overflowed
+        int nf = 1;
+        s_fin[0] = p1;
+        const bool list_ok = ln <= kListCap && s_list[0].cnt != LLONG_MIN && s_list[0].slot == p1.slot &&
+                             s_list[0].a == p1.a && s_list[0].b == p1.b;
+        if (list_ok)
+            while (nf < kTopM && s_list[nf].cnt != LLONG_MIN) { s_fin[nf] = s_list[nf]; ++nf; }
+        if (ln > kListCap) bs->n_overflow++;
+        else if (!list_ok) bs->n_headmiss++;
+        else if (nf < kTopM) bs->n_short++;
         s_nfin = nf;
         const int round = st->round;
         int stop = HALT_NONE;
@@ -991,63 +1078,97 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         s_nw_old[tid] = old;
     }
     __syncthreads();
-    if (tid != 0) return;
-    // ---- the batch rule
-    const int maxb = min(st->max_batch, kMaxBatch);
-    int k = 1;
-    {
-        unsigned used[2 * kMaxBatch];
-        int nu = 0;
+    if (tid == 0) probe_stamp(st, ptrip, 3);
+    // ---- the batch rule (thread 0), then the record filled by one thread per member
+    if (tid == 0) {
+        const int maxb = min(st->max_batch, kMaxBatch);
+        int k = 1;
         const Cand& p0 = s_fin[0];
-        const bool first_ok = p0.a != p0.b && s_fresh[0];
-        used[nu++] = p0.a;
-        used[nu++] = p0.b;
-        while (first_ok && k < maxb && k < nf) {
-            const Cand& c = s_fin[k];
-            if (c.cnt < T || c.a == c.b || !s_fresh[k]) break;
-            bool clash = false;
-            for (int u = 0; u < nu; ++u) clash |= used[u] == c.a || used[u] == c.b;
-            if (clash) break;
-            // new bytes must differ from every earlier member's new bytes
-            const unsigned long long h = s_meta[k].ha * s_meta[k].pb + s_meta[k].hb;
-            for (int j = 0; j < k && !clash; ++j) {
-                const unsigned long long hj = s_meta[j].ha * s_meta[j].pb + s_meta[j].hb;
-                if (hj != h || s_meta[j].la + s_meta[j].lb != s_meta[k].la + s_meta[k].lb) continue;
+        if (p0.a != p0.b && s_fresh[0]) {
+            while (k < maxb && k < nf) {
+                const Cand& c = s_fin[k];
+                if (c.cnt < T || c.a == c.b || !s_fresh[k]) break;
+                bool clash = false;
+                for (int j = 0; j < k; ++j)
+                    clash |= s_fin[j].a == c.a || s_fin[j].a == c.b || s_fin[j].b == c.a || s_fin[j].b == c.b;
+                // new bytes must differ from every earlier member's new bytes
+                const unsigned long long h = s_meta[k].ha * s_meta[k].pb + s_meta[k].hb;
                 const unsigned ln = s_meta[k].la + s_meta[k].lb;
-                bool eq = true;
-                for (unsigned i = 0; i < ln && eq; ++i)
-                    eq = concat_byte(K, s_fin[j].a, s_meta[j].la, s_fin[j].b, i) ==
-                         concat_byte(K, c.a, s_meta[k].la, c.b, i);
-                clash = eq;
+                for (int j = 0; j < k && !clash; ++j) {
+                    if (s_meta[j].ha * s_meta[j].pb + s_meta[j].hb != h || s_meta[j].la + s_meta[j].lb != ln) continue;
+                    bool eq = true;
+                    for (unsigned i = 0; i < ln && eq; ++i)
+                        eq = concat_byte(K, s_fin[j].a, s_meta[j].la, s_fin[j].b, i) ==
+                             concat_byte(K, c.a, s_meta[k].la, c.b, i);
+                    clash = eq;
+                }
+                if (clash) break;
+                ++k;
             }
-            if (clash) break;
-            used[nu++] = c.a;
-            used[nu++] = c.b;
-            ++k;
+            // (4) strictly above the next candidate: listed (s_fin[k]), or unlisted (below T2,
+            // and every member is listed, so >= T2)
+            while (k > 1 && k < nf && !(s_fin[k - 1].cnt > s_fin[k].cnt)) --k;
         }
-        // (4) strictly above the next candidate (keys outside C are below T <= count(Pk))
-        while (k > 1 && k < nf && !(s_fin[k - 1].cnt > s_fin[k].cnt)) --k;
+        k = min(k, s_nrounds - s_round);
+        // per member: pool offset, new id, posting-list prefix
+        unsigned pool = s_pool, fresh = 0, pre = 0, full = 0;
+        for (int j = 0; j < k; ++j) {
+            const TokMetaS& m = s_meta[j];
+            const bool pick_a = m.za <= m.zb;
+            const unsigned lu = pick_a ? m.za : m.zb;
+            const bool use = lu != kNoAnc && lu <= X.full_threshold;
+            s_off[j] = pool;
+            s_newid[j] = s_fresh[j] ? (unsigned)ntok + fresh : s_nw_old[j];
+            s_pre[j] = pre;
+            if (s_fresh[j]) { pool += m.la + m.lb; ++fresh; }
+            pre += use ? lu : 0;
+            full |= !use;
+        }
+        s_pre[k] = pre;
+        s_k = k;
+        Batch& B = *bt;
+        B.stop = 0;
+        B.k = k;
+        B.round = s_round;
+        B.ntok = ntok;
+        B.trip = s_trip;
+        B.prev_k = s_prevk;
+        B.batch_id = s_bid;
+        B.nC_base = nC;
+        B.full_scan = full;
+        B.n_fresh = fresh;
+        for (int j = 0; j <= k; ++j) B.list_pre[j] = s_pre[j];
+        st->pool_used = pool;
+        bs->batch_seq = s_bid;
+        {   // the next list: about kListTarget keys.  With the list ranked, T2 = the count of the
+            // kListTarget-th best (this trip pops at most kMaxBatch of those above it); on overflow
+            // raise T2 halfway to the top; with too few keys, extend the range below the last one
+            constexpr unsigned kListTarget = 24;
+            const long long top = s_fin[0].cnt;
+            const long long t2 = bs->T2 < T ? T : bs->T2;
+            long long nt;
+            if (ln > kListCap) nt = t2 + (top - t2) / 2;
+            else if (ln >= kListTarget) nt = s_rankcnt[kListTarget - 1];
+            else if (ln > 0) nt = s_rankcnt[ln - 1] - (top - s_rankcnt[ln - 1]) - 1;
+            else nt = T;
+            bs->T2 = nt < T ? T : (nt > top ? top : nt);
+            bs->list_n = 0;   // the apply of this trip fills it again
+        }
+        bs->pend_insert = fresh != 0;
+        if (k > 1) { bs->rounds_batched += k; bs->trips_batched += 1; }
+        bs->k_hist[k]++;
+        if (trip_info) { trip_info[2 * trip_slot] = s_round; trip_info[2 * trip_slot + 1] = k; }
     }
-    const int round = st->round;
-    k = min(k, st->n_rounds - round);
-    // ---- the batch record
-    Batch& B = *bt;
-    B.stop = 0;
-    B.k = k;
-    B.round = round;
-    B.ntok = ntok;
-    B.trip = bs->trip;
-    B.prev_k = bs->prev_k;
-    B.batch_id = ++bs->batch_seq;
-    B.nC_base = nC;
-    unsigned pool = st->pool_used, fresh = 0, full = 0, pre = 0;
-    for (int j = 0; j < k; ++j) {
-        const Cand& c = s_fin[j];
-        const TokMetaS& m = s_meta[j];
-        BatchMember& M = B.m[j];
+    __syncthreads();
+    const int k = s_k;
+    if (tid < k) {
+        const int j = tid, round = s_round;
+        const Cand c = s_fin[j];
+        const TokMetaS m = s_meta[j];
+        BatchMember M;
         const bool isnew = s_fresh[j];
         M.a = c.a; M.b = c.b; M.slot = c.slot; M.cnt = c.cnt;
-        M.nw = isnew ? (unsigned)ntok + fresh : s_nw_old[j];
+        M.nw = s_newid[j];
         M.isnew = isnew;
         M.hash = m.ha * m.pb + m.hb;
         M.pw = m.pa * m.pb;
@@ -1060,22 +1181,13 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         M.list_len = M.use_list ? lu : 0;
         M.cov_beg = bu;
         M.cov_len = isnew ? lu : kNoAnc;   // dedupe: uncovered until the next index build
-        M.pool_off = pool;
-        if (isnew) { pool += M.ln; ++fresh; }
-        full |= !M.use_list;
-        B.list_pre[j] = pre;
-        pre += M.list_len;
+        M.pool_off = s_off[j];
+        bt->m[j] = M;
         m_a[round + j] = c.a; m_b[round + j] = c.b; m_new[round + j] = M.nw;
         m_mode[round + j] = M.use_list ? M.list_len : 0xffffffffu;
         if (m_cnt) m_cnt[round + j] = c.cnt;
     }
-    B.list_pre[k] = pre;
-    B.full_scan = full;
-    B.n_fresh = fresh;
-    st->pool_used = pool;
-    bs->pend_insert = fresh != 0;
-    if (k > 1) { bs->rounds_batched += k; bs->trips_batched += 1; }
-    if (trip_info) { trip_info[2 * trip_slot] = round; trip_info[2 * trip_slot + 1] = k; }
+    if (tid == 0) probe_stamp(st, ptrip, 4);
 }
 
 // the slot word of class C addressed directly, every member applied in order
@@ -1119,32 +1231,33 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
     const Batch& B = *bt;
     if (B.stop) return;
     const int k = B.k;
+    if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 5);
     for (unsigned q = tid; q < 2 * kLdsB * (unsigned)k; q += blockDim.x) l_lr[q] = 0;
     unsigned long long* LRt = LRbase + (size_t)(B.trip & 1) * lr_parity;   // member j at + j * lr_member
 
-    if (blockIdx.x == 0) {   // pop the members, cover and register their new tokens
-        if (tid < k) {
-            const BatchMember& M = B.m[tid];
+    if ((int)blockIdx.x < k) {   // block j pops member j, covers and registers its new token
+        const BatchMember& M = B.m[blockIdx.x];
+        if (tid == 0) {
             P.cnt[M.slot] = 0;                       // byte_pair_frequencies.pop(best_pair)
             atomicAnd(&P.flag[M.slot], ~kPresent);
             X.beg[M.nw] = M.cov_beg;
             X.len[M.nw] = M.cov_len;
-            if (M.isnew) {
+        }
+        if (M.isnew) {
+            if (M.pool_off + M.ln <= st->pool_cap) {
+                const unsigned la = K.len[M.a];
+                for (unsigned i = tid; i < M.ln; i += blockDim.x) K.pool[M.pool_off + i] = concat_byte(K, M.a, la, M.b, i);
+            } else if (tid == 0) {
+                atomicOr(&st->err, ERR_POOL);
+            }
+            if (tid == 0) {
                 K.off[M.nw] = M.pool_off; K.len[M.nw] = M.ln;
                 K.hash[M.nw] = M.hash; K.pw[M.nw] = M.pw; K.key8[M.nw] = M.k8;
             }
         }
-        for (int j = 0; j < k; ++j) {
-            const BatchMember& M = B.m[j];
-            if (!M.isnew || M.pool_off + M.ln > st->pool_cap) continue;
-            const unsigned la = K.len[M.a];
-            for (unsigned i = tid; i < M.ln; i += blockDim.x) K.pool[M.pool_off + i] = concat_byte(K, M.a, la, M.b, i);
-        }
-        if (tid == 0)
-            for (int j = 0; j < k; ++j)
-                if (B.m[j].isnew && B.m[j].pool_off + B.m[j].ln > st->pool_cap) atomicOr(&st->err, ERR_POOL);
     }
     __syncthreads();   // l_lr cleared
+    if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 6);
 
     unsigned singles = 0;
     const unsigned bid = blockIdx.x;
@@ -1219,10 +1332,12 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
     singles = wave_sum(singles);   // words that became one token (rare: no contention)
     if ((tid & 63) == 0 && singles) atomicAdd(&st->n_single, singles);
     __syncthreads();
+    if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 7);
     for (unsigned q = tid; q < 2 * kLdsB * (unsigned)k; q += blockDim.x) {
         const unsigned long long v = l_lr[q];
         if (v) atomicAdd(&LRt[(size_t)(q / (2 * kLdsB)) * lr_member + q % (2 * kLdsB)], v);
     }
+    if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 8);
 }
 
 // Apply the trip's deltas and list the next trip's candidates.  Items:
@@ -1242,15 +1357,17 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
                                                                     const Batch* __restrict__ bt, PairsDev P, ToksDev K,
                                                                     unsigned long long* __restrict__ LRbase,
                                                                     size_t lr_member, size_t lr_parity, unsigned ntb,
-                                                                    Partial* __restrict__ part, int scan_only) {
+                                                                    Partial* __restrict__ part,
+                                                                    Partial* __restrict__ list, int scan_only) {
     __shared__ unsigned s_tok[3 * kMaxBatch];
     __shared__ int s_ns;
-    __shared__ Cand s_wave[kApplyBatchThreads / 64][kTopM];
-    __shared__ Cand s_out[kTopM];
+    __shared__ Cand s_wave[kApplyBatchThreads / 64];
     const Batch& B = *bt;
     if (!scan_only && B.stop) return;   // halted: part[] keeps the lists the next select reads
     const int k = scan_only ? 0 : B.k;
     const int tid = threadIdx.x;
+    const bool pw0 = !scan_only && blockIdx.x == 0 && tid == 0;
+    if (pw0) probe_stamp(st, B.trip, 9);
     if (tid == 0) {   // S, deduplicated (a == b is possible only when k == 1)
         int ns = 0;
         for (int j = 0; j < k; ++j) {
@@ -1281,12 +1398,14 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
         for (unsigned q = g; q < (unsigned)B.prev_k * nprev; q += S)
             LRo[(size_t)(q / nprev) * lr_member + q % nprev] = 0;
     }
+    if (pw0) probe_stamp(st, B.trip, 10);
     auto in_S = [&](unsigned x) {
         bool r = false;
         for (int u = 0; u < ns; ++u) r |= s_tok[u] == x;
         return r;
     };
-    Cand mine = cand_none();   // this wave's top-kTopM, distributed over its lanes
+    const long long T2 = bs->T2 < T ? T : bs->T2;
+    Cand best = cand_none();   // this thread's best candidate (exact argmax)
     Cand cand = cand_none();   // this lane's candidate of the current item
     // an updated key: a candidate if present and >= T; an increment across T admits it to C
     auto consider = [&](size_t s, unsigned p, unsigned q, long long c, unsigned f, bool inc) -> bool {
@@ -1350,9 +1469,15 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
                         if ((p == M.b || p == M.nw) && L[2 * (size_t)q + 1] != 0) touched = true;
                     }
                 }
-                if (!touched && (f & kPresent) && c >= T) cand = Cand{c, K.key8[p], K.key8[q], e.x, p, q};
+                if (!touched && (f & kPresent)) cand = Cand{c, K.key8[p], K.key8[q], e.x, p, q};
             }
-            wave_top_offer<kTopM>(mine, cand.cnt != LLONG_MIN, cand, K);
+            if (cand_better(cand, best, K.pool, K.off, K.len)) best = cand;
+            {   // every present key >= T2 goes to the candidate list
+                const bool listed = cand.cnt != LLONG_MIN && cand.cnt >= T2;
+                const unsigned li = wave_append(listed, &bs->list_n);
+                if (listed && li < kListCap)
+                    list[li] = Partial{cand.cnt, cand.ka, cand.kb, cand.slot, cand.a, cand.b, 0};
+            }
             const unsigned idx = wave_append(add, &st->nC);
             if (add) {
                 if (idx < st->capC) P.C[idx] = add_e;
@@ -1360,11 +1485,19 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
             }
         }
     }
-    block_top<kTopM, kApplyBatchThreads / 64>(mine, s_wave, s_out, K);
-    if (tid < kTopM) {
-        const Cand c = s_out[tid];
-        part[blockIdx.x * kTopM + tid] = Partial{c.cnt, c.ka, c.kb, c.slot, c.a, c.b, 0};
+    if (pw0) probe_stamp(st, B.trip, 11);
+    for (int o = 32; o > 0; o >>= 1) {
+        const Cand oc = shfl_xor_cand(best, o);
+        if (cand_better(oc, best, K.pool, K.off, K.len)) best = oc;
     }
+    if ((tid & 63) == 0) s_wave[tid >> 6] = best;
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < (int)(kApplyBatchThreads / 64); ++w)
+            if (cand_better(s_wave[w], best, K.pool, K.off, K.len)) best = s_wave[w];
+        part[blockIdx.x] = Partial{best.cnt, best.ka, best.kb, best.slot, best.a, best.b, 0};
+    }
+    if (pw0) probe_stamp(st, B.trip, 12);
     if (blockIdx.x == 0 && tid == 0) {
         st->nparts = gridDim.x;
         if (!scan_only) {   // finish the trip: k rounds done
@@ -1374,6 +1507,7 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
             bs->prev_k = k;
         }
     }
+    if (pw0) probe_stamp(st, B.trip, 13);
 }
 
 // ------------------------------------------------------------------ word table build
@@ -1800,7 +1934,9 @@ class MergeLoop {
     DevBuf<Batch> batch_;
     DevBuf<uint32_t> tags_;      // per slot word: the last batch that claimed it
     DevBuf<int> trip_info_;      // per trip of a host batch: first round, members
-    DevBuf<Partial> lists_;      // per apply workgroup: its top-kTopM candidates
+    DevBuf<unsigned long long> probe_;   // BPE355_PROBE stamps
+    void report_probe();
+    DevBuf<Partial> list_;       // the candidate list (every present key >= T2)
     static constexpr unsigned kApplyBatchBlocks = 256;
     void reset_tags();
     void run_trips(bool timing, std::vector<hipEvent_t>& ev, double& k1_ms, double& k1_bytes,
@@ -1992,7 +2128,7 @@ void MergeLoop<TokT>::layout_blocks() {
     W.lblk0 = blk;
     W.lnblk = std::min(ceil_div(W.ln, 256u), 64u);
     blk += W.lnblk;
-    merge_grid_ = std::max(blk, 1u);
+    merge_grid_ = std::max(blk, (unsigned)kMaxBatch);   // k_merge_batch: block j registers member j
     wdev_ = W;
     // algorithmic bytes of one k_merge launch: every slot, and every long word's ids + length
     scan_bytes_ = 0;
@@ -2087,10 +2223,12 @@ int MergeLoop<TokT>::rebuild() {
     hs_.halt = HALT_NONE;
     push_state();
     hipLaunchKernelGGL(k_build_C, dim3(grid), dim3(256), 0, s_, pairs(), pcap_, T, st_.p);
-    if (batched_)   // the candidates of the rebuilt C as the apply workgroups' top-M lists
+    if (batched_) {   // the rebuilt C's best (partials) and candidate list
+        BPE_HIP(hipMemsetAsync(&bs_.p->list_n, 0, sizeof(unsigned), s_));
         hipLaunchKernelGGL(k_apply_batch, dim3(kApplyBatchBlocks), dim3(kApplyBatchThreads), 0, s_, st_.p, bs_.p,
                            (const Batch*)batch_.p, pairs(), toks(), LR_.p, 2ull * tok_cap_,
-                           (size_t)kMaxBatch * 2ull * tok_cap_, tok_cap_, lists_.p, 1);
+                           (size_t)kMaxBatch * 2ull * tok_cap_, tok_cap_, part_.p, list_.p, 1);
+    }
     else
         hipLaunchKernelGGL(k_argmax, dim3(kArgBlocks), dim3(256), 0, s_, st_.p, pairs(), toks(), part_.p);
     nparts_ = kArgBlocks;
@@ -2109,7 +2247,8 @@ void MergeLoop<TokT>::run() {
     st_.alloc(1);
     rs_.alloc(1);
     tok_cap_ = 256u + (unsigned)n_rounds_ + 1u;
-    part_.alloc(std::max<size_t>(kArgBlocks, ceil_div(4ull * tok_cap_, 256) + kCScanBlocks));
+    part_.alloc(std::max<size_t>(std::max<size_t>(kArgBlocks, kApplyBatchBlocks),
+                                 ceil_div(4ull * tok_cap_, 256) + kCScanBlocks));
     // single rank: batched rounds (BPE355_BATCH = members per trip, 1..8; 0 = the per-round
     // kernels); sharded per-round exchange: the per-round kernels
     {
@@ -2126,7 +2265,7 @@ void MergeLoop<TokT>::run() {
         batch_.alloc(1);
         BPE_HIP(hipMemsetAsync(batch_.p, 0, sizeof(Batch), s_));
         trip_info_.alloc(2 * kTrips);
-        lists_.alloc((size_t)kApplyBatchBlocks * kTopM);
+        list_.alloc(kListCap);
     }
     m_a_.alloc(n_rounds_); m_b_.alloc(n_rounds_); m_new_.alloc(n_rounds_); m_mode_.alloc(n_rounds_);
     const char* round_log = std::getenv("BPE355_ROUND_LOG");   // analysis knob: per-round records
@@ -2171,6 +2310,11 @@ void MergeLoop<TokT>::run() {
     hs_.halt = HALT_REBUILD;
     hs_.max_len = std::max(max_len_, 1u);
     hs_.max_batch = max_batch_;
+    if (batched_ && std::getenv("BPE355_PROBE")) {
+        probe_.alloc(16ull * (n_rounds_ / kProbeTrip + 2));
+        BPE_HIP(hipMemsetAsync(probe_.p, 0, probe_.bytes(), s_));
+        hs_.probe = probe_.p;
+    }
 
     const bool timing = timing_enabled();
     std::vector<hipEvent_t> ev;
@@ -2316,11 +2460,18 @@ void MergeLoop<TokT>::run() {
             std::fclose(f);
         }
     }
+    if (probe_.p) report_probe();
     if (batched_) {
         BatchState b{};
         BPE_HIP(hipMemcpy(&b, bs_.p, sizeof(b), hipMemcpyDeviceToHost));
         out_.stats.n_trips = trips_run_;
         out_.stats.n_rounds_batched = (int64_t)b.rounds_batched;
+        if (std::getenv("BPE355_TRACE")) {
+            std::fprintf(stderr, "[bpe355] trips: list overflow %llu, head miss %llu, short %llu; k:", b.n_overflow,
+                         b.n_headmiss, b.n_short);
+            for (int i = 0; i <= kMaxBatch; ++i) std::fprintf(stderr, " %llu", b.k_hist[i]);
+            std::fprintf(stderr, "\n");
+        }
     }
     out_.stats.merge_kernel_ms = k1_ms;
     out_.stats.merge_kernel_launches = k1_launches;
@@ -2353,6 +2504,33 @@ void MergeLoop<TokT>::run() {
     for (auto& m : tail) out_.merges.push_back(std::move(m));
 }
 
+// BPE355_PROBE summary (stderr): mean phase durations of the sampled trips, us
+template <class TokT>
+void MergeLoop<TokT>::report_probe() {
+    std::vector<unsigned long long> pr(probe_.n);
+    BPE_HIP(hipMemcpy(pr.data(), probe_.p, probe_.bytes(), hipMemcpyDeviceToHost));
+    const char* names[] = {"sel:insert", "sel:lists", "sel:meta", "sel:rule", "gap sel>merge", "merge:pop",
+                           "merge:rewrite", "merge:flush", "gap merge>apply", "apply:clear", "apply:items",
+                           "apply:blocktop", "apply:end", "gap apply>sel"};
+    const int from[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13};
+    const int to[] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 16};
+    double acc[14] = {};
+    int n = 0;
+    for (size_t t = 0; t + 1 < pr.size() / 16; ++t) {
+        const unsigned long long* p = &pr[16 * t];
+        const unsigned long long* q = &pr[16 * (t + 1)];
+        bool ok = true;
+        for (int i = 0; i < 14; ++i) ok &= p[i] != 0;
+        if (!ok) continue;
+        for (int i = 0; i < 13; ++i) acc[i] += (double)(p[to[i]] - p[from[i]]) * 0.01;
+        (void)q;
+        ++n;
+    }
+    std::fprintf(stderr, "[bpe355 probe] %d sampled trips, mean us:", n);
+    for (int i = 0; i < 13 && n; ++i) std::fprintf(stderr, " %s %.2f |", names[i], acc[i] / n);
+    std::fprintf(stderr, "\n");
+}
+
 template <class TokT>
 void MergeLoop<TokT>::reset_tags() {
     tags_.alloc(std::max(idev_.n_slot_words, 1u));
@@ -2371,14 +2549,16 @@ void MergeLoop<TokT>::run_trips(bool timing, std::vector<hipEvent_t>& ev, double
     for (int t = 0; t < kTrips; ++t) {
         const bool timed = timing && (trips_launched_ + t) % kTimingStride == 0;
         hipLaunchKernelGGL(k_select, dim3(1), dim3(kSelThreads), 0, s_, st_.p, bs_.p, pairs(), toks(), idev_,
-                           batch_.p, (const Partial*)lists_.p, m_a_.p, m_b_.p, m_new_.p, m_mode_.p, m_cnt_.p,
+                           batch_.p, (const Partial*)part_.p, (const Partial*)list_.p, m_a_.p, m_b_.p, m_new_.p,
+                           m_mode_.p, m_cnt_.p,
                            trip_info_.p, t);
         hipExtLaunchKernelGGL(k_merge_batch<TokT>, dim3(merge_grid_), dim3(256), 0, s_,
                               timed ? ev[2 * t] : nullptr, timed ? ev[2 * t + 1] : nullptr, 0,
                               st_.p, (const Batch*)batch_.p, pairs(), toks(), wdev_, idev_, LR_.p, lr_member,
                               lr_parity, tags_.p);
         hipLaunchKernelGGL(k_apply_batch, dim3(apply_blocks), dim3(kApplyBatchThreads), 0, s_, st_.p, bs_.p,
-                           (const Batch*)batch_.p, pairs(), toks(), LR_.p, lr_member, lr_parity, ntb, lists_.p, 0);
+                           (const Batch*)batch_.p, pairs(), toks(), LR_.p, lr_member, lr_parity, ntb, part_.p,
+                           list_.p, 0);
     }
     BPE_HIP(hipGetLastError());
     pull_state();
