@@ -815,7 +815,7 @@ struct Batch {
 
 // device-owned batch state (the host only initializes it; its limits live in RoundState)
 struct BatchState {
-    unsigned pend_insert;    // the last batch's new tokens still have to enter the dedupe map
+    unsigned pend_insert;    // unused (k_apply_batch inserts the batch's new tokens into the map)
     unsigned batch_seq;      // last batch_id handed out
     int trip;                // trips completed
     int prev_k;              // members of the last trip (its cells are cleared by the next apply)
@@ -827,6 +827,7 @@ struct BatchState {
     unsigned long long n_overflow, n_headmiss, n_short, k_hist[kMaxBatch + 1];   // diagnostics
 };
 constexpr unsigned kListCap = 64;   // the candidate list k_select sorts (one wave)
+constexpr unsigned kApplyGrid = 256;   // k_apply_batch workgroups (k_select reads one partial each)
 
 struct TokMetaS {
     unsigned long long ha, pb, hb, pa;   // hash(a), P^len(b), hash(b), P^len(a)
@@ -866,79 +867,31 @@ __device__ __forceinline__ Cand readlane_cand(const Cand& c, int j) {
     return r;
 }
 
-// A wave's sorted top-M candidates, distributed: lane i < M holds the i-th best (cand_none
-// padding), so no lane keeps an array.
-__device__ __forceinline__ Cand shfl_cand(const Cand& c, int src) {
-    Cand r;
-    r.cnt = __shfl(c.cnt, src);
-    r.ka = __shfl(c.ka, src);
-    r.kb = __shfl(c.kb, src);
-    r.slot = __shfl(c.slot, src);
-    r.a = __shfl(c.a, src);
-    r.b = __shfl(c.b, src);
-    return r;
-}
-// every lane of the wave calls; lanes with `has` offer c
-template <int M>
-__device__ __forceinline__ void wave_top_offer(Cand& mine, bool has, const Cand& c, const ToksDev& K) {
-    const int lane = threadIdx.x & 63;
-    const Cand last = shfl_cand(mine, M - 1);
-    unsigned long long pend = __ballot(has && cand_better(c, last, K.pool, K.off, K.len));
-    while (pend) {
-        const int src = __ffsll((long long)pend) - 1;
-        pend &= pend - 1;
-        const Cand x = shfl_cand(c, src);
-        const bool ahead = lane < M && cand_better(mine, x, K.pool, K.off, K.len);
-        const int pos = __popcll(__ballot(ahead));   // entries that stay ahead of x
-        if (pos < M) {
-            const Cand up = shfl_cand(mine, lane > 0 ? lane - 1 : 0);
-            if (lane > pos && lane < M) mine = up;
-            if (lane == pos) mine = x;
-        }
+// A listed candidate's token metadata and dedupe lookup (does the pair's byte string exist as a
+// token already?).  The map holds every token up to the last trip's (k_apply_batch inserts them).
+__device__ __forceinline__ void cand_meta(const Cand& c, const ToksDev& K, const IndexDev& X, TokMetaS& m,
+                                          unsigned& old) {
+    const unsigned a = c.a, b = c.b;
+    m.ha = K.hash[a]; m.pb = K.pw[b]; m.hb = K.hash[b]; m.pa = K.pw[a];
+    m.la = K.len[a]; m.lb = K.len[b];
+    m.za = X.len[a]; m.zb = X.len[b]; m.ba = X.beg[a]; m.bb = X.beg[b];
+    const unsigned long long h = m.ha * m.pb + m.hb;
+    const unsigned ln = m.la + m.lb;
+    unsigned s = (unsigned)mix64(h) & K.map_mask;
+    old = ~0u;
+    for (unsigned mm = K.map[s]; mm != 0; s = (s + 1) & K.map_mask, mm = K.map[s]) {
+        const unsigned id = mm - 1;
+        if (K.hash[id] == h && K.len[id] == ln && equals_concat(K, id, a, b)) { old = id; break; }
     }
-}
-// a workgroup's top-M from its waves' lists (every thread calls; out[0..M) valid after return):
-// the NW * M entries go to LDS, then wave 0 extracts the best M (each lane scans its share)
-template <int M, int NW>
-__device__ __forceinline__ void block_top(const Cand& mine, Cand (*s_wave)[M], Cand* out, const ToksDev& K) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (lane < M) s_wave[wv][lane] = mine;
-    __syncthreads();
-    if (wv == 0) {
-        constexpr int E = NW * M, PER = (E + 63) / 64;
-        Cand* flat = &s_wave[0][0];
-        unsigned taken = 0;   // bit i: this lane's entry i was extracted
-        for (int t = 0; t < M; ++t) {
-            Cand best = cand_none();
-            int bi = -1;
-#pragma unroll
-            for (int i = 0; i < PER; ++i) {
-                const int e = lane + 64 * i;
-                if (e >= E || ((taken >> i) & 1)) continue;
-                const Cand x = flat[e];
-                if (x.cnt != LLONG_MIN && (bi < 0 || cand_better(x, best, K.pool, K.off, K.len))) { best = x; bi = i; }
-            }
-            int from = lane;
-            for (int o = 32; o > 0; o >>= 1) {
-                const Cand oc = shfl_xor_cand(best, o);
-                const int of = __shfl_xor(from, o);
-                if (cand_better(oc, best, K.pool, K.off, K.len) ||
-                    (!cand_better(best, oc, K.pool, K.off, K.len) && of < from)) {
-                    best = oc;
-                    from = of;
-                }
-            }
-            if (lane == from && bi >= 0) taken |= 1u << bi;
-            if (lane == 0) out[t] = best;
-        }
-    }
-    __syncthreads();
 }
 
-constexpr int kSelThreads = 512;
-// One workgroup: the top-(kMaxBatch + 1) candidates of C, the batch rule, the batch record, and
-// the merge records of its rounds.  Also puts the previous batch's new tokens into the dedupe
-// map first (single writer of the map).
+// One workgroup: the batch of this trip.  Waves 0-3 reduce the apply's per-workgroup partials
+// to the exact best candidate P1; wave 4 ranks the candidate list (every present key >= T2) and
+// looks up its entries' metadata; thread 0 has loaded the scalars meanwhile.  All global loads
+// are issued before the first barrier, so the kernel costs about one memory round trip plus the
+// dedupe lookups' chain, then the rule (thread 0) and the record (one thread per member).
+constexpr int kSelThreads = 320;
+constexpr int kSelListWave = 4;
 __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__ st, BatchState* __restrict__ bs,
                                                         PairsDev P, ToksDev K, IndexDev X, Batch* __restrict__ bt,
                                                         const Partial* __restrict__ part,
@@ -947,205 +900,207 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
                                                         uint32_t* __restrict__ m_new, uint32_t* __restrict__ m_mode,
                                                         long long* __restrict__ m_cnt, int* __restrict__ trip_info,
                                                         int trip_slot) {
-    __shared__ Cand s_wave[kSelThreads / 64][kTopM];
-    __shared__ Cand s_fin[kTopM], s_list[kTopM];
+    static_assert(kApplyGrid <= 64 * kSelListWave, "one partial per thread of waves 0-3");
+    __shared__ Cand s_wave[kSelListWave];
+    __shared__ Cand s_list[kTopM];
     __shared__ long long s_rankcnt[kListCap];
-    __shared__ int s_nfin, s_stop;
-    __shared__ unsigned s_fresh[kTopM], s_nw_old[kTopM];
+    __shared__ unsigned s_nw_old[kTopM];
     __shared__ TokMetaS s_meta[kTopM];
-    __shared__ unsigned s_off[kMaxBatch], s_newid[kMaxBatch], s_pre[kMaxBatch + 1];
-    __shared__ int s_k, s_round, s_nrounds, s_trip, s_prevk;
-    __shared__ unsigned s_pool, s_bid;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int ptrip = bs->trip;
-    if (tid == 0) {   // scalars the rule needs, loaded together
-        s_round = st->round; s_nrounds = st->n_rounds; s_trip = bs->trip; s_prevk = bs->prev_k;
-        s_pool = st->pool_used; s_bid = bs->batch_seq + 1;
-    }
     if (tid == 0) probe_stamp(st, ptrip, 0);
-    // ---- the previous batch's tokens enter the dedupe map
-    if (bs->pend_insert) {
-        const int pk = bt->k;
-        if (tid < pk && bt->m[tid].isnew) {
-            const unsigned nw = bt->m[tid].nw;
-            unsigned s = (unsigned)mix64(bt->m[tid].hash) & K.map_mask;
-            while (atomicCAS(&K.map[s], 0u, nw + 1) != 0u) s = (s + 1) & K.map_mask;
-        }
-        __syncthreads();
-        if (tid == 0) bs->pend_insert = 0;
-    }
-    if (tid == 0) probe_stamp(st, ptrip, 1);
-    const int halt = st->halt;
-    if (halt) {
-        if (tid == 0) {
-            bt->stop = -1;
-            if (trip_info) { trip_info[2 * trip_slot] = -1; trip_info[2 * trip_slot + 1] = 0; }
-        }
-        return;
-    }
-    // ---- the best candidate: the apply workgroups' partials (exact); the next ones: the
-    // candidate list, which holds every present key >= T2 (exact top-M among them)
-    const unsigned nC = st->nC;
-    const long long T = st->T;
+    // ---- every independent load first
+    Partial q{};
+    if (wv < kSelListWave) q = part[tid];   // the buffer holds kApplyBatchBlocks entries
+    Partial lq{};
+    if (wv == kSelListWave) lq = list[lane];
     const int nparts = st->nparts;
-    {
+    const unsigned ln = bs->list_n;
+    if (tid == 0) probe_stamp(st, ptrip, 1);
+    if (wv < kSelListWave) {   // P1: the exact best over the partials
         Cand best = cand_none();
-        for (int i = tid; i < nparts; i += kSelThreads) {
-            const Partial q = part[i];
-            const Cand c{q.cnt, q.ka, q.kb, q.slot, q.a, q.b};
-            if (cand_better(c, best, K.pool, K.off, K.len)) best = c;
-        }
+        if (tid < nparts) best = Cand{q.cnt, q.ka, q.kb, q.slot, q.a, q.b};
         for (int o = 32; o > 0; o >>= 1) {
             const Cand oc = shfl_xor_cand(best, o);
             if (cand_better(oc, best, K.pool, K.off, K.len)) best = oc;
         }
-        if ((tid & 63) == 0) s_wave[tid >> 6][0] = best;
-    }
-    const unsigned ln = bs->list_n;
-    if (tid < kTopM) s_list[tid] = cand_none();
-    __syncthreads();
-    if (tid < 64) {   // wave 0: each listed key's rank = the listed keys better than it
+        if (lane == 0) s_wave[wv] = best;
+    } else if (wv == kSelListWave) {   // the list: metadata of every entry, then its rank
+        if (lane < kTopM) s_list[lane] = cand_none();
         const bool usable = ln <= kListCap;
-        Cand x = cand_none();
-        if (usable && (unsigned)tid < ln) {
-            const Partial q = list[tid];
-            x = Cand{q.cnt, q.ka, q.kb, q.slot, q.a, q.b};
-        }
         const int nl = usable ? (int)ln : 0;
+        const bool have = lane < nl;
+        const Cand x = have ? Cand{lq.cnt, lq.ka, lq.kb, lq.slot, lq.a, lq.b} : cand_none();
+        TokMetaS m{};
+        unsigned old = ~0u;
+        if (have) cand_meta(x, K, X, m, old);
         int rank = 0;
         for (int j = 0; j < nl; ++j) {
             const Cand y = readlane_cand(x, j);
             rank += cand_better(y, x, K.pool, K.off, K.len) ? 1 : 0;
         }
-        if (x.cnt != LLONG_MIN && rank < kTopM) s_list[rank] = x;
-        if (x.cnt != LLONG_MIN) s_rankcnt[rank] = x.cnt;
+        __builtin_amdgcn_wave_barrier();
+        if (have && rank < kTopM) {
+            s_list[rank] = x;
+            s_meta[rank] = m;
+            s_nw_old[rank] = old;
+        }
+        if (have) s_rankcnt[rank] = x.cnt;
     }
     __syncthreads();
     if (tid == 0) probe_stamp(st, ptrip, 2);
-    if (tid == 0) {
-        Cand p1 = s_wave[0][0];
-        for (int w = 1; w < kSelThreads / 64; ++w)
-            if (cand_better(s_wave[w][0], p1, K.pool, K.off, K.len)) p1 = s_wave[w][0];
-        // the list's head is the global best whenever the best is >= T2 and nothing overflowed
-        int nf = 1;
-        s_fin[0] = p1;
-        const bool list_ok = ln <= kListCap && s_list[0].cnt != LLONG_MIN && s_list[0].slot == p1.slot &&
-                             s_list[0].a == p1.a && s_list[0].b == p1.b;
-        if (list_ok)
-            while (nf < kTopM && s_list[nf].cnt != LLONG_MIN) { s_fin[nf] = s_list[nf]; ++nf; }
-        if (ln > kListCap) bs->n_overflow++;
-        else if (!list_ok) bs->n_headmiss++;
-        else if (nf < kTopM) bs->n_short++;
-        s_nfin = nf;
-        const int round = st->round;
-        int stop = HALT_NONE;
-        if (round >= st->n_rounds) stop = HALT_DONE;
-        else if (nC > st->c_limit) stop = HALT_REBUILD;               // C bloated: re-threshold
-        else if (nf == 0 || s_fin[0].cnt < T) stop = HALT_REBUILD;    // max(C) < T: re-threshold
-        else if (round >= st->host_round || st->n_single > st->single_limit ||
-                 st->pair_used + 2ull * (unsigned)(st->ntok + kMaxBatch) * kMaxBatch > st->pair_limit ||
-                 st->pool_used + (unsigned long long)kMaxBatch * st->max_len > st->pool_cap)
-            stop = HALT_HOST;
-        s_stop = stop;
-        if (stop) {
-            st->halt = stop;
+    if (wv != 0) return;
+    // ---- wave 0: the rule and the record, lane i holding candidate i (no workgroup barrier)
+    const int halt = st->halt, round = st->round, n_rounds = st->n_rounds, host_round = st->host_round;
+    const unsigned nC = st->nC, c_limit = st->c_limit;
+    const long long T = st->T;
+    const unsigned n_single = st->n_single, single_limit = st->single_limit;
+    const unsigned long long pair_used = st->pair_used, pair_limit = st->pair_limit;
+    const unsigned pool_used = st->pool_used, pool_cap = st->pool_cap;
+    const unsigned max_len = st->max_len;
+    const int ntok = st->ntok, max_batch = st->max_batch;
+    const int prev_k = bs->prev_k;
+    const unsigned bid = bs->batch_seq + 1;
+    const long long T2old = bs->T2;
+    Cand p1 = s_wave[0];
+    for (int w = 1; w < kSelListWave; ++w)
+        if (cand_better(s_wave[w], p1, K.pool, K.off, K.len)) p1 = s_wave[w];
+    // the list's head is the global best whenever the best is >= T2 and nothing overflowed; the
+    // ranks are distinct, so s_list holds a prefix
+    const bool list_ok = ln <= kListCap && s_list[0].cnt != LLONG_MIN && s_list[0].slot == p1.slot &&
+                         s_list[0].a == p1.a && s_list[0].b == p1.b;
+    int nf = 1;
+    if (list_ok) {
+        const unsigned long long vm =
+            __ballot(lane >= 1 && lane < kTopM && s_list[lane < kTopM ? lane : 0].cnt != LLONG_MIN) | 1ull;
+        nf = __builtin_ctzll(~vm);
+    }
+    int stop = HALT_NONE;
+    if (halt) stop = halt;
+    else if (round >= n_rounds) stop = HALT_DONE;
+    else if (nC > c_limit) stop = HALT_REBUILD;                        // C bloated: re-threshold
+    else if (p1.cnt == LLONG_MIN || p1.cnt < T) stop = HALT_REBUILD;   // max(C) < T: re-threshold
+    else if (round >= host_round || n_single > single_limit ||
+             pair_used + 2ull * (unsigned)(ntok + kMaxBatch) * kMaxBatch > pair_limit ||
+             pool_used + (unsigned long long)kMaxBatch * max_len > pool_cap)
+        stop = HALT_HOST;
+    if (lane == 0 && !halt) {   // no-return atomics: nothing waits on them
+        if (ln > kListCap) atomicAdd(&bs->n_overflow, 1ull);
+        else if (!list_ok) atomicAdd(&bs->n_headmiss, 1ull);
+        else if (nf < kTopM) atomicAdd(&bs->n_short, 1ull);
+    }
+    if (stop) {
+        if (lane == 0) {
+            if (!halt) st->halt = stop;
             bt->stop = -1;
             if (trip_info) { trip_info[2 * trip_slot] = -1; trip_info[2 * trip_slot + 1] = 0; }
         }
+        return;
     }
-    __syncthreads();
-    if (s_stop) return;
-    // ---- the candidates' token metadata and dedupe lookups (one thread each)
-    const int nf = s_nfin;
-    const int ntok = st->ntok;
-    if (tid < nf && tid < kMaxBatch) {
-        const Cand c = s_fin[tid];
-        const unsigned a = c.a, b = c.b;
-        TokMetaS m;
-        m.ha = K.hash[a]; m.pb = K.pw[b]; m.hb = K.hash[b]; m.pa = K.pw[a];
-        m.la = K.len[a]; m.lb = K.len[b];
-        m.za = X.len[a]; m.zb = X.len[b]; m.ba = X.beg[a]; m.bb = X.beg[b];
-        const unsigned long long h = m.ha * m.pb + m.hb;
-        const unsigned ln = m.la + m.lb;
-        unsigned s = (unsigned)mix64(h) & K.map_mask;
-        unsigned old = ~0u;
-        for (unsigned mm = K.map[s]; mm != 0; s = (s + 1) & K.map_mask, mm = K.map[s]) {
-            const unsigned id = mm - 1;
-            if (K.hash[id] == h && K.len[id] == ln && equals_concat(K, id, a, b)) { old = id; break; }
-        }
-        s_meta[tid] = m;
-        s_fresh[tid] = old == ~0u;
-        s_nw_old[tid] = old;
+    const int i = lane;
+    Cand e = cand_none();
+    TokMetaS m{};
+    unsigned old = ~0u;
+    if (i == 0) {
+        e = p1;
+        if (list_ok) { m = s_meta[0]; old = s_nw_old[0]; }
+        else cand_meta(p1, K, X, m, old);   // rare: P1 alone, its metadata here
+    } else if (i < nf) {
+        e = s_list[i];
+        m = s_meta[i];
+        old = s_nw_old[i];
     }
-    __syncthreads();
-    if (tid == 0) probe_stamp(st, ptrip, 3);
-    // ---- the batch rule (thread 0), then the record filled by one thread per member
-    if (tid == 0) {
-        const int maxb = min(st->max_batch, kMaxBatch);
-        int k = 1;
-        const Cand& p0 = s_fin[0];
-        if (p0.a != p0.b && s_fresh[0]) {
-            while (k < maxb && k < nf) {
-                const Cand& c = s_fin[k];
-                if (c.cnt < T || c.a == c.b || !s_fresh[k]) break;
-                bool clash = false;
-                for (int j = 0; j < k; ++j)
-                    clash |= s_fin[j].a == c.a || s_fin[j].a == c.b || s_fin[j].b == c.a || s_fin[j].b == c.b;
-                // new bytes must differ from every earlier member's new bytes
-                const unsigned long long h = s_meta[k].ha * s_meta[k].pb + s_meta[k].hb;
-                const unsigned ln = s_meta[k].la + s_meta[k].lb;
-                for (int j = 0; j < k && !clash; ++j) {
-                    if (s_meta[j].ha * s_meta[j].pb + s_meta[j].hb != h || s_meta[j].la + s_meta[j].lb != ln) continue;
-                    bool eq = true;
-                    for (unsigned i = 0; i < ln && eq; ++i)
-                        eq = concat_byte(K, s_fin[j].a, s_meta[j].la, s_fin[j].b, i) ==
-                             concat_byte(K, c.a, s_meta[k].la, c.b, i);
-                    clash = eq;
-                }
-                if (clash) break;
-                ++k;
+    const bool fr = i < nf && old == ~0u;
+    const unsigned long long h = m.ha * m.pb + m.hb;
+    const unsigned lk = m.la + m.lb;
+    // (1) tokens disjoint from, and (3) new bytes different from, every earlier candidate's
+    bool clash = false;
+    for (int j = 0; j < kMaxBatch; ++j) {
+        const unsigned aj = __builtin_amdgcn_readlane((int)e.a, j), bj = __builtin_amdgcn_readlane((int)e.b, j);
+        const unsigned long long hj = readlane64(h, j);
+        const unsigned lj = __builtin_amdgcn_readlane((int)lk, j), laj = __builtin_amdgcn_readlane((int)m.la, j);
+        if (j < i && i < nf) {
+            clash |= aj == e.a || aj == e.b || bj == e.a || bj == e.b;
+            if (!clash && hj == h && lj == lk) {
+                bool eq = true;
+                for (unsigned x = 0; x < lk && eq; ++x)
+                    eq = concat_byte(K, aj, laj, bj, x) == concat_byte(K, e.a, m.la, e.b, x);
+                clash = eq;
             }
-            // (4) strictly above the next candidate: listed (s_fin[k]), or unlisted (below T2,
-            // and every member is listed, so >= T2)
-            while (k > 1 && k < nf && !(s_fin[k - 1].cnt > s_fin[k].cnt)) --k;
         }
-        k = min(k, s_nrounds - s_round);
-        // per member: pool offset, new id, posting-list prefix
-        unsigned pool = s_pool, fresh = 0, pre = 0, full = 0;
-        for (int j = 0; j < k; ++j) {
-            const TokMetaS& m = s_meta[j];
-            const bool pick_a = m.za <= m.zb;
-            const unsigned lu = pick_a ? m.za : m.zb;
-            const bool use = lu != kNoAnc && lu <= X.full_threshold;
-            s_off[j] = pool;
-            s_newid[j] = s_fresh[j] ? (unsigned)ntok + fresh : s_nw_old[j];
-            s_pre[j] = pre;
-            if (s_fresh[j]) { pool += m.la + m.lb; ++fresh; }
-            pre += use ? lu : 0;
-            full |= !use;
-        }
-        s_pre[k] = pre;
-        s_k = k;
-        Batch& B = *bt;
+    }
+    // k: the first candidate that fails (count >= T, (2) a != b, fresh, no clash), within the
+    // allowed batch; one merge when P1 itself is not batchable
+    const int maxb = min(max_batch, kMaxBatch);
+    const bool okb = i >= 1 && i < nf && e.cnt >= T && e.a != e.b && fr && !clash;
+    int k = __builtin_ctzll(~(__ballot(okb) | 1ull));
+    k = min(k, min(maxb, nf));
+    if (!(p1.a != p1.b && __builtin_amdgcn_readlane((int)fr, 0))) k = 1;
+    // (4) strictly above the next candidate: listed (candidate k), or unlisted (below T2, and
+    // every member is listed, so >= T2): the largest k' <= k with that gap
+    {
+        const long long cprev = __shfl(e.cnt, i > 0 ? i - 1 : 0);
+        const unsigned long long gm =
+            __ballot(i >= 1 && (i >= nf || cprev > e.cnt)) & ((2ull << k) - 1) & ~1ull;
+        k = gm ? 63 - __builtin_clzll(gm) : 1;
+    }
+    k = min(k, n_rounds - round);
+    // per member: pool offset, new id, posting-list prefix (exclusive scans over lanes < k)
+    const bool mem = i < k;
+    const unsigned lu = m.za <= m.zb ? m.za : m.zb, bu = m.za <= m.zb ? m.ba : m.bb;
+    const bool use = lu != kNoAnc && lu <= X.full_threshold;
+    const unsigned add_pool = mem && fr ? lk : 0u, add_fresh = mem && fr ? 1u : 0u, add_list = mem && use ? lu : 0u;
+    unsigned pre_pool = 0, pre_fresh = 0, pre_list = 0;
+    for (int j = 0; j < kMaxBatch; ++j) {
+        const unsigned pj = __builtin_amdgcn_readlane((int)add_pool, j);
+        const unsigned fj = __builtin_amdgcn_readlane((int)add_fresh, j);
+        const unsigned uj = __builtin_amdgcn_readlane((int)add_list, j);
+        if (j < i) { pre_pool += pj; pre_fresh += fj; pre_list += uj; }
+    }
+    const bool full = __ballot(mem && !use) != 0;
+    const unsigned tot_pool = __builtin_amdgcn_readlane((int)pre_pool, k);
+    const unsigned tot_fresh = __builtin_amdgcn_readlane((int)pre_fresh, k);
+    Batch& B = *bt;
+    if (i <= k) B.list_pre[i] = pre_list;
+    if (mem) {
+        BatchMember M;
+        M.a = e.a; M.b = e.b; M.slot = e.slot; M.cnt = e.cnt;
+        M.nw = fr ? (unsigned)ntok + pre_fresh : old;
+        M.isnew = fr;
+        M.hash = h;
+        M.pw = m.pa * m.pb;
+        M.ln = lk;
+        M.k8 = m.la >= 8 ? e.ka : (e.ka | (e.kb >> (8 * m.la)));
+        M.use_list = use;
+        M.list_beg = use ? bu : 0;
+        M.list_len = use ? lu : 0;
+        M.cov_beg = bu;
+        M.cov_len = fr ? lu : kNoAnc;   // dedupe: uncovered until the next index build
+        M.pool_off = pool_used + pre_pool;
+        B.m[i] = M;
+        m_a[round + i] = e.a; m_b[round + i] = e.b; m_new[round + i] = M.nw;
+        m_mode[round + i] = use ? lu : 0xffffffffu;
+        if (m_cnt) m_cnt[round + i] = e.cnt;
+    }
+    if (lane == 0) {
         B.stop = 0;
         B.k = k;
-        B.round = s_round;
+        B.round = round;
         B.ntok = ntok;
-        B.trip = s_trip;
-        B.prev_k = s_prevk;
-        B.batch_id = s_bid;
+        B.trip = ptrip;
+        B.prev_k = prev_k;
+        B.batch_id = bid;
         B.nC_base = nC;
         B.full_scan = full;
-        B.n_fresh = fresh;
-        for (int j = 0; j <= k; ++j) B.list_pre[j] = s_pre[j];
-        st->pool_used = pool;
-        bs->batch_seq = s_bid;
+        B.n_fresh = tot_fresh;
+        st->pool_used = pool_used + tot_pool;
+        bs->batch_seq = bid;
         {   // the next list: about kListTarget keys.  With the list ranked, T2 = the count of the
             // kListTarget-th best (this trip pops at most kMaxBatch of those above it); on overflow
             // raise T2 halfway to the top; with too few keys, extend the range below the last one
             constexpr unsigned kListTarget = 24;
-            const long long top = s_fin[0].cnt;
-            const long long t2 = bs->T2 < T ? T : bs->T2;
+            const long long top = p1.cnt;
+            const long long t2 = T2old < T ? T : T2old;
             long long nt;
             if (ln > kListCap) nt = t2 + (top - t2) / 2;
             else if (ln >= kListTarget) nt = s_rankcnt[kListTarget - 1];
@@ -1154,47 +1109,25 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
             bs->T2 = nt < T ? T : (nt > top ? top : nt);
             bs->list_n = 0;   // the apply of this trip fills it again
         }
-        bs->pend_insert = fresh != 0;
-        if (k > 1) { bs->rounds_batched += k; bs->trips_batched += 1; }
-        bs->k_hist[k]++;
-        if (trip_info) { trip_info[2 * trip_slot] = s_round; trip_info[2 * trip_slot + 1] = k; }
+        if (k > 1) {
+            atomicAdd(&bs->rounds_batched, (unsigned long long)k);
+            atomicAdd(&bs->trips_batched, 1ull);
+        }
+        atomicAdd(&bs->k_hist[k], 1ull);
+        if (trip_info) { trip_info[2 * trip_slot] = round; trip_info[2 * trip_slot + 1] = k; }
+        probe_stamp(st, ptrip, 3);
+        probe_stamp(st, ptrip, 4);
     }
-    __syncthreads();
-    const int k = s_k;
-    if (tid < k) {
-        const int j = tid, round = s_round;
-        const Cand c = s_fin[j];
-        const TokMetaS m = s_meta[j];
-        BatchMember M;
-        const bool isnew = s_fresh[j];
-        M.a = c.a; M.b = c.b; M.slot = c.slot; M.cnt = c.cnt;
-        M.nw = s_newid[j];
-        M.isnew = isnew;
-        M.hash = m.ha * m.pb + m.hb;
-        M.pw = m.pa * m.pb;
-        M.ln = m.la + m.lb;
-        M.k8 = m.la >= 8 ? c.ka : (c.ka | (c.kb >> (8 * m.la)));
-        const bool pick_a = m.za <= m.zb;
-        const unsigned lu = pick_a ? m.za : m.zb, bu = pick_a ? m.ba : m.bb;
-        M.use_list = lu != kNoAnc && lu <= X.full_threshold;
-        M.list_beg = M.use_list ? bu : 0;
-        M.list_len = M.use_list ? lu : 0;
-        M.cov_beg = bu;
-        M.cov_len = isnew ? lu : kNoAnc;   // dedupe: uncovered until the next index build
-        M.pool_off = s_off[j];
-        bt->m[j] = M;
-        m_a[round + j] = c.a; m_b[round + j] = c.b; m_new[round + j] = M.nw;
-        m_mode[round + j] = M.use_list ? M.list_len : 0xffffffffu;
-        if (m_cnt) m_cnt[round + j] = c.cnt;
-    }
-    if (tid == 0) probe_stamp(st, ptrip, 4);
 }
 
-// the slot word of class C addressed directly, every member applied in order
+// the slot word of class C addressed directly, every member applied in order.  claim: the word
+// (global slot index f) may be on several members' lists; the first thread to claim it rewrites
+// it.  The word is loaded before the claim: only the claimant writes it during this batch.
 template <class TokT, int C>
 __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigned i, const Batch& B,
                                                  unsigned long long* LRt, size_t lr_member,
-                                                 unsigned long long* lds, unsigned& singles) {
+                                                 unsigned long long* lds, unsigned& singles,
+                                                 uint32_t* tags = nullptr, unsigned f = 0) {
     constexpr int W = slot_w(C);
     constexpr int V = W * (int)sizeof(TokT) / 16;
     TokT* s = S.slot + (size_t)i * W;
@@ -1202,6 +1135,7 @@ __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigne
 #pragma unroll
     for (int v = 0; v < V; ++v) r[v] = reinterpret_cast<const uint4*>(s)[v];
     const unsigned long long c = S.cnt[i];   // issued with the slot
+    if (tags && atomicMax(&tags[f], B.batch_id) >= B.batch_id) return;
     TokT e[W];
     __builtin_memcpy(e, r, sizeof(e));
     for (int j = 0; j < B.k; ++j) {
@@ -1304,11 +1238,10 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
                 while (j + 1 < k && i >= B.list_pre[j + 1]) ++j;
                 const unsigned f = X.list[B.m[j].list_beg + (i - B.list_pre[j])];
                 // a word on several members' lists is rewritten by the first thread to claim it
-                if (atomicMax(&tags[f], B.batch_id) >= B.batch_id) continue;
-                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f, B, LRt, lr_member, l_lr, singles);
-                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1], B, LRt, lr_member, l_lr, singles);
-                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2], B, LRt, lr_member, l_lr, singles);
-                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3], B, LRt, lr_member, l_lr, singles);
+                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f, B, LRt, lr_member, l_lr, singles, tags, f);
+                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1], B, LRt, lr_member, l_lr, singles, tags, f);
+                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2], B, LRt, lr_member, l_lr, singles, tags, f);
+                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3], B, LRt, lr_member, l_lr, singles, tags, f);
             }
         }
     }
@@ -1352,6 +1285,7 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
 // entries alone (after a rebuild of C).
 constexpr unsigned kBatchApplyItems = 4;
 constexpr unsigned kApplyBatchThreads = 256;
+constexpr unsigned kApplyCLds = 256;   // C admissions a workgroup stages in LDS (more: direct appends)
 __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* __restrict__ st,
                                                                     BatchState* __restrict__ bs,
                                                                     const Batch* __restrict__ bt, PairsDev P, ToksDev K,
@@ -1362,6 +1296,9 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     __shared__ unsigned s_tok[3 * kMaxBatch];
     __shared__ int s_ns;
     __shared__ Cand s_wave[kApplyBatchThreads / 64];
+    __shared__ Partial s_lst[kListCap];
+    __shared__ uint4 s_cadd[kApplyCLds];
+    __shared__ unsigned s_nl, s_nc, s_lbase, s_cbase;
     const Batch& B = *bt;
     if (!scan_only && B.stop) return;   // halted: part[] keeps the lists the next select reads
     const int k = scan_only ? 0 : B.k;
@@ -1369,16 +1306,21 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     const bool pw0 = !scan_only && blockIdx.x == 0 && tid == 0;
     if (pw0) probe_stamp(st, B.trip, 9);
     if (tid == 0) {   // S, deduplicated (a == b is possible only when k == 1)
+        unsigned t[3 * kMaxBatch];
+#pragma unroll
+        for (int j = 0; j < kMaxBatch; ++j) {
+            t[3 * j] = B.m[j].a; t[3 * j + 1] = B.m[j].b; t[3 * j + 2] = B.m[j].nw;
+        }
         int ns = 0;
-        for (int j = 0; j < k; ++j) {
-            const unsigned t3[3] = {B.m[j].a, B.m[j].b, B.m[j].nw};
-            for (int q = 0; q < 3; ++q) {
-                bool dup = false;
-                for (int u = 0; u < ns; ++u) dup |= s_tok[u] == t3[q];
-                if (!dup) s_tok[ns++] = t3[q];
-            }
+#pragma unroll
+        for (int i = 0; i < 3 * kMaxBatch; ++i) {
+            bool dup = i >= 3 * k;
+            for (int u = 0; u < ns; ++u) dup |= s_tok[u] == t[i];
+            if (!dup) s_tok[ns++] = t[i];
         }
         s_ns = ns;
+        s_nl = 0;
+        s_nc = 0;
     }
     __syncthreads();
     const int ns = s_ns;
@@ -1406,34 +1348,84 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     };
     const long long T2 = bs->T2 < T ? T : bs->T2;
     Cand best = cand_none();   // this thread's best candidate (exact argmax)
-    Cand cand = cand_none();   // this lane's candidate of the current item
-    // an updated key: a candidate if present and >= T; an increment across T admits it to C
-    auto consider = [&](size_t s, unsigned p, unsigned q, long long c, unsigned f, bool inc) -> bool {
-        if (s == ~(size_t)0 || !(f & kPresent) || c < T) return false;
-        cand = Cand{c, K.key8[p], K.key8[q], (unsigned)s, p, q};
-        if (!inc || (f & kInC)) return false;
-        P.flag[s] = f | kInC;
-        return true;
+    // a candidate for the list (>= T2) and for this thread's best
+    auto offer = [&](const Cand& c) {
+        if (cand_better(c, best, K.pool, K.off, K.len)) best = c;
+        if (c.cnt != LLONG_MIN && c.cnt >= T2) {
+            const unsigned li = atomicAdd(&s_nl, 1u);
+            if (li < kListCap) s_lst[li] = Partial{c.cnt, c.ka, c.kb, c.slot, c.a, c.b, 0};
+        }
     };
-    for (unsigned base = (blockIdx.x * blockDim.x + (tid & ~63u)) * kBatchApplyItems; base < n_items;
-         base += S * kBatchApplyItems) {
+    // an increment across T admits the key to C
+    auto admit = [&](size_t s, unsigned p, unsigned q) {
+        const unsigned ci = atomicAdd(&s_nc, 1u);
+        if (ci < kApplyCLds) {
+            s_cadd[ci] = make_uint4((unsigned)s, p, q, 0u);
+        } else {
+            const unsigned idx = atomicAdd(&st->nC, 1u);
+            if (idx < st->capC) P.C[idx] = make_uint4((unsigned)s, p, q, 0u);
+            else atomicOr(&st->err, ERR_C_FULL);
+        }
+    };
+    // an updated key: a candidate if present and >= T
+    auto updated = [&](size_t s, unsigned p, unsigned q, long long c, unsigned f, bool inc,
+                       unsigned long long kp, unsigned long long kq) {
+        if (s == ~(size_t)0 || !(f & kPresent) || c < T) return;
+        offer(Cand{c, kp, kq, (unsigned)s, p, q});
+        if (inc && !(f & kInC)) {
+            P.flag[s] = f | kInC;
+            admit(s, p, q);
+        }
+    };
+    // step u of a pass takes items base + u * S + g: a wave's 64 items are contiguous (coalesced)
+    // and its steps far apart, so the dense start of each member's cells (the byte tokens, which
+    // neighbour everything) spreads over many waves instead of serialising in a few
+    for (unsigned base = 0; base < n_items; base += S * kBatchApplyItems) {
+        // every item's first load, then every C entry's slot state, before any processing
+        unsigned long long dv[kBatchApplyItems];
+        uint4 ce[kBatchApplyItems];
+#pragma unroll
         for (unsigned u = 0; u < kBatchApplyItems; ++u) {
-            const unsigned v = base + u * 64 + (tid & 63);
-            bool add = false;
-            uint4 add_e = make_uint4(0, 0, 0, 0);
-            cand = cand_none();
+            const unsigned v = base + u * S + g;
+            dv[u] = 0;
+            ce[u] = make_uint4(0, 0, 0, 0);
             if (v < n_cell) {
                 const unsigned j = v / per_member, r = v % per_member, x = r >> 2, op = r & 3;
-                const BatchMember& M = B.m[j];
-                const long long d = (long long)LRc[(size_t)j * lr_member + 2 * (size_t)x + (op >> 1)];
+                dv[u] = LRc[(size_t)j * lr_member + 2 * (size_t)x + (op >> 1)];
+            } else if (v >= n_cell + n_sp && v < n_items) {
+                ce[u] = P.C[v - n_cell - n_sp];
+            }
+        }
+        long long cc[kBatchApplyItems];
+        unsigned cf[kBatchApplyItems];
+        unsigned long long ck[kBatchApplyItems][2];
+#pragma unroll
+        for (unsigned u = 0; u < kBatchApplyItems; ++u) {
+            const unsigned v = base + u * S + g;
+            cc[u] = 0; cf[u] = 0; ck[u][0] = 0; ck[u][1] = 0;
+            if (v >= n_cell + n_sp && v < n_items) {
+                cf[u] = P.flag[ce[u].x];
+                cc[u] = P.cnt[ce[u].x];
+                ck[u][0] = K.key8[ce[u].y];
+                ck[u][1] = K.key8[ce[u].z];
+            }
+        }
+#pragma unroll
+        for (unsigned u = 0; u < kBatchApplyItems; ++u) {
+            const unsigned v = base + u * S + g;
+            if (v < n_cell) {
+                const unsigned j = v / per_member, r = v % per_member, x = r >> 2, op = r & 3;
+                const long long d = (long long)dv[u];
                 if (d && !in_S(x)) {
+                    const BatchMember& M = B.m[j];
                     const unsigned p = op <= 1 ? x : (op == 2 ? M.b : M.nw);
                     const unsigned q = op == 0 ? M.a : (op == 1 ? M.nw : x);
                     const bool inc = op & 1;
+                    const unsigned long long kp = K.key8[p], kq = K.key8[q];   // issued with the probe
                     long long c;
                     unsigned f;
                     const size_t s = pair_update(P, st, p, q, inc ? d : -d, inc, &c, &f);
-                    if (consider(s, p, q, c, f, inc)) { add = true; add_e = make_uint4((unsigned)s, p, q, 0u); }
+                    updated(s, p, q, c, f, inc, kp, kq);
                 }
             } else if (v < n_cell + n_sp) {
                 const unsigned sp = v - n_cell;
@@ -1450,16 +1442,14 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
                     if (p == M.nw) inc += (long long)L[2 * (size_t)q + 1];
                 }
                 if (!popped && (inc || dec)) {
+                    const unsigned long long kp = K.key8[p], kq = K.key8[q];
                     long long c;
                     unsigned f;
                     const size_t s = pair_update(P, st, p, q, inc - dec, inc != 0, &c, &f);
-                    if (consider(s, p, q, c, f, inc != 0)) { add = true; add_e = make_uint4((unsigned)s, p, q, 0u); }
+                    updated(s, p, q, c, f, inc != 0, kp, kq);
                 }
             } else if (v < n_items) {
-                const uint4 e = P.C[v - n_cell - n_sp];
-                const unsigned p = e.y, q = e.z;
-                const unsigned f = P.flag[e.x];
-                const long long c = P.cnt[e.x];
+                const unsigned p = ce[u].y, q = ce[u].z;
                 bool touched = false;
                 if (in_S(p) || in_S(q)) {   // does an item of this trip update the key?
                     for (int j = 0; j < k && !touched; ++j) {
@@ -1469,19 +1459,7 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
                         if ((p == M.b || p == M.nw) && L[2 * (size_t)q + 1] != 0) touched = true;
                     }
                 }
-                if (!touched && (f & kPresent)) cand = Cand{c, K.key8[p], K.key8[q], e.x, p, q};
-            }
-            if (cand_better(cand, best, K.pool, K.off, K.len)) best = cand;
-            {   // every present key >= T2 goes to the candidate list
-                const bool listed = cand.cnt != LLONG_MIN && cand.cnt >= T2;
-                const unsigned li = wave_append(listed, &bs->list_n);
-                if (listed && li < kListCap)
-                    list[li] = Partial{cand.cnt, cand.ka, cand.kb, cand.slot, cand.a, cand.b, 0};
-            }
-            const unsigned idx = wave_append(add, &st->nC);
-            if (add) {
-                if (idx < st->capC) P.C[idx] = add_e;
-                else atomicOr(&st->err, ERR_C_FULL);
+                if (!touched && (cf[u] & kPresent)) offer(Cand{cc[u], ck[u][0], ck[u][1], ce[u].x, p, q});
             }
         }
     }
@@ -1496,8 +1474,27 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
         for (int w = 1; w < (int)(kApplyBatchThreads / 64); ++w)
             if (cand_better(s_wave[w], best, K.pool, K.off, K.len)) best = s_wave[w];
         part[blockIdx.x] = Partial{best.cnt, best.ka, best.kb, best.slot, best.a, best.b, 0};
+        // the workgroup's list entries and C admissions: one reservation each
+        const unsigned nl = s_nl, nc = min(s_nc, kApplyCLds);
+        s_lbase = nl ? atomicAdd(&bs->list_n, nl) : 0u;
+        s_cbase = nc ? atomicAdd(&st->nC, nc) : 0u;
+    }
+    __syncthreads();
+    {
+        const unsigned nl = min(s_nl, kListCap), nc = min(s_nc, kApplyCLds);
+        const unsigned lb = s_lbase, cb = s_cbase;
+        if ((unsigned)tid < nl && lb + tid < kListCap) list[lb + tid] = s_lst[tid];
+        for (unsigned i = tid; i < nc; i += blockDim.x) {
+            if (cb + i < st->capC) P.C[cb + i] = s_cadd[i];
+            else atomicOr(&st->err, ERR_C_FULL);
+        }
     }
     if (pw0) probe_stamp(st, B.trip, 12);
+    if (blockIdx.x == gridDim.x - 1 && tid < k && B.m[tid].isnew) {   // the new tokens enter the dedupe map
+        const unsigned nw = B.m[tid].nw;
+        unsigned s = (unsigned)mix64(B.m[tid].hash) & K.map_mask;
+        while (atomicCAS(&K.map[s], 0u, nw + 1) != 0u) s = (s + 1) & K.map_mask;
+    }
     if (blockIdx.x == 0 && tid == 0) {
         st->nparts = gridDim.x;
         if (!scan_only) {   // finish the trip: k rounds done
@@ -1937,7 +1934,7 @@ class MergeLoop {
     DevBuf<unsigned long long> probe_;   // BPE355_PROBE stamps
     void report_probe();
     DevBuf<Partial> list_;       // the candidate list (every present key >= T2)
-    static constexpr unsigned kApplyBatchBlocks = 256;
+    static constexpr unsigned kApplyBatchBlocks = kApplyGrid;
     void reset_tags();
     void run_trips(bool timing, std::vector<hipEvent_t>& ev, double& k1_ms, double& k1_bytes,
                    long long& k1_launches);
@@ -2509,7 +2506,7 @@ template <class TokT>
 void MergeLoop<TokT>::report_probe() {
     std::vector<unsigned long long> pr(probe_.n);
     BPE_HIP(hipMemcpy(pr.data(), probe_.p, probe_.bytes(), hipMemcpyDeviceToHost));
-    const char* names[] = {"sel:insert", "sel:lists", "sel:meta", "sel:rule", "gap sel>merge", "merge:pop",
+    const char* names[] = {"sel:issue", "sel:p1+list+meta", "sel:rule", "sel:fill", "gap sel>merge", "merge:pop",
                            "merge:rewrite", "merge:flush", "gap merge>apply", "apply:clear", "apply:items",
                            "apply:blocktop", "apply:end", "gap apply>sel"};
     const int from[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13};
@@ -2528,6 +2525,33 @@ void MergeLoop<TokT>::report_probe() {
     }
     std::fprintf(stderr, "[bpe355 probe] %d sampled trips, mean us:", n);
     for (int i = 0; i < 13 && n; ++i) std::fprintf(stderr, " %s %.2f |", names[i], acc[i] / n);
+    std::fprintf(stderr, "\n");
+    // distribution of whole trips (select start -> apply end) and of the rewrite, by trip decile
+    std::vector<double> tot, rw;
+    std::vector<double> dec_tot(10, 0.0), dec_rw(10, 0.0);
+    std::vector<int> dec_n(10, 0);
+    const size_t nt = pr.size() / 16;
+    for (size_t t = 0; t < nt; ++t) {
+        const unsigned long long* p = &pr[16 * t];
+        bool ok = true;
+        for (int i = 0; i < 14; ++i) ok &= p[i] != 0;
+        if (!ok) continue;
+        const double a = (double)(p[13] - p[0]) * 0.01, b = (double)(p[7] - p[6]) * 0.01;
+        tot.push_back(a); rw.push_back(b);
+        const size_t d = t * 10 / nt;
+        dec_tot[d] += a; dec_rw[d] += b; dec_n[d]++;
+    }
+    auto pct = [](std::vector<double> v, double q) {
+        if (v.empty()) return 0.0;
+        std::sort(v.begin(), v.end());
+        return v[std::min(v.size() - 1, (size_t)(q * v.size()))];
+    };
+    std::fprintf(stderr, "[bpe355 probe] trip us p50 %.1f p90 %.1f p99 %.1f max %.1f | rewrite p50 %.1f p90 %.1f p99 %.1f max %.1f\n",
+                 pct(tot, 0.5), pct(tot, 0.9), pct(tot, 0.99), pct(tot, 1.0), pct(rw, 0.5), pct(rw, 0.9), pct(rw, 0.99),
+                 pct(rw, 1.0));
+    std::fprintf(stderr, "[bpe355 probe] by decile (trip/rewrite us):");
+    for (int d = 0; d < 10; ++d)
+        if (dec_n[d]) std::fprintf(stderr, " %.1f/%.1f", dec_tot[d] / dec_n[d], dec_rw[d] / dec_n[d]);
     std::fprintf(stderr, "\n");
 }
 
