@@ -1285,7 +1285,8 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
 // entries alone (after a rebuild of C).
 constexpr unsigned kBatchApplyItems = 4;
 constexpr unsigned kApplyBatchThreads = 256;
-constexpr unsigned kApplyCLds = 256;   // C admissions a workgroup stages in LDS (more: direct appends)
+constexpr unsigned kApplyCLds = 256;
+constexpr unsigned kSFilterWords = 128;   // C admissions a workgroup stages in LDS (more: direct appends)
 __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* __restrict__ st,
                                                                     BatchState* __restrict__ bs,
                                                                     const Batch* __restrict__ bt, PairsDev P, ToksDev K,
@@ -1294,6 +1295,8 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
                                                                     Partial* __restrict__ part,
                                                                     Partial* __restrict__ list, int scan_only) {
     __shared__ unsigned s_tok[3 * kMaxBatch];
+    __shared__ unsigned s_role[3 * kMaxBatch];   // S entry: member << 3 | roles (1 a, 2 b, 4 new)
+    __shared__ unsigned s_filt[kSFilterWords];   // bit (x mod 4096): x may be in S
     __shared__ int s_ns;
     __shared__ Cand s_wave[kApplyBatchThreads / 64];
     __shared__ Partial s_lst[kListCap];
@@ -1305,22 +1308,32 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     const int tid = threadIdx.x;
     const bool pw0 = !scan_only && blockIdx.x == 0 && tid == 0;
     if (pw0) probe_stamp(st, B.trip, 9);
-    if (tid == 0) {   // S, deduplicated (a == b is possible only when k == 1)
-        unsigned t[3 * kMaxBatch];
-#pragma unroll
-        for (int j = 0; j < kMaxBatch; ++j) {
-            t[3 * j] = B.m[j].a; t[3 * j + 1] = B.m[j].b; t[3 * j + 2] = B.m[j].nw;
+    if (tid < 64) {   // wave 0: S deduplicated (a == b is possible only when k == 1), lane i = entry i
+        static_assert(3 * kMaxBatch <= 64, "S fits one wave");
+        const int i = tid;
+        const bool have = i < 3 * k;
+        const unsigned ti = have ? (i % 3 == 0 ? B.m[i / 3].a : (i % 3 == 1 ? B.m[i / 3].b : B.m[i / 3].nw)) : ~0u;
+        bool dup = false;
+        unsigned roles = 0;   // members' tokens are disjoint for k > 1: one member per token
+        for (int j = 0; j < 3 * kMaxBatch; ++j) {
+            const unsigned tj = __builtin_amdgcn_readlane((int)ti, j);
+            dup |= j < i && tj == ti;
+            if (j < 3 * k && tj == ti) roles |= 1u << (j % 3);
         }
-        int ns = 0;
-#pragma unroll
-        for (int i = 0; i < 3 * kMaxBatch; ++i) {
-            bool dup = i >= 3 * k;
-            for (int u = 0; u < ns; ++u) dup |= s_tok[u] == t[i];
-            if (!dup) s_tok[ns++] = t[i];
+        const bool keep = have && !dup;
+        const unsigned long long km = __ballot(keep);
+        for (unsigned w = i; w < kSFilterWords; w += 64) s_filt[w] = 0;
+        if (keep) {
+            const unsigned pos = __builtin_amdgcn_mbcnt_hi((unsigned)(km >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)km, 0u));
+            s_tok[pos] = ti;
+            s_role[pos] = (unsigned)(i / 3) << 3 | roles;
+            atomicOr(&s_filt[(ti >> 5) % kSFilterWords], 1u << (ti & 31));
         }
-        s_ns = ns;
-        s_nl = 0;
-        s_nc = 0;
+        if (i == 0) {
+            s_ns = __popcll(km);
+            s_nl = 0;
+            s_nc = 0;
+        }
     }
     __syncthreads();
     const int ns = s_ns;
@@ -1341,11 +1354,13 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
             LRo[(size_t)(q / nprev) * lr_member + q % nprev] = 0;
     }
     if (pw0) probe_stamp(st, B.trip, 10);
-    auto in_S = [&](unsigned x) {
-        bool r = false;
-        for (int u = 0; u < ns; ++u) r |= s_tok[u] == x;
+    auto find_S = [&](unsigned x) -> int {   // x's entry in S, or -1
+        if (!((s_filt[(x >> 5) % kSFilterWords] >> (x & 31)) & 1u)) return -1;
+        int r = -1;
+        for (int u = 0; u < ns; ++u) r = s_tok[u] == x ? u : r;
         return r;
     };
+    auto in_S = [&](unsigned x) { return find_S(x) >= 0; };
     const long long T2 = bs->T2 < T ? T : bs->T2;
     Cand best = cand_none();   // this thread's best candidate (exact argmax)
     // a candidate for the list (>= T2) and for this thread's best
@@ -1430,17 +1445,16 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
             } else if (v < n_cell + n_sp) {
                 const unsigned sp = v - n_cell;
                 const unsigned p = s_tok[sp / ns], q = s_tok[sp % ns];
-                bool popped = false;
+                const unsigned rp = s_role[sp / ns], rq = s_role[sp % ns];
+                // q's member sees p on its left (cell 2p), p's member sees q on its right (2q + 1)
+                const unsigned long long lq = (rq & 5) ? LRc[(size_t)(rq >> 3) * lr_member + 2 * (size_t)p] : 0ull;
+                const unsigned long long lp = (rp & 6) ? LRc[(size_t)(rp >> 3) * lr_member + 2 * (size_t)q + 1] : 0ull;
+                const bool popped = (rp >> 3) == (rq >> 3) && (rp & 1) && (rq & 2);
                 long long inc = 0, dec = 0;
-                for (int j = 0; j < k; ++j) {
-                    const BatchMember& M = B.m[j];
-                    popped |= p == M.a && q == M.b;
-                    const unsigned long long* L = LRc + (size_t)j * lr_member;
-                    if (q == M.a) dec += (long long)L[2 * (size_t)p];
-                    if (q == M.nw) inc += (long long)L[2 * (size_t)p];
-                    if (p == M.b) dec += (long long)L[2 * (size_t)q + 1];
-                    if (p == M.nw) inc += (long long)L[2 * (size_t)q + 1];
-                }
+                if (rq & 1) dec += (long long)lq;
+                if (rq & 4) inc += (long long)lq;
+                if (rp & 2) dec += (long long)lp;
+                if (rp & 4) inc += (long long)lp;
                 if (!popped && (inc || dec)) {
                     const unsigned long long kp = K.key8[p], kq = K.key8[q];
                     long long c;
@@ -1451,13 +1465,11 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
             } else if (v < n_items) {
                 const unsigned p = ce[u].y, q = ce[u].z;
                 bool touched = false;
-                if (in_S(p) || in_S(q)) {   // does an item of this trip update the key?
-                    for (int j = 0; j < k && !touched; ++j) {
-                        const BatchMember& M = B.m[j];
-                        const unsigned long long* L = LRc + (size_t)j * lr_member;
-                        if ((q == M.a || q == M.nw) && L[2 * (size_t)p] != 0) touched = true;
-                        if ((p == M.b || p == M.nw) && L[2 * (size_t)q + 1] != 0) touched = true;
-                    }
+                {   // does an item of this trip update the key?
+                    const int ip = find_S(p), iq = find_S(q);
+                    const unsigned rp = ip >= 0 ? s_role[ip] : 0u, rq = iq >= 0 ? s_role[iq] : 0u;
+                    if ((rq & 5) && LRc[(size_t)(rq >> 3) * lr_member + 2 * (size_t)p] != 0) touched = true;
+                    if ((rp & 6) && LRc[(size_t)(rp >> 3) * lr_member + 2 * (size_t)q + 1] != 0) touched = true;
                 }
                 if (!touched && (cf[u] & kPresent)) offer(Cand{cc[u], ck[u][0], ck[u][1], ce[u].x, p, q});
             }
