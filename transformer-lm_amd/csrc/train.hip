@@ -790,9 +790,9 @@ __global__ void __launch_bounds__(256) k_argmax(RoundState* __restrict__ st, Pai
 // The rewrite applies the members in order to each word (the deltas of member j see the word
 // after members < j, as the reference's sequence of rounds does), so counts, present keys and
 // words after the trip equal the state after k rounds.
-constexpr int kMaxBatch = 8;
+constexpr int kMaxBatch = 16;
 constexpr int kTopM = kMaxBatch + 1;
-constexpr unsigned kLdsB = 256;          // LDS-summed cells per member (ids below kLdsB)
+constexpr unsigned kLdsB = 128;          // LDS-summed cells per member (ids below kLdsB)
 
 struct BatchMember {
     unsigned a, b, nw, slot;
@@ -825,8 +825,9 @@ struct BatchState {
     unsigned list_n;         // keys the apply appended to the list (> kListCap: overflow)
     unsigned pad;
     unsigned long long n_overflow, n_headmiss, n_short, k_hist[kMaxBatch + 1];   // diagnostics
+    unsigned long long k1_why[6];   // single-merge trips: P1 a == b / P1 not fresh / no list / P2 fails / tie / end
 };
-constexpr unsigned kListCap = 64;   // the candidate list k_select sorts (one wave)
+constexpr unsigned kListCap = 256;   // the candidate list k_select ranks (one thread per entry)
 constexpr unsigned kApplyGrid = 256;   // k_apply_batch workgroups (k_select reads one partial each)
 
 struct TokMetaS {
@@ -886,12 +887,13 @@ __device__ __forceinline__ void cand_meta(const Cand& c, const ToksDev& K, const
 }
 
 // One workgroup: the batch of this trip.  Waves 0-3 reduce the apply's per-workgroup partials
-// to the exact best candidate P1; wave 4 ranks the candidate list (every present key >= T2) and
-// looks up its entries' metadata; thread 0 has loaded the scalars meanwhile.  All global loads
-// are issued before the first barrier, so the kernel costs about one memory round trip plus the
-// dedupe lookups' chain, then the rule (thread 0) and the record (one thread per member).
-constexpr int kSelThreads = 320;
-constexpr int kSelListWave = 4;
+// to the exact best candidate P1; waves 4-7 hold the candidate list (every present key >= T2),
+// look up its entries' metadata and rank them.  All global loads are issued before the first
+// barrier, so the kernel costs about one memory round trip plus the dedupe lookups' chain, then
+// the ranking, the rule and the record (wave 0).
+constexpr int kSelListWave = 4;   // first wave of the list
+constexpr unsigned kListTarget = 48;   // keys the next list should hold (T2 control)
+constexpr int kSelThreads = 64 * kSelListWave + (int)kListCap;
 __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__ st, BatchState* __restrict__ bs,
                                                         PairsDev P, ToksDev K, IndexDev X, Batch* __restrict__ bt,
                                                         const Partial* __restrict__ part,
@@ -902,8 +904,10 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
                                                         int trip_slot) {
     static_assert(kApplyGrid <= 64 * kSelListWave, "one partial per thread of waves 0-3");
     __shared__ Cand s_wave[kSelListWave];
+    __shared__ Cand s_all[kListCap];
     __shared__ Cand s_list[kTopM];
-    __shared__ long long s_rankcnt[kListCap];
+    __shared__ long long s_cnt[kListCap];
+    __shared__ long long s_cnt_target, s_cnt_last;   // counts at sorted positions kListTarget - 1, ln - 1
     __shared__ unsigned s_nw_old[kTopM];
     __shared__ TokMetaS s_meta[kTopM];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -913,7 +917,8 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     Partial q{};
     if (wv < kSelListWave) q = part[tid];   // the buffer holds kApplyBatchBlocks entries
     Partial lq{};
-    if (wv == kSelListWave) lq = list[lane];
+    const int li = tid - 64 * kSelListWave;   // list entry of this thread (>= 0: list waves)
+    if (li >= 0) lq = list[li];
     const int nparts = st->nparts;
     const unsigned ln = bs->list_n;
     if (tid == 0) probe_stamp(st, ptrip, 1);
@@ -925,27 +930,49 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
             if (cand_better(oc, best, K.pool, K.off, K.len)) best = oc;
         }
         if (lane == 0) s_wave[wv] = best;
-    } else if (wv == kSelListWave) {   // the list: metadata of every entry, then its rank
-        if (lane < kTopM) s_list[lane] = cand_none();
-        const bool usable = ln <= kListCap;
-        const int nl = usable ? (int)ln : 0;
-        const bool have = lane < nl;
-        const Cand x = have ? Cand{lq.cnt, lq.ka, lq.kb, lq.slot, lq.a, lq.b} : cand_none();
-        TokMetaS m{};
-        unsigned old = ~0u;
-        if (have) cand_meta(x, K, X, m, old);
-        int rank = 0;
-        for (int j = 0; j < nl; ++j) {
-            const Cand y = readlane_cand(x, j);
-            rank += cand_better(y, x, K.pool, K.off, K.len) ? 1 : 0;
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (have && rank < kTopM) {
+    }
+    // the list: each entry's rank among the entries, then the metadata of the top kTopM
+    const int nl = ln <= kListCap ? (int)ln : 0;
+    const bool have = li >= 0 && li < nl;
+    const Cand x = have ? Cand{lq.cnt, lq.ka, lq.kb, lq.slot, lq.a, lq.b} : cand_none();
+    if (li >= 0) {
+        if (li < kTopM) s_list[li] = cand_none();
+        if (li == 0) { s_cnt_target = LLONG_MAX; s_cnt_last = LLONG_MAX; }
+        s_all[li] = x;
+        s_cnt[li] = x.cnt;
+    }
+    __syncthreads();
+    long long tgt = LLONG_MAX, last = LLONG_MAX;
+    if (have) {
+        // rank by count first (cheap); the full order only among equal counts near the top
+        int rc = 0;
+#pragma unroll 8
+        for (int j = 0; j < nl; ++j) rc += s_cnt[j] > x.cnt ? 1 : 0;
+        int rank = rc;
+        if (rc < kTopM)
+            for (int j = 0; j < nl; ++j)
+                rank += (s_cnt[j] == x.cnt && j != li && cand_better(s_all[j], x, K.pool, K.off, K.len)) ? 1 : 0;
+        if (rank < kTopM) {
+            TokMetaS lm;
+            unsigned lold;
+            cand_meta(x, K, X, lm, lold);
             s_list[rank] = x;
-            s_meta[rank] = m;
-            s_nw_old[rank] = old;
+            s_meta[rank] = lm;
+            s_nw_old[rank] = lold;
         }
-        if (have) s_rankcnt[rank] = x.cnt;
+        // the count at sorted position t is the least count whose first position is <= t
+        tgt = rc <= (int)kListTarget - 1 ? x.cnt : LLONG_MAX;
+        last = x.cnt;
+    }
+    if (li >= 0) {   // wave minima, then one LDS atomic per wave
+        for (int o = 32; o > 0; o >>= 1) {
+            tgt = min(tgt, (long long)__shfl_xor(tgt, o));
+            last = min(last, (long long)__shfl_xor(last, o));
+        }
+        if (lane == 0 && last != LLONG_MAX) {
+            atomicMin(&s_cnt_target, tgt);
+            atomicMin(&s_cnt_last, last);
+        }
     }
     __syncthreads();
     if (tid == 0) probe_stamp(st, ptrip, 2);
@@ -1035,6 +1062,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     const bool okb = i >= 1 && i < nf && e.cnt >= T && e.a != e.b && fr && !clash;
     int k = __builtin_ctzll(~(__ballot(okb) | 1ull));
     k = min(k, min(maxb, nf));
+    const int k_rule = k;
     if (!(p1.a != p1.b && __builtin_amdgcn_readlane((int)fr, 0))) k = 1;
     // (4) strictly above the next candidate: listed (candidate k), or unlisted (below T2, and
     // every member is listed, so >= T2): the largest k' <= k with that gap
@@ -1043,6 +1071,11 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         const unsigned long long gm =
             __ballot(i >= 1 && (i >= nf || cprev > e.cnt)) & ((2ull << k) - 1) & ~1ull;
         k = gm ? 63 - __builtin_clzll(gm) : 1;
+    }
+    const bool fr0 = __builtin_amdgcn_readlane((int)fr, 0);
+    if (k == 1 && lane == 0) {
+        const int why = p1.a == p1.b ? 0 : !fr0 ? 1 : nf == 1 ? 2 : k_rule == 1 ? 3 : 4;
+        atomicAdd(&bs->k1_why[why], 1ull);
     }
     k = min(k, n_rounds - round);
     // per member: pool offset, new id, posting-list prefix (exclusive scans over lanes < k)
@@ -1098,13 +1131,12 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         {   // the next list: about kListTarget keys.  With the list ranked, T2 = the count of the
             // kListTarget-th best (this trip pops at most kMaxBatch of those above it); on overflow
             // raise T2 halfway to the top; with too few keys, extend the range below the last one
-            constexpr unsigned kListTarget = 24;
             const long long top = p1.cnt;
             const long long t2 = T2old < T ? T : T2old;
             long long nt;
             if (ln > kListCap) nt = t2 + (top - t2) / 2;
-            else if (ln >= kListTarget) nt = s_rankcnt[kListTarget - 1];
-            else if (ln > 0) nt = s_rankcnt[ln - 1] - (top - s_rankcnt[ln - 1]) - 1;
+            else if (ln >= kListTarget) nt = s_cnt_target;
+            else if (ln > 0) nt = s_cnt_last - (top - s_cnt_last) - 1;
             else nt = T;
             bs->T2 = nt < T ? T : (nt > top ? top : nt);
             bs->list_n = 0;   // the apply of this trip fills it again
@@ -1366,14 +1398,14 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     // a candidate for the list (>= T2) and for this thread's best
     auto offer = [&](const Cand& c) {
         if (cand_better(c, best, K.pool, K.off, K.len)) best = c;
-        if (c.cnt != LLONG_MIN && c.cnt >= T2) {
-            const unsigned li = atomicAdd(&s_nl, 1u);
-            if (li < kListCap) s_lst[li] = Partial{c.cnt, c.ka, c.kb, c.slot, c.a, c.b, 0};
-        }
+        const bool listed = c.cnt != LLONG_MIN && c.cnt >= T2;
+        const unsigned li = wave_append(listed, &s_nl);   // one LDS atomic per wave
+        if (listed && li < kListCap) s_lst[li] = Partial{c.cnt, c.ka, c.kb, c.slot, c.a, c.b, 0};
     };
     // an increment across T admits the key to C
-    auto admit = [&](size_t s, unsigned p, unsigned q) {
-        const unsigned ci = atomicAdd(&s_nc, 1u);
+    auto admit = [&](bool pred, size_t s, unsigned p, unsigned q) {
+        const unsigned ci = wave_append(pred, &s_nc);
+        if (!pred) return;
         if (ci < kApplyCLds) {
             s_cadd[ci] = make_uint4((unsigned)s, p, q, 0u);
         } else {
@@ -1387,10 +1419,9 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
                        unsigned long long kp, unsigned long long kq) {
         if (s == ~(size_t)0 || !(f & kPresent) || c < T) return;
         offer(Cand{c, kp, kq, (unsigned)s, p, q});
-        if (inc && !(f & kInC)) {
-            P.flag[s] = f | kInC;
-            admit(s, p, q);
-        }
+        const bool adm = inc && !(f & kInC);
+        if (adm) P.flag[s] = f | kInC;
+        admit(adm, s, p, q);
     };
     // step u of a pass takes items base + u * S + g: a wave's 64 items are contiguous (coalesced)
     // and its steps far apart, so the dense start of each member's cells (the byte tokens, which
@@ -2479,7 +2510,8 @@ void MergeLoop<TokT>::run() {
             std::fprintf(stderr, "[bpe355] trips: list overflow %llu, head miss %llu, short %llu; k:", b.n_overflow,
                          b.n_headmiss, b.n_short);
             for (int i = 0; i <= kMaxBatch; ++i) std::fprintf(stderr, " %llu", b.k_hist[i]);
-            std::fprintf(stderr, "\n");
+            std::fprintf(stderr, "; k=1 because: a==b %llu, not fresh %llu, no list %llu, P2 fails %llu, tie %llu\n",
+                         b.k1_why[0], b.k1_why[1], b.k1_why[2], b.k1_why[3], b.k1_why[4]);
         }
     }
     out_.stats.merge_kernel_ms = k1_ms;
