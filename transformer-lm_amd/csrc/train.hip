@@ -286,11 +286,12 @@ constexpr unsigned kLdsLR = 512;
 
 // (Applying the four pair updates of a cell inside the merge kernel instead was measured
 // slower: one hit's updates form a serial chain on one thread; see DESIGN.md.)
+typedef __attribute__((address_space(3))) unsigned long long LdsU64;   // an LDS cell
 struct DeltaSink {
     unsigned long long* LR;     // global delta cells (all-reduced when sharded) for k_apply
-    unsigned long long* lds;
+    LdsU64* lds;
     __device__ __forceinline__ void add(unsigned cell, unsigned long long c) const {
-        if (cell < 2 * kLdsLR) atomicAdd(&lds[cell], c);
+        if (cell < 2 * kLdsLR) __hip_atomic_fetch_add(&lds[cell], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         else atomicAdd(&LR[cell], c);
     }
 };
@@ -313,6 +314,39 @@ __device__ __forceinline__ uint32_t rewrite_word(TokT* __restrict__ t, uint32_t 
     }
     if (pad)
         for (uint32_t k = j; k < len; ++k) t[k] = sentinel<TokT>();
+    return j;
+}
+
+// rewrite_word for a slot word already in registers (e: the slot, e[0] = length, sentinel-padded):
+// the matches are found on the registers (every index a compile-time constant), so the only
+// memory traffic is the stores of the shifted tail, not a load per token
+template <class TokT, int W, class Sink>
+__device__ __forceinline__ uint32_t rewrite_slot(const TokT (&e)[W], TokT* __restrict__ s, TokT a, TokT b,
+                                                 TokT nw, unsigned long long c, const Sink& D) {
+    const TokT sent = sentinel<TokT>();
+    uint32_t j = 0;      // output tokens so far
+    TokT prev = sent;    // the last output token
+    bool skip = false;   // this position is the b of the previous match
+#pragma unroll
+    for (int q = 1; q < W; ++q) {
+        const TokT x = e[q];
+        if (x == sent) break;
+        if (skip) { skip = false; continue; }
+        if (q + 1 < W && x == a && e[q + 1 < W ? q + 1 : q] == b) {
+            if (j > 0) D.add(2u * (unsigned)prev, c);                      // (x,a)-=c, (x,new)+=c
+            if (q + 2 < W && e[q + 2 < W ? q + 2 : q] != sent)
+                D.add(2u * (unsigned)e[q + 2 < W ? q + 2 : q] + 1, c);     // (b,y)-=c, (new,y)+=c
+            s[1 + j] = nw;
+            prev = nw;
+            skip = true;
+        } else {
+            if (j != (uint32_t)(q - 1)) s[1 + j] = x;
+            prev = x;
+        }
+        ++j;
+    }
+    for (uint32_t p = j; p < (uint32_t)e[0]; ++p) s[1 + p] = sent;
+    s[0] = (TokT)j;
     return j;
 }
 
@@ -343,10 +377,7 @@ __device__ __forceinline__ void scan_class(const SlotCls<TokT>& S, unsigned bi, 
 #pragma unroll
             for (int k = 1; k + 1 < W; ++k) hit |= (e[k] == a) & (e[k + 1] == b);
             if (hit) {
-                TokT* s = S.slot + (size_t)i * W;
-                const uint32_t len = e[0];
-                const uint32_t j = rewrite_word(s + 1, len, a, b, nw, S.cnt[i], D, true);
-                s[0] = (TokT)j;
+                const uint32_t j = rewrite_slot(e, S.slot + (size_t)i * W, a, b, nw, S.cnt[i], D);
                 singles += (j < 2);
             }
         }
@@ -369,9 +400,7 @@ __device__ __forceinline__ void merge_one(const SlotCls<TokT>& S, unsigned i, To
 #pragma unroll
     for (int k = 1; k + 1 < W; ++k) hit |= (e[k] == a) & (e[k + 1] == b);
     if (hit) {
-        TokT* s = S.slot + (size_t)i * W;
-        const uint32_t j = rewrite_word(s + 1, e[0], a, b, nw, c, D, true);
-        s[0] = (TokT)j;
+        const uint32_t j = rewrite_slot(e, S.slot + (size_t)i * W, a, b, nw, c, D);
         singles += (j < 2);
     }
 }
@@ -530,7 +559,7 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
     unsigned singles = 0;
     const unsigned bid = blockIdx.x;
     const TokT ta = (TokT)a, tb = (TokT)b, tn = (TokT)nw;
-    const DeltaSink D{LR, l_lr};
+    const DeltaSink D{LR, (LdsU64*)l_lr};
     if (sb.use_list && bid < W.lblk0) {
         // index mode: only the words on the posting list (a gather of their slots)
         const uint32_t* L = X.list + sb.list_beg;
@@ -838,9 +867,9 @@ struct TokMetaS {
 template <unsigned N>
 struct DeltaSinkN {
     unsigned long long* LR;     // this member's global cells
-    unsigned long long* lds;    // this member's LDS cells (ids below N)
+    LdsU64* lds;                // this member's LDS cells (ids below N)
     __device__ __forceinline__ void add(unsigned cell, unsigned long long c) const {
-        if (cell < 2 * N) atomicAdd(&lds[cell], c);
+        if (cell < 2 * N) __hip_atomic_fetch_add(&lds[cell], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         else atomicAdd(&LR[cell], c);
     }
 };
@@ -1152,13 +1181,16 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     }
 }
 
+typedef __attribute__((address_space(3))) unsigned LdsU32;   // an LDS word (explicit address space)
+
 // the slot word of class C addressed directly, every member applied in order.  claim: the word
 // (global slot index f) may be on several members' lists; the first thread to claim it rewrites
 // it.  The word is loaded before the claim: only the claimant writes it during this batch.
 template <class TokT, int C>
 __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigned i, const Batch& B,
                                                  unsigned long long* LRt, size_t lr_member,
-                                                 unsigned long long* lds, unsigned& singles,
+                                                 unsigned long long* lds, const LdsU32* sm_a,
+                                                 const LdsU32* sm_b, const LdsU32* sm_n, unsigned& singles,
                                                  uint32_t* tags = nullptr, unsigned f = 0) {
     constexpr int W = slot_w(C);
     constexpr int V = W * (int)sizeof(TokT) / 16;
@@ -1170,20 +1202,29 @@ __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigne
     if (tags && atomicMax(&tags[f], B.batch_id) >= B.batch_id) return;
     TokT e[W];
     __builtin_memcpy(e, r, sizeof(e));
+    // the members this word holds: members' tokens are disjoint and their new tokens fresh, so a
+    // rewrite neither makes nor breaks another member's pair and the original word decides
+    unsigned hits = 0;
     for (int j = 0; j < B.k; ++j) {
-        const TokT ta = (TokT)B.m[j].a, tb = (TokT)B.m[j].b;
+        const TokT ta = (TokT)sm_a[j], tb = (TokT)sm_b[j];
         bool hit = false;
 #pragma unroll
         for (int q = 1; q + 1 < W; ++q) hit |= (e[q] == ta) & (e[q + 1] == tb);
-        if (!hit) continue;
-        // rewrite in memory; the next member tests the rewritten word (this thread's own stores)
-        const DeltaSinkN<kLdsB> D{LRt + (size_t)j * lr_member, lds + 2 * kLdsB * j};
-        const uint32_t nl = rewrite_word(s + 1, (uint32_t)e[0], ta, tb, (TokT)B.m[j].nw, c, D, true);
-        s[0] = (TokT)nl;
-        if (nl < 2) { ++singles; break; }
+        hits |= (unsigned)hit << j;
+    }
+    bool first = true;
+    while (hits) {
+        const int j = __builtin_ctz(hits);
+        hits &= hits - 1;
+        if (!first) {   // a second member: the word as rewritten (this thread's own stores)
 #pragma unroll
-        for (int v = 0; v < V; ++v) r[v] = reinterpret_cast<const uint4*>(s)[v];
-        __builtin_memcpy(e, r, sizeof(e));
+            for (int v = 0; v < V; ++v) r[v] = reinterpret_cast<const uint4*>(s)[v];
+            __builtin_memcpy(e, r, sizeof(e));
+        }
+        first = false;
+        const DeltaSinkN<kLdsB> D{LRt + (size_t)j * lr_member, (LdsU64*)(lds + 2 * kLdsB * j)};
+        const uint32_t nl = rewrite_slot(e, s, (TokT)sm_a[j], (TokT)sm_b[j], (TokT)sm_n[j], c, D);
+        if (nl < 2) { ++singles; break; }
     }
 }
 
@@ -1193,10 +1234,12 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
                                                      unsigned long long* __restrict__ LRbase, size_t lr_member,
                                                      size_t lr_parity, uint32_t* __restrict__ tags) {
     __shared__ unsigned long long l_lr[2 * kLdsB * kMaxBatch];
+    __shared__ unsigned s_ma[kMaxBatch], s_mb[kMaxBatch], s_mn[kMaxBatch];   // the members' tokens
     const int tid = threadIdx.x;
     const Batch& B = *bt;
     if (B.stop) return;
     const int k = B.k;
+    if (tid < k) { s_ma[tid] = B.m[tid].a; s_mb[tid] = B.m[tid].b; s_mn[tid] = B.m[tid].nw; }
     if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 5);
     for (unsigned q = tid; q < 2 * kLdsB * (unsigned)k; q += blockDim.x) l_lr[q] = 0;
     unsigned long long* LRt = LRbase + (size_t)(B.trip & 1) * lr_parity;   // member j at + j * lr_member
@@ -1231,7 +1274,7 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
         // one member: the per-round rewrite (index list or a scan of every slot)
         const BatchMember& M = B.m[0];
         const TokT ta = (TokT)M.a, tb = (TokT)M.b, tn = (TokT)M.nw;
-        const DeltaSinkN<kLdsB> D{LRt, l_lr};
+        const DeltaSinkN<kLdsB> D{LRt, (LdsU64*)l_lr};
         if (M.use_list && bid < W.lblk0) {
             const uint32_t* L = X.list + M.list_beg;
             for (unsigned i = bid * blockDim.x + tid; i < M.list_len; i += W.lblk0 * blockDim.x) {
@@ -1258,10 +1301,10 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
         if (B.full_scan) {
             const unsigned total = W.off[kNumCls];
             for (unsigned f = bid * blockDim.x + tid; f < total; f += W.lblk0 * blockDim.x) {
-                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f, B, LRt, lr_member, l_lr, singles);
-                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1], B, LRt, lr_member, l_lr, singles);
-                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2], B, LRt, lr_member, l_lr, singles);
-                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3], B, LRt, lr_member, l_lr, singles);
+                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f,  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles);
+                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles);
+                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles);
+                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles);
             }
         } else {
             const unsigned total = B.list_pre[k];
@@ -1270,10 +1313,10 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
                 while (j + 1 < k && i >= B.list_pre[j + 1]) ++j;
                 const unsigned f = X.list[B.m[j].list_beg + (i - B.list_pre[j])];
                 // a word on several members' lists is rewritten by the first thread to claim it
-                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f, B, LRt, lr_member, l_lr, singles, tags, f);
-                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1], B, LRt, lr_member, l_lr, singles, tags, f);
-                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2], B, LRt, lr_member, l_lr, singles, tags, f);
-                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3], B, LRt, lr_member, l_lr, singles, tags, f);
+                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f,  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles, tags, f);
+                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles, tags, f);
+                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles, tags, f);
+                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles, tags, f);
             }
         }
     }
@@ -1287,7 +1330,7 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
                 bool hit = false;
                 for (uint32_t q = 0; q + 1 < len && !hit; ++q) hit = (t[q] == ta) & (t[q + 1] == tb);
                 if (!hit) continue;
-                const DeltaSinkN<kLdsB> D{LRt + (size_t)j * lr_member, l_lr + 2 * kLdsB * j};
+                const DeltaSinkN<kLdsB> D{LRt + (size_t)j * lr_member, (LdsU64*)(l_lr + 2 * kLdsB * j)};
                 len = rewrite_word(t, len, ta, tb, (TokT)B.m[j].nw, W.lcnt[i], D, false);
                 W.llen[i] = len;
                 singles += (len < 2);
