@@ -922,6 +922,7 @@ __device__ __forceinline__ void cand_meta(const Cand& c, const ToksDev& K, const
 // the ranking, the rule and the record (wave 0).
 constexpr int kSelListWave = 4;   // first wave of the list
 constexpr unsigned kListTarget = 48;   // keys the next list should hold (T2 control)
+constexpr bool kSelMetaAll = true;     // metadata of every listed key before the ranking
 constexpr int kSelThreads = 64 * kSelListWave + (int)kListCap;
 __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__ st, BatchState* __restrict__ bs,
                                                         PairsDev P, ToksDev K, IndexDev X, Batch* __restrict__ bt,
@@ -950,6 +951,18 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     if (li >= 0) lq = list[li];
     const int nparts = st->nparts;
     const unsigned ln = bs->list_n;
+    // the rule's scalars (uniform: scalar loads, in flight with the vector loads above)
+    const int halt = st->halt, round = st->round, n_rounds = st->n_rounds, host_round = st->host_round;
+    const unsigned nC = st->nC, c_limit = st->c_limit;
+    const long long T = st->T;
+    const unsigned n_single = st->n_single, single_limit = st->single_limit;
+    const unsigned long long pair_used = st->pair_used, pair_limit = st->pair_limit;
+    const unsigned pool_used = st->pool_used, pool_cap = st->pool_cap;
+    const unsigned max_len = st->max_len;
+    const int ntok = st->ntok, max_batch = st->max_batch;
+    const int prev_k = bs->prev_k;
+    const unsigned bid = bs->batch_seq + 1;
+    const long long T2old = bs->T2;
     if (tid == 0) probe_stamp(st, ptrip, 1);
     if (wv < kSelListWave) {   // P1: the exact best over the partials
         Cand best = cand_none();
@@ -964,11 +977,14 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     const int nl = ln <= kListCap ? (int)ln : 0;
     const bool have = li >= 0 && li < nl;
     const Cand x = have ? Cand{lq.cnt, lq.ka, lq.kb, lq.slot, lq.a, lq.b} : cand_none();
+    TokMetaS lm{};
+    unsigned lold = ~0u;
     if (li >= 0) {
         if (li < kTopM) s_list[li] = cand_none();
         if (li == 0) { s_cnt_target = LLONG_MAX; s_cnt_last = LLONG_MAX; }
         s_all[li] = x;
         s_cnt[li] = x.cnt;
+        if (have && kSelMetaAll) cand_meta(x, K, X, lm, lold);   // overlaps the partials' reduction
     }
     __syncthreads();
     long long tgt = LLONG_MAX, last = LLONG_MAX;
@@ -982,9 +998,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
             for (int j = 0; j < nl; ++j)
                 rank += (s_cnt[j] == x.cnt && j != li && cand_better(s_all[j], x, K.pool, K.off, K.len)) ? 1 : 0;
         if (rank < kTopM) {
-            TokMetaS lm;
-            unsigned lold;
-            cand_meta(x, K, X, lm, lold);
+            if (!kSelMetaAll) cand_meta(x, K, X, lm, lold);
             s_list[rank] = x;
             s_meta[rank] = lm;
             s_nw_old[rank] = lold;
@@ -1007,17 +1021,6 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     if (tid == 0) probe_stamp(st, ptrip, 2);
     if (wv != 0) return;
     // ---- wave 0: the rule and the record, lane i holding candidate i (no workgroup barrier)
-    const int halt = st->halt, round = st->round, n_rounds = st->n_rounds, host_round = st->host_round;
-    const unsigned nC = st->nC, c_limit = st->c_limit;
-    const long long T = st->T;
-    const unsigned n_single = st->n_single, single_limit = st->single_limit;
-    const unsigned long long pair_used = st->pair_used, pair_limit = st->pair_limit;
-    const unsigned pool_used = st->pool_used, pool_cap = st->pool_cap;
-    const unsigned max_len = st->max_len;
-    const int ntok = st->ntok, max_batch = st->max_batch;
-    const int prev_k = bs->prev_k;
-    const unsigned bid = bs->batch_seq + 1;
-    const long long T2old = bs->T2;
     Cand p1 = s_wave[0];
     for (int w = 1; w < kSelListWave; ++w)
         if (cand_better(s_wave[w], p1, K.pool, K.off, K.len)) p1 = s_wave[w];
@@ -1119,7 +1122,8 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         const unsigned uj = __builtin_amdgcn_readlane((int)add_list, j);
         if (j < i) { pre_pool += pj; pre_fresh += fj; pre_list += uj; }
     }
-    const bool full = __ballot(mem && !use) != 0;
+    // one scan of every word once the members' lists together pass the scan threshold
+    const bool full = __ballot(mem && !use) != 0 || __builtin_amdgcn_readlane((int)pre_list, k) > (int)X.full_threshold;
     const unsigned tot_pool = __builtin_amdgcn_readlane((int)pre_pool, k);
     const unsigned tot_fresh = __builtin_amdgcn_readlane((int)pre_fresh, k);
     Batch& B = *bt;
@@ -2180,7 +2184,11 @@ void MergeLoop<TokT>::build_index() {
     }
     BPE_HIP(hipGetLastError());
     BPE_HIP(hipStreamSynchronize(s_));
-    idev_ = IndexDev{ilist_.p, ibeg_.p, ilen_.p, n / 6, n};
+    static const unsigned full_div = [] {
+        const char* e = std::getenv("BPE355_FULL_DIV");   // experiment knob: scan when lists > n / div
+        return e ? (unsigned)std::max(1, std::atoi(e)) : 6u;
+    }();
+    idev_ = IndexDev{ilist_.p, ibeg_.p, ilen_.p, n / full_div, n};
     out_.stats.n_index_builds++;
 }
 
@@ -2213,6 +2221,9 @@ void MergeLoop<TokT>::layout_blocks() {
     blk += W.lnblk;
     merge_grid_ = std::max(blk, (unsigned)kMaxBatch);   // k_merge_batch: block j registers member j
     wdev_ = W;
+    if (std::getenv("BPE355_TRACE"))
+        std::fprintf(stderr, "[bpe355] words per slot class: %u %u %u %u, long %u (%llu ids); merge grid %u\n", W.c[0].n,
+                     W.c[1].n, W.c[2].n, W.c[3].n, W.ln, (unsigned long long)long_tokens_, merge_grid_);
     // algorithmic bytes of one k_merge launch: every slot, and every long word's ids + length
     scan_bytes_ = 0;
     for (int c = 0; c < kNumCls; ++c) scan_bytes_ += (double)W.c[c].n * slot_w(c) * sizeof(TokT);
