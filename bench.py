@@ -123,11 +123,15 @@ def main():
     k_count_bytes = sum(s["count_kernel_bytes"] for s in stats)
     roofline = None
     if k_merge_ms > 0 or k_count_ms > 0:
-        # k_merge is event-timed on a 1-in-8 sample of its launches: compare per-step estimates
-        merge_step_ms = k_merge_ms / max(1, k_merge_launch) * rounds
+        # the merge kernel is event-timed on a sample of its launches: compare per-step
+        # estimates (one launch per trip when rounds are batched, else one per round)
+        trips = sum(s.get("n_trips", 0) for s in stats) / len(stats)
+        merge_launches = trips if trips > 0 else rounds
+        merge_step_ms = k_merge_ms / max(1, k_merge_launch) * merge_launches
         count_step_ms = k_count_ms / len(stats)
         if merge_step_ms >= count_step_ms:
-            kname, kms, kb, kl = "k_merge", k_merge_ms, k_merge_bytes, k_merge_launch
+            kname = "k_merge_batch" if trips > 0 else "k_merge"
+            kms, kb, kl = k_merge_ms, k_merge_bytes, k_merge_launch
         else:
             kname, kms, kb, kl = "k_count_words", k_count_ms, k_count_bytes, len(stats)
         achieved = kb / (kms / 1e3) / 1e9
@@ -138,7 +142,7 @@ def main():
         roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "kernel": kname,
-                    "launches_per_step": rounds if kname == "k_merge" else 1,
+                    "launches_per_step": round(merge_launches) if kname != "k_count_words" else 1,
                     "timed_launches": kl,
                     "avg_launch_us": round(kms / kl * 1e3, 3),
                     "bytes_per_launch": kb / kl}
