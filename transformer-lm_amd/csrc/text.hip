@@ -152,7 +152,8 @@ __device__ __forceinline__ bool global_add(const uint8_t* __restrict__ s, const 
     return ins;
 }
 
-constexpr int kCache = 1024;         // LDS word-cache entries (2-way)
+constexpr int kCache = 1024;         // LDS word-cache entries
+constexpr int kWays = 2;             // associativity (a set is kWays adjacent entries)
 constexpr int kEpoch = 4;            // chunks between cache evictions
 constexpr unsigned kKeep = 2;        // an entry stays if it was hit this often in the epoch
 
@@ -199,9 +200,9 @@ __global__ void __launch_bounds__(256, 3) k_count_words(const uint8_t* __restric
                 else wh |= b << (8 * (i - 8));
             }
             const uint64_t h = short_hash(wl, wh, len);
-            const unsigned ls = (unsigned)(h >> 40) & (kCache - 2);
+            const unsigned ls = (unsigned)(h >> 40) & (kCache - kWays);
             const unsigned long long mine = ((unsigned long long)len << 40) | (gpos + 1);
-            for (int way = 0; way < 2; ++way) {
+            for (int way = 0; way < kWays; ++way) {
                 const unsigned sl = ls + way;
                 unsigned long long k = c_key[sl];
                 if (k == 0) {

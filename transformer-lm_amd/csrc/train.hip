@@ -1102,7 +1102,37 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         const long long cprev = __shfl(e.cnt, i > 0 ? i - 1 : 0);
         const unsigned long long gm =
             __ballot(i >= 1 && (i >= nf || cprev > e.cnt)) & ((2ull << k) - 1) & ~1ull;
-        k = gm ? 63 - __builtin_clzll(gm) : 1;
+        const int k_strict = gm ? 63 - __builtin_clzll(gm) : 1;
+        // (4') a tie at the boundary is harmless unless a tied non-member could seed a new pair:
+        // a pair created by the batch has at most the count of the old pair (x, a_j) or (b_j, y)
+        // it replaces, so with every tied non-member free of those shapes, no new pair reaches
+        // count(Pk).  Every key >= T2 is listed, so the tied keys are all in s_all.
+        if (k_strict < k && k > 1) {
+            const long long c = readlane64((unsigned long long)e.cnt, k - 1);
+            unsigned ma[kMaxBatch], mb[kMaxBatch], ms[kMaxBatch];
+#pragma unroll
+            for (int j = 0; j < kMaxBatch; ++j) {
+                ma[j] = __builtin_amdgcn_readlane((int)e.a, j);
+                mb[j] = __builtin_amdgcn_readlane((int)e.b, j);
+                ms[j] = __builtin_amdgcn_readlane((int)e.slot, j);
+            }
+            bool bad = false;
+            for (int t = lane; t < nl; t += 64) {
+                const Cand q = s_all[t];
+                if (q.cnt != c) continue;
+                bool member = false, seeds = false;
+#pragma unroll
+                for (int j = 0; j < kMaxBatch; ++j) {
+                    if (j >= k) break;
+                    member |= q.slot == ms[j];
+                    seeds |= q.b == ma[j] || q.a == mb[j];
+                }
+                bad |= !member && seeds;
+            }
+            k = __ballot(bad) ? k_strict : k;
+        } else {
+            k = k_strict;
+        }
     }
     const bool fr0 = __builtin_amdgcn_readlane((int)fr, 0);
     if (k == 1 && lane == 0) {
@@ -1950,7 +1980,7 @@ class MergeLoop {
 
    private:
     static constexpr int kBatch = 64;
-    static constexpr int kTrips = 64;   // batched mode: [k_select][k_merge_batch][k_apply_batch] per host sync
+    static constexpr int kTrips = 32;   // batched mode: [k_select][k_merge_batch][k_apply_batch] per host sync
     static constexpr int kArgBlocks = 64;
     static constexpr unsigned kCScanBlocks = 64;   // k_apply_argmax workgroups scanning C
     unsigned nparts_ = 0;                          // argmax partials the next k_merge reduces
