@@ -1756,54 +1756,128 @@ struct MoveCounts {
     unsigned long long long_tokens, long_fill;
 };
 
+// Compaction in three launches, with no same-address atomics on the hot path: every workgroup
+// owns a contiguous range of words; k_move_count writes its per-class counts, k_move_scan turns
+// them into per-workgroup bases (one workgroup), k_move places each word at base + running
+// offset + rank in its chunk.  Words keep their relative order within a class.
+constexpr unsigned kMoveBlocks = 1024;
+constexpr int kMoveK = kNumCls + 1;   // destination classes: the slot classes and "long"
+
+__device__ __forceinline__ unsigned move_per_block(unsigned total) { return (total + kMoveBlocks - 1) / kMoveBlocks; }
+
 template <class TokT>
-__global__ void k_move_count(WordsDev<TokT> W, unsigned total, MoveCounts* mc) {
-    const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ int move_class(const WordsDev<TokT>& W, unsigned g, unsigned total, int* c, unsigned* i,
+                                          uint32_t* len) {
     int d = -1;
-    uint32_t len = 0;
+    *len = 0;
     if (g < total) {
-        int c;
-        unsigned i;
-        word_at(W, g, &c, &i);
-        len = word_len(W, c, i);
-        if (len >= 2) d = class_for(len);
+        word_at(W, g, c, i);
+        *len = word_len(W, *c, *i);
+        if (*len >= 2) d = class_for(*len);
     }
-    for (int k = 0; k <= kNumCls; ++k) (void)wave_append(d == k, &mc->n[k]);
-    const unsigned long long lt = wave_sum((unsigned long long)(d == kNumCls ? len : 0u));
-    if ((threadIdx.x & 63) == 0 && lt) atomicAdd(&mc->long_tokens, lt);
+    return d;
 }
 
 template <class TokT>
-__global__ void k_move(WordsDev<TokT> W, unsigned total, WordsDev<TokT> D, MoveCounts* mc) {
-    const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
-    int c = 0, d = -1;
-    unsigned i = 0;
-    uint32_t len = 0;
-    if (g < total) {
-        word_at(W, g, &c, &i);
-        len = word_len(W, c, i);
-        if (len >= 2) d = class_for(len);
+__global__ void __launch_bounds__(256) k_move_count(WordsDev<TokT> W, unsigned total, unsigned* __restrict__ blk_cnt,
+                                                    MoveCounts* mc) {
+    __shared__ unsigned s_c[4][kMoveK];
+    const unsigned per = move_per_block(total);
+    const unsigned beg = blockIdx.x * per, end = min(total, beg + per);
+    unsigned cnt[kMoveK] = {};
+    unsigned long long lt = 0;
+    for (unsigned g = beg + threadIdx.x; g < end; g += blockDim.x) {
+        int c;
+        unsigned i;
+        uint32_t len;
+        const int d = move_class(W, g, total, &c, &i, &len);
+#pragma unroll
+        for (int k = 0; k < kMoveK; ++k) cnt[k] += d == k;
+        if (d == kNumCls) lt += len;
     }
-    unsigned j = ~0u;
-    for (int k = 0; k <= kNumCls; ++k) {
-        const unsigned t = wave_append(d == k, &mc->fill[k]);
-        if (d == k) j = t;
+    const int wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < kMoveK; ++k) {
+        const unsigned v = (unsigned)wave_sum((unsigned long long)cnt[k]);
+        if ((threadIdx.x & 63) == 0) s_c[wv][k] = v;
     }
-    if (d < 0) return;
-    const TokT* src = c < kNumCls ? W.c[c].slot + (size_t)i * slot_w(c) + 1 : W.ltok + W.lbeg[i];
-    const unsigned long long cnt = c < kNumCls ? W.c[c].cnt[i] : W.lcnt[i];
-    if (d < kNumCls) {
-        TokT* dst = D.c[d].slot + (size_t)j * slot_w(d);
-        dst[0] = (TokT)len;
-        for (uint32_t k = 0; k < len; ++k) dst[1 + k] = src[k];
-        for (int k = (int)len + 1; k < slot_w(d); ++k) dst[k] = sentinel<TokT>();
-        D.c[d].cnt[j] = cnt;
-    } else {
-        const unsigned long long bg = atomicAdd(&mc->long_fill, (unsigned long long)len);
-        for (uint32_t k = 0; k < len; ++k) D.ltok[bg + k] = src[k];
-        D.lbeg[j] = bg;
-        D.llen[j] = len;
-        D.lcnt[j] = cnt;
+    lt = wave_sum(lt);
+    if ((threadIdx.x & 63) == 0 && lt) atomicAdd(&mc->long_tokens, lt);
+    __syncthreads();
+    if (threadIdx.x < kMoveK)
+        blk_cnt[blockIdx.x * kMoveK + threadIdx.x] =
+            s_c[0][threadIdx.x] + s_c[1][threadIdx.x] + s_c[2][threadIdx.x] + s_c[3][threadIdx.x];
+}
+
+// one workgroup of kMoveBlocks threads: exclusive scan of every class's per-block counts
+__global__ void __launch_bounds__(kMoveBlocks) k_move_scan(unsigned* __restrict__ blk_cnt, MoveCounts* mc) {
+    __shared__ unsigned s_w[kMoveBlocks / 64];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    for (int k = 0; k < kMoveK; ++k) {
+        const unsigned v = blk_cnt[t * kMoveK + k];
+        unsigned x = v;   // inclusive scan in the wave
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_w[wv] = x;
+        __syncthreads();
+        unsigned base = 0;
+        for (int w = 0; w < wv; ++w) base += s_w[w];
+        blk_cnt[t * kMoveK + k] = base + x - v;   // exclusive
+        if (t == kMoveBlocks - 1) mc->n[k] = base + x;
+        __syncthreads();
+    }
+}
+
+template <class TokT>
+__global__ void __launch_bounds__(256) k_move(WordsDev<TokT> W, unsigned total, WordsDev<TokT> D,
+                                              const unsigned* __restrict__ blk_off, MoveCounts* mc) {
+    __shared__ unsigned s_run[kMoveK];        // words of each class placed by earlier chunks
+    __shared__ unsigned s_wc[4][kMoveK];      // this chunk: per-wave counts
+    const unsigned per = move_per_block(total);
+    const unsigned beg = blockIdx.x * per, end = min(total, beg + per);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (threadIdx.x < kMoveK) s_run[threadIdx.x] = blk_off[blockIdx.x * kMoveK + threadIdx.x];
+    for (unsigned g0 = beg; g0 < end; g0 += blockDim.x) {
+        const unsigned g = g0 + threadIdx.x;
+        int c = 0;
+        unsigned i = 0;
+        uint32_t len = 0;
+        const int d = g < end ? move_class(W, g, total, &c, &i, &len) : -1;
+        unsigned rank = 0;
+#pragma unroll
+        for (int k = 0; k < kMoveK; ++k) {
+            const unsigned long long m = __ballot(d == k);
+            if (d == k) rank = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+            if (lane == 0) s_wc[wv][k] = (unsigned)__popcll(m);
+        }
+        __syncthreads();   // s_run from the previous chunk, s_wc of this one
+        unsigned j = ~0u;
+        if (d >= 0) {
+            unsigned below = 0;
+            for (int w = 0; w < wv; ++w) below += s_wc[w][d];
+            j = s_run[d] + below + rank;
+        }
+        __syncthreads();
+        if (threadIdx.x < kMoveK)
+            s_run[threadIdx.x] += s_wc[0][threadIdx.x] + s_wc[1][threadIdx.x] + s_wc[2][threadIdx.x] + s_wc[3][threadIdx.x];
+        if (d < 0) continue;
+        const TokT* src = c < kNumCls ? W.c[c].slot + (size_t)i * slot_w(c) + 1 : W.ltok + W.lbeg[i];
+        const unsigned long long cnt = c < kNumCls ? W.c[c].cnt[i] : W.lcnt[i];
+        if (d < kNumCls) {
+            TokT* dst = D.c[d].slot + (size_t)j * slot_w(d);
+            dst[0] = (TokT)len;
+            for (uint32_t k = 0; k < len; ++k) dst[1 + k] = src[k];
+            for (int k = (int)len + 1; k < slot_w(d); ++k) dst[k] = sentinel<TokT>();
+            D.c[d].cnt[j] = cnt;
+        } else {
+            const unsigned long long bg = atomicAdd(&mc->long_fill, (unsigned long long)len);
+            for (uint32_t k = 0; k < len; ++k) D.ltok[bg + k] = src[k];
+            D.lbeg[j] = bg;
+            D.llen[j] = len;
+            D.lcnt[j] = cnt;
+        }
     }
 }
 
@@ -2140,10 +2214,13 @@ void MergeLoop<TokT>::compact() {
     HostWords<TokT>& H = words_;
     const unsigned total = H.total();
     DevBuf<MoveCounts> mc(1);
+    DevBuf<unsigned> blk((size_t)kMoveBlocks * kMoveK);
     BPE_HIP(hipMemsetAsync(mc.p, 0, sizeof(MoveCounts), s_));
     const WordsDev<TokT> src = H.dev();
-    if (total)
-        hipLaunchKernelGGL(k_move_count<TokT>, dim3(ceil_div(total, 256)), dim3(256), 0, s_, src, total, mc.p);
+    if (total) {
+        hipLaunchKernelGGL(k_move_count<TokT>, dim3(kMoveBlocks), dim3(256), 0, s_, src, total, blk.p, mc.p);
+        hipLaunchKernelGGL(k_move_scan, dim3(1), dim3(kMoveBlocks), 0, s_, blk.p, mc.p);
+    }
     MoveCounts h{};
     BPE_HIP(hipMemcpyAsync(&h, mc.p, sizeof(h), hipMemcpyDeviceToHost, s_));
     BPE_HIP(hipStreamSynchronize(s_));
@@ -2159,7 +2236,7 @@ void MergeLoop<TokT>::compact() {
     D.llen.alloc(std::max(D.ln, 1u));
     D.lcnt.alloc(std::max(D.ln, 1u));
     if (total)
-        hipLaunchKernelGGL(k_move<TokT>, dim3(ceil_div(total, 256)), dim3(256), 0, s_, src, total, D.dev(), mc.p);
+        hipLaunchKernelGGL(k_move<TokT>, dim3(kMoveBlocks), dim3(256), 0, s_, src, total, D.dev(), blk.p, mc.p);
     BPE_HIP(hipGetLastError());
     BPE_HIP(hipStreamSynchronize(s_));
     words_ = std::move(D);
