@@ -1052,7 +1052,10 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         if (lane == 0) {
             if (!halt) st->halt = stop;
             bt->stop = -1;
-            if (trip_info) { trip_info[2 * trip_slot] = -1; trip_info[2 * trip_slot + 1] = 0; }
+            if (trip_info) {
+                trip_info[4 * trip_slot] = -1; trip_info[4 * trip_slot + 1] = 0;
+                trip_info[4 * trip_slot + 2] = 0; trip_info[4 * trip_slot + 3] = 0;
+            }
         }
         return;
     }
@@ -1155,6 +1158,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     // one scan of every word once the members' lists together pass the scan threshold
     const bool full = __ballot(mem && !use) != 0 || __builtin_amdgcn_readlane((int)pre_list, k) > (int)X.full_threshold;
     const unsigned tot_pool = __builtin_amdgcn_readlane((int)pre_pool, k);
+    const unsigned tot_list = __builtin_amdgcn_readlane((int)pre_list, k);
     const unsigned tot_fresh = __builtin_amdgcn_readlane((int)pre_fresh, k);
     Batch& B = *bt;
     if (i <= k) B.list_pre[i] = pre_list;
@@ -1209,7 +1213,10 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
             atomicAdd(&bs->trips_batched, 1ull);
         }
         atomicAdd(&bs->k_hist[k], 1ull);
-        if (trip_info) { trip_info[2 * trip_slot] = round; trip_info[2 * trip_slot + 1] = k; }
+        if (trip_info) {   // for the host: first round, members, scan mode, list entries
+            trip_info[4 * trip_slot] = round; trip_info[4 * trip_slot + 1] = k;
+            trip_info[4 * trip_slot + 2] = full; trip_info[4 * trip_slot + 3] = (int)tot_list;
+        }
         probe_stamp(st, ptrip, 3);
         probe_stamp(st, ptrip, 4);
     }
@@ -2048,13 +2055,22 @@ class MergeLoop {
    public:
     MergeLoop(hipStream_t stream, Comm* comm, const uint8_t* text, int n_rounds, TrainOutput& out)
         : s_(stream), comm_(comm), text_(text), n_rounds_(n_rounds), out_(out) {}
+    ~MergeLoop() {
+        if (snap_st_) (void)hipHostFree(snap_st_);
+        if (snap_ti_) (void)hipHostFree(snap_ti_);
+        for (auto e : blk_ev_)
+            if (e) (void)hipEventDestroy(e);
+    }
+    MergeLoop(const MergeLoop&) = delete;
+    MergeLoop& operator=(const MergeLoop&) = delete;
 
     void build_words(const WordCounts& wc, const std::vector<std::string>& specials);
     void run();
 
    private:
     static constexpr int kBatch = 64;
-    static constexpr int kTrips = 32;   // batched mode: [k_select][k_merge_batch][k_apply_batch] per host sync
+    static constexpr int kTrips = 32;   // batched mode: [k_select][k_merge_batch][k_apply_batch] per block
+    static_assert(2 * kTrips <= kBatch, "two blocks' timing events fit the event pool");
     static constexpr int kArgBlocks = 64;
     static constexpr unsigned kCScanBlocks = 64;   // k_apply_argmax workgroups scanning C
     unsigned nparts_ = 0;                          // argmax partials the next k_merge reduces
@@ -2124,14 +2140,20 @@ class MergeLoop {
     DevBuf<BatchState> bs_;
     DevBuf<Batch> batch_;
     DevBuf<uint32_t> tags_;      // per slot word: the last batch that claimed it
-    DevBuf<int> trip_info_;      // per trip of a host batch: first round, members
+    DevBuf<int> trip_info_;      // per trip of a block: first round, members, scan mode, list entries (2 slots)
+    RoundState* snap_st_ = nullptr;   // pinned: the state at the end of each in-flight block
+    int* snap_ti_ = nullptr;          // pinned: each block's trip_info
+    hipEvent_t blk_ev_[2] = {nullptr, nullptr};
+    long long slot_base_[2] = {0, 0};   // trips launched before each slot's block
+    void launch_block(int slot, bool timing, std::vector<hipEvent_t>& ev);
+    void finish_block(int slot, bool timing, std::vector<hipEvent_t>& ev, double& k1_ms, double& k1_bytes,
+                      long long& k1_launches);
     DevBuf<unsigned long long> probe_;   // BPE355_PROBE stamps
     void report_probe();
     DevBuf<Partial> list_;       // the candidate list (every present key >= T2)
     static constexpr unsigned kApplyBatchBlocks = kApplyGrid;
     void reset_tags();
-    void run_trips(bool timing, std::vector<hipEvent_t>& ev, double& k1_ms, double& k1_bytes,
-                   long long& k1_launches);
+
     DevBuf<long long> m_cnt_;   // BPE355_ROUND_LOG: each round's winning count (else unallocated)
     DevBuf<RebuildStats> rs_;
     // posting index
@@ -2465,7 +2487,12 @@ void MergeLoop<TokT>::run() {
         BPE_HIP(hipMemsetAsync(bs_.p, 0, sizeof(BatchState), s_));
         batch_.alloc(1);
         BPE_HIP(hipMemsetAsync(batch_.p, 0, sizeof(Batch), s_));
-        trip_info_.alloc(2 * kTrips);
+        trip_info_.alloc(2 * 4 * kTrips);
+        if (!snap_st_) {
+            BPE_HIP(hipHostMalloc(reinterpret_cast<void**>(&snap_st_), 2 * sizeof(RoundState)));
+            BPE_HIP(hipHostMalloc(reinterpret_cast<void**>(&snap_ti_), 2 * 4 * kTrips * sizeof(int)));
+            for (auto& e : blk_ev_) BPE_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
         list_.alloc(kListCap);
     }
     m_a_.alloc(n_rounds_); m_b_.alloc(n_rounds_); m_new_.alloc(n_rounds_); m_mode_.alloc(n_rounds_);
@@ -2554,7 +2581,17 @@ void MergeLoop<TokT>::run() {
             hs_.single_limit = n_live_ / 4 + 1024;
             hs_.pair_limit = pcap_ / 2;
             push_state();
-            run_trips(timing, ev, k1_ms, k1_bytes, k1_launches);
+            {   // blocks back to back until one halts; the block behind a halted one is empty
+                int slot = 0;
+                launch_block(slot, timing, ev);
+                for (;;) {
+                    launch_block(slot ^ 1, timing, ev);
+                    finish_block(slot, timing, ev, k1_ms, k1_bytes, k1_launches);
+                    if (hs_.halt != HALT_NONE || hs_.err) break;
+                    slot ^= 1;
+                }
+                finish_block(slot ^ 1, timing, ev, k1_ms, k1_bytes, k1_launches);   // drained
+            }
             BPE_REQUIRE(!(hs_.err & ERR_PAIRS_FULL), BPE_E_NOMEM, "pair table overflow");
             BPE_REQUIRE(!(hs_.err & ERR_C_FULL), BPE_E_NOMEM, "candidate list overflow");
             BPE_REQUIRE(!(hs_.err & ERR_POOL), BPE_E_NOMEM, "token pool overflow");
@@ -2766,23 +2803,27 @@ void MergeLoop<TokT>::reset_tags() {
     BPE_HIP(hipMemsetAsync(tags_.p, 0, tags_.bytes(), s_));
 }
 
-// kTrips x [k_select][k_merge_batch][k_apply_batch], then one host sync.  A trip after a halt
-// finds nothing to do.  With timing on, k_merge_batch is event-timed on one trip in
-// kTimingStride (events stamped by its own dispatch packet).
+// One block: kTrips x [k_select][k_merge_batch][k_apply_batch], then a snapshot of the state
+// and of the trips' records into pinned memory, ordered on the stream, and an event.  Two blocks
+// are in flight: the host reads one block's snapshot while the next one runs, so the device does
+// not idle at every host check.  A block launched after a halt finds nothing to do (k_select
+// sees st->halt).  With timing on, k_merge_batch is event-timed on one trip in kTimingStride
+// (events stamped by its own dispatch packet).
 template <class TokT>
-void MergeLoop<TokT>::run_trips(bool timing, std::vector<hipEvent_t>& ev, double& k1_ms, double& k1_bytes,
-                                long long& k1_launches) {
+void MergeLoop<TokT>::launch_block(int slot, bool timing, std::vector<hipEvent_t>& ev) {
     const size_t lr_member = 2ull * tok_cap_, lr_parity = (size_t)kMaxBatch * lr_member;
     const unsigned ntb = tok_cap_;
     const unsigned apply_blocks = kApplyBatchBlocks;
+    int* ti = trip_info_.p + (size_t)slot * 4 * kTrips;
+    slot_base_[slot] = trips_launched_;
     for (int t = 0; t < kTrips; ++t) {
         const bool timed = timing && (trips_launched_ + t) % kTimingStride == 0;
+        hipEvent_t* e = &ev[2 * ((size_t)slot * kTrips + t)];
         hipLaunchKernelGGL(k_select, dim3(1), dim3(kSelThreads), 0, s_, st_.p, bs_.p, pairs(), toks(), idev_,
                            batch_.p, (const Partial*)part_.p, (const Partial*)list_.p, m_a_.p, m_b_.p, m_new_.p,
-                           m_mode_.p, m_cnt_.p,
-                           trip_info_.p, t);
+                           m_mode_.p, m_cnt_.p, ti, t);
         hipExtLaunchKernelGGL(k_merge_batch<TokT>, dim3(merge_grid_), dim3(256), 0, s_,
-                              timed ? ev[2 * t] : nullptr, timed ? ev[2 * t + 1] : nullptr, 0,
+                              timed ? e[0] : nullptr, timed ? e[1] : nullptr, 0,
                               st_.p, (const Batch*)batch_.p, pairs(), toks(), wdev_, idev_, LR_.p, lr_member,
                               lr_parity, tags_.p);
         hipLaunchKernelGGL(k_apply_batch, dim3(apply_blocks), dim3(kApplyBatchThreads), 0, s_, st_.p, bs_.p,
@@ -2790,33 +2831,34 @@ void MergeLoop<TokT>::run_trips(bool timing, std::vector<hipEvent_t>& ev, double
                            list_.p, 0);
     }
     BPE_HIP(hipGetLastError());
-    pull_state();
-    std::vector<int> ti(2 * kTrips);
-    BPE_HIP(hipMemcpy(ti.data(), trip_info_.p, ti.size() * 4, hipMemcpyDeviceToHost));
-    for (int t = 0; t < kTrips; ++t) trips_run_ += ti[2 * t + 1] > 0;
-    if (timing) {
-        const double slot_avg = scan_bytes_ / std::max(1u, idev_.n_slot_words + words_.ln);
-        for (int t = 0; t < kTrips; ++t) {
-            if ((trips_launched_ + t) % kTimingStride || ti[2 * t + 1] <= 0) continue;
-            float ms = 0;
-            BPE_HIP(hipEventElapsedTime(&ms, ev[2 * t], ev[2 * t + 1]));
-            const int r0 = ti[2 * t], k = ti[2 * t + 1];
-            std::vector<uint32_t> mode(k);
-            BPE_HIP(hipMemcpy(mode.data(), m_mode_.p + r0, k * 4ull, hipMemcpyDeviceToHost));
-            // algorithmic bytes: every slot on a full scan, else the members' list entries and
-            // their slots (at the table's mean slot size); every long word once per trip
-            bool full = false;
-            double b = long_bytes_;
-            for (uint32_t m : mode) {
-                if (m == 0xffffffffu) full = true;
-                else b += m * (4.0 + slot_avg);
-            }
-            k1_ms += ms;
-            k1_bytes += full ? scan_bytes_ : b;
-            ++k1_launches;
-        }
-    }
+    BPE_HIP(hipMemcpyAsync(&snap_st_[slot], st_.p, sizeof(RoundState), hipMemcpyDeviceToHost, s_));
+    BPE_HIP(hipMemcpyAsync(snap_ti_ + (size_t)slot * 4 * kTrips, ti, 4 * kTrips * sizeof(int),
+                           hipMemcpyDeviceToHost, s_));
+    BPE_HIP(hipEventRecord(blk_ev_[slot], s_));
     trips_launched_ += kTrips;
+}
+
+template <class TokT>
+void MergeLoop<TokT>::finish_block(int slot, bool timing, std::vector<hipEvent_t>& ev, double& k1_ms,
+                                   double& k1_bytes, long long& k1_launches) {
+    BPE_HIP(hipEventSynchronize(blk_ev_[slot]));
+    hs_ = snap_st_[slot];
+    const int* ti = snap_ti_ + (size_t)slot * 4 * kTrips;
+    for (int t = 0; t < kTrips; ++t) trips_run_ += ti[4 * t + 1] > 0;
+    if (!timing) return;
+    const double slot_avg = scan_bytes_ / std::max(1u, idev_.n_slot_words + words_.ln);
+    for (int t = 0; t < kTrips; ++t) {
+        if ((slot_base_[slot] + t) % kTimingStride || ti[4 * t + 1] <= 0) continue;
+        float ms = 0;
+        const hipEvent_t* e = &ev[2 * ((size_t)slot * kTrips + t)];
+        BPE_HIP(hipEventElapsedTime(&ms, e[0], e[1]));
+        // algorithmic bytes: every slot on a full scan, else the members' list entries and their
+        // slots (at the table's mean slot size); every long word once per trip
+        const bool full = ti[4 * t + 2] != 0;
+        k1_ms += ms;
+        k1_bytes += full ? scan_bytes_ : long_bytes_ + (double)(unsigned)ti[4 * t + 3] * (4.0 + slot_avg);
+        ++k1_launches;
+    }
 }
 
 // Every word is one token: the reference keeps popping the remaining zero-count keys,
