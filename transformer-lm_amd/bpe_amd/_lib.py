@@ -9,6 +9,7 @@ from __future__ import annotations
 import ctypes
 import errno as _errno
 import os
+import re
 import pathlib
 import struct
 
@@ -131,7 +132,10 @@ def check(rc: int, what: str = ""):
         en = lib().bpe_last_errno() or _errno.EIO
         raise OSError(en, os.strerror(en), what or msg)
     if rc == BPE_E_UTF8:
-        raise UnicodeDecodeError("utf-8", b"", 0, 1, msg)
+        # start/end name the first ill-formed byte, as CPython's decoder reports it
+        m = re.search(r"position (\d+)", msg)
+        pos = int(m.group(1)) if m else 0
+        raise UnicodeDecodeError("utf-8", b"", pos, pos + 1, msg)
     if rc == BPE_E_KEY:
         raise KeyError(msg)
     raise RuntimeError(f"libbpe355 {what} failed ({rc}): {msg}")

@@ -81,7 +81,72 @@ __global__ void k_validate(const uint8_t* __restrict__ s, size_t n,
             cr_bits |= (x - 0x01010101u) & ~x & 0x80808080u;
         }
         if (cr_bits) atomicOr(has_cr, 1u);
+        // neighbours for the sequences that cross the unit: the adjacent lanes hold the adjacent
+        // units (a unit at a wave's edge reads its neighbour from memory)
+        const int lane = threadIdx.x & 63;
+        uint32_t prev = __shfl_up(w[3], 1), next = __shfl_down(w[0], 1);
         if (!hi_bits) return;                                       // all ASCII: done
+        if (lane == 0) prev = lo >= 4 ? *reinterpret_cast<const uint32_t*>(s + lo - 4) : 0u;
+        if (lane == 63 || lo + 2 * kValidateBytes > n) {   // the next unit is not a full one in a lane
+            next = 0;
+            for (int k = 0; k < 4 && lo + kValidateBytes + k < n; ++k) next |= (uint32_t)s[lo + kValidateBytes + k] << (8 * k);
+        }
+        // window b[0..24): 4 bytes before the unit, its 16, 4 after
+        uint8_t b[24];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            b[k] = (uint8_t)(prev >> (8 * k));
+            b[20 + k] = (uint8_t)(next >> (8 * k));
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) b[4 + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+        // bytes of the text left from window index x (the window may run past the end)
+        auto avail = [&](int x) -> size_t { const size_t i = lo + (size_t)x - 4; return i < n ? n - i : 0; };
+        auto len_valid = [&](int x) -> int {   // utf8_len_valid on the window (x: a constant)
+            const uint32_t b0 = b[x];
+            uint32_t need, lo8 = 0x80, hi8 = 0xBF;
+            if (b0 < 0x80u) return 1;
+            if (b0 >= 0xC2u && b0 <= 0xDFu) need = 2;
+            else if (b0 == 0xE0u) { need = 3; lo8 = 0xA0; }
+            else if (b0 >= 0xE1u && b0 <= 0xECu) need = 3;
+            else if (b0 == 0xEDu) { need = 3; hi8 = 0x9F; }
+            else if (b0 >= 0xEEu && b0 <= 0xEFu) need = 3;
+            else if (b0 == 0xF0u) { need = 4; lo8 = 0x90; }
+            else if (b0 >= 0xF1u && b0 <= 0xF3u) need = 4;
+            else if (b0 == 0xF4u) { need = 4; hi8 = 0x8F; }
+            else return 0;
+            if (avail(x) < need) return 0;
+            const uint32_t b1 = b[x + 1];
+            if (b1 < lo8 || b1 > hi8) return 0;
+            if (need >= 3 && (b[x + 2] & 0xC0u) != 0x80u) return 0;
+            if (need == 4 && (b[x + 3] & 0xC0u) != 0x80u) return 0;
+            return (int)need;
+        };
+        int bad_k = -1;
+#pragma unroll
+        for (int k = 0; k < kValidateBytes; ++k) {   // byte_ok for the high-bit bytes
+            const int x = 4 + k;
+            if (bad_k >= 0 || b[x] < 0x80u) continue;
+            bool ok;
+            if ((b[x] & 0xC0u) != 0x80u) {
+                ok = len_valid(x) > 0;
+            } else {   // a continuation byte: covered by the nearest lead byte within 3 before it
+                ok = false;
+                bool found = false;
+#pragma unroll
+                for (int d = 1; d <= 3; ++d) {
+                    if (found || lo + (size_t)k < (size_t)d) continue;   // no byte before the text
+                    if ((b[x - d] & 0xC0u) != 0x80u) {
+                        found = true;
+                        const int l = len_valid(x - d);
+                        ok = l > 0 && d < l;
+                    }
+                }
+            }
+            if (!ok) bad_k = k;
+        }
+        if (bad_k >= 0) atomicMin(err_pos, (unsigned long long)(lo + (size_t)bad_k));
+        return;
     }
     const size_t hi = lo + kValidateBytes < n ? lo + kValidateBytes : n;
     for (size_t i = lo; i < hi; ++i) {
