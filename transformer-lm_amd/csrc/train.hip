@@ -1280,6 +1280,15 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
     const Batch& B = *bt;
     if (B.stop) return;
     const int k = B.k;
+    {   // list mode: workgroups past the listed words (and past the members' registrations) have
+        // nothing to do -- skip their LDS clear, barriers and flush
+        const unsigned bid = blockIdx.x;
+        if (bid >= (unsigned)k && bid < W.lblk0) {
+            const bool lists = k > 1 ? !B.full_scan : B.m[0].use_list != 0;
+            const unsigned total = k > 1 ? B.list_pre[k] : B.m[0].list_len;
+            if (lists && bid * blockDim.x >= total) return;
+        }
+    }
     if (tid < k) { s_ma[tid] = B.m[tid].a; s_mb[tid] = B.m[tid].b; s_mn[tid] = B.m[tid].nw; }
     if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 5);
     for (unsigned q = tid; q < 2 * kLdsB * (unsigned)k; q += blockDim.x) l_lr[q] = 0;
