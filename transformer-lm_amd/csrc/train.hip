@@ -951,6 +951,16 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     if (li >= 0) lq = list[li];
     const int nparts = st->nparts;
     const unsigned ln = bs->list_n;
+    if (st->halt) {   // a trip queued behind a halt: nothing to do (the host takes over)
+        if (tid == 0) {
+            bt->stop = -1;
+            if (trip_info) {
+                trip_info[4 * trip_slot] = -1; trip_info[4 * trip_slot + 1] = 0;
+                trip_info[4 * trip_slot + 2] = 0; trip_info[4 * trip_slot + 3] = 0;
+            }
+        }
+        return;
+    }
     // the rule's scalars (uniform: scalar loads, in flight with the vector loads above)
     const int halt = st->halt, round = st->round, n_rounds = st->n_rounds, host_round = st->host_round;
     const unsigned nC = st->nC, c_limit = st->c_limit;
