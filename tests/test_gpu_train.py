@@ -69,3 +69,26 @@ def test_deterministic_repeat():
     r1 = bpe_amd.train_bpe_bytes(data, 1500, ["<|endoftext|>"])
     r2 = bpe_amd.train_bpe_bytes(data, 1500, ["<|endoftext|>"])
     assert r1 == r2
+
+
+def _tie_heavy_text(rng, n_words):
+    """Short words over a tiny alphabet: pair counts tie constantly, and tied pairs often share a
+    token with the top ones -- the cases the batched rounds' rules (1)-(4') must get right."""
+    alpha = rng.choice(["ab", "abc", "abcd", "aab", "xyz "])
+    words = []
+    for _ in range(n_words):
+        words.append("".join(rng.choice(alpha) for _ in range(rng.randint(1, 7))))
+    sep = rng.choice([" ", "  ", "\n", " \n"])
+    return sep.join(words)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_train_matches_oracle_tie_heavy(seed):
+    import random
+    rng = random.Random(9000 + seed)
+    data = _tie_heavy_text(rng, rng.choice([200, 2000, 20000])).encode("utf-8")
+    vocab = rng.choice([300, 400, 1000])
+    want = oracle.train_raw(data, vocab, ["<|endoftext|>"])
+    got = bpe_amd.train_bpe_bytes(data, vocab, ["<|endoftext|>"])
+    assert got[1] == want[1]
+    assert got[0] == want[0]
