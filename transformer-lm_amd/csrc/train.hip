@@ -2519,7 +2519,7 @@ void MergeLoop<TokT>::run() {
     if (round_log) m_cnt_.alloc(n_rounds_);
     toff_.alloc(tok_cap_); tlen_.alloc(tok_cap_);
     thash_.alloc(tok_cap_); tpw_.alloc(tok_cap_); tkey8_.alloc(tok_cap_);
-    tmap_.alloc(next_pow2(4ull * tok_cap_));
+    tmap_.alloc(next_pow2(16ull * tok_cap_));   // load <= 1/16: a miss (a fresh pair) is ~1 probe
     BPE_HIP(hipMemsetAsync(tmap_.p, 0, tmap_.bytes(), s_));
     const unsigned pool_cap = std::max(1u << 16, 64u * std::max(max_len_, 8u));
     pool_.alloc(pool_cap);
