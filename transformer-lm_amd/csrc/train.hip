@@ -2095,6 +2095,9 @@ class MergeLoop {
     unsigned nparts_ = 0;                          // argmax partials the next k_merge reduces
     static constexpr int kTimingStride = 8;   // k_merge launches timed: one in 8
     static constexpr unsigned long long kTarget = 4096;
+    // batched mode: the pair table grows past load 1 / kPairLoadDiv (an insert is an unsuccessful
+    // linear-probe search: ~2.5 dependent probes at load 1/2, ~1.4 at 1/4)
+    static constexpr size_t kPairLoadDiv = 2;   // 4 measured: no gain (366 vs 364 ms)
 
     void alloc_pairs(size_t cap);
     void grow_pairs();
@@ -2589,7 +2592,7 @@ void MergeLoop<TokT>::run() {
         if (batched_) {
             // k_select checks the pair table, the token pool and the compaction schedule before
             // every trip and hands back to the host (HALT_HOST); here the host makes room
-            if (hs_.pair_used + 4ull * (hs_.ntok + kMaxBatch) * kMaxBatch > pcap_ / 2) {
+            if (hs_.pair_used + 4ull * (hs_.ntok + kMaxBatch) * kMaxBatch > pcap_ / kPairLoadDiv) {
                 grow_pairs();
                 hs_.halt = HALT_REBUILD;   // C holds slot indices: rebuild it
                 continue;
@@ -2598,7 +2601,7 @@ void MergeLoop<TokT>::run() {
             if (hs_.halt == HALT_HOST) hs_.halt = HALT_NONE;
             hs_.host_round = next_index_round_;
             hs_.single_limit = n_live_ / 4 + 1024;
-            hs_.pair_limit = pcap_ / 2;
+            hs_.pair_limit = pcap_ / kPairLoadDiv;
             push_state();
             {   // blocks back to back until one halts; the block behind a halted one is empty
                 int slot = 0;
