@@ -857,7 +857,7 @@ struct BatchState {
     unsigned long long k1_why[6];   // single-merge trips: P1 a == b / P1 not fresh / no list / P2 fails / tie / end
 };
 constexpr unsigned kListCap = 256;   // the candidate list k_select ranks (one thread per entry)
-constexpr unsigned kApplyGrid = 256;   // k_apply_batch workgroups (k_select reads one partial each)
+constexpr unsigned kApplyGrid = 512;   // k_apply_batch workgroups (k_select reads one partial each)
 
 struct TokMetaS {
     unsigned long long ha, pb, hb, pa;   // hash(a), P^len(b), hash(b), P^len(a)
@@ -915,12 +915,12 @@ __device__ __forceinline__ void cand_meta(const Cand& c, const ToksDev& K, const
     }
 }
 
-// One workgroup: the batch of this trip.  Waves 0-3 reduce the apply's per-workgroup partials
-// to the exact best candidate P1; waves 4-7 hold the candidate list (every present key >= T2),
+// One workgroup: the batch of this trip.  Waves 0-7 reduce the apply's per-workgroup partials
+// to the exact best candidate P1; waves 8-11 hold the candidate list (every present key >= T2),
 // look up its entries' metadata and rank them.  All global loads are issued before the first
 // barrier, so the kernel costs about one memory round trip plus the dedupe lookups' chain, then
 // the ranking, the rule and the record (wave 0).
-constexpr int kSelListWave = 4;   // first wave of the list
+constexpr int kSelListWave = 8;   // first wave of the list
 constexpr unsigned kListTarget = 48;   // keys the next list should hold (T2 control)
 constexpr bool kSelMetaAll = true;     // metadata of every listed key before the ranking
 constexpr int kSelThreads = 64 * kSelListWave + (int)kListCap;
@@ -932,7 +932,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
                                                         uint32_t* __restrict__ m_new, uint32_t* __restrict__ m_mode,
                                                         long long* __restrict__ m_cnt, int* __restrict__ trip_info,
                                                         int trip_slot) {
-    static_assert(kApplyGrid <= 64 * kSelListWave, "one partial per thread of waves 0-3");
+    static_assert(kApplyGrid <= 64 * kSelListWave, "one partial per thread of the partial waves");
     __shared__ Cand s_wave[kSelListWave];
     __shared__ Cand s_all[kListCap];
     __shared__ Cand s_list[kTopM];
