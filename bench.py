@@ -1,31 +1,42 @@
 #!/usr/bin/env python3
 """bench.py -- BPE train input MB/s + merges/s at 32k vocab; encode MB/s (BASELINE.json metric).
 
-One step = one full train_bpe (BASELINE.json configs[2]: OpenWebText sizing, vocab 32000 with
-<|endoftext|>, perf/bpe/owt.py:4-6) over a synthetic OWT-like corpus already resident in HBM:
-UTF-8 check, GPT-2 pre-tokenization, unique-word count, pair histogram, 31,743 merge rounds,
-merges/vocab back on the host.  OWT itself is not available offline; the corpus is the
-library's deterministic generator (bpe_synth_corpus_device), `--bytes` per GPU.
+One step = one drop-in `train_bpe(input_path, 32000, ["<|endoftext|>"])` (reference
+models/tokenizer/train.py:142-231; BASELINE configs[2]: OpenWebText sizing, perf/bpe/owt.py:4-6)
+over an OWT-sized synthetic corpus FILE, page-cache warm: the file read (train.py:22), UTF-8
+check, GPT-2 pre-tokenization, unique-word count, pair histogram, 31,743 merge rounds, merges and
+vocab back in host memory.  OWT itself is not available offline; the corpus is the library's
+deterministic generator (bpe_synth_corpus_host), written once to a scratch file before timing.
 
-Multi-GPU (torchrun, one rank per GPU): each rank owns a slab of the same global corpus (weak
-scaling: per-GPU bytes fixed) and pre-tokenizes/counts it; ONE RCCL all-gather of the slabs'
-unique-word tables follows, and every rank trains on their union (no per-round collective;
-BPE355_EXCHANGE=rounds selects the per-round all-reduce of the pair deltas instead).  Every rank
-ends with the identical global merge list.
+`value` is that end-to-end rate ("input MB/s = N / end-to-end wall, file read ->
+merges in host memory").  `device_resident` is the same training with the corpus already in HBM
+(train_bpe_device), i.e. without the file read and the host->device copy.
 
-Prints ONE JSON line on rank 0.  Extra fields: merges_per_s, encode MB/s (Tokenizer.encode of
-the same corpus with the trained merges), roofline of the dominant kernel (HIP events on the
-library's stream), and cpu_baseline: the pure-Python port of the reference (oracle/cpu_ref.py)
-on a bounded sample, timed on this host.
+GPUs (strong scaling: the corpus size is fixed, --bytes in total):
+  * `python bench.py --gpus N` (no WORLD_SIZE): ONE process drives N devices, as the reference's
+    single-process caller would (perf/bpe/util.py:16): train_bpe with set_num_gpus(N) -- one slab
+    of the file per device, one RCCL all-gather of the word tables, the merge loop on device 0.
+  * under torch.distributed.run (WORLD_SIZE = N): one process per GPU; every rank reads its share
+    of the same file (train_bpe(..., comm, split_file=True)); same exchange.  --gpus must equal
+    WORLD_SIZE.
+`n_gpus` reports the ranks that actually took part (from the library's stats).
+
+Prints ONE JSON line on rank 0.  Extra fields: merges_per_s, merge_loop (trips, time per trip),
+encode (Tokenizer.encode of the corpus with the trained merges, device to device), roofline of
+the dominant kernel (HIP events stamped by the kernel's own dispatch, on the library's stream),
+and cpu_baseline: the pure-Python port of the reference (oracle/cpu_ref.py) on a bounded sample,
+timed on this host (rank 0, N = 1 only).
 """
 from __future__ import annotations
 
 import argparse
 import ctypes
 import json
+import mmap
 import os
 import pathlib
 import sys
+import tempfile
 import time
 
 ROOT = pathlib.Path(__file__).resolve().parent
@@ -43,10 +54,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--bytes", type=float, default=11.9e9, help="corpus bytes per GPU")
+    ap.add_argument("--bytes", type=float, default=11.9e9, help="corpus bytes in total (strong scaling)")
     ap.add_argument("--vocab", type=int, default=32000)
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--flavour", type=int, default=0, help="0 OWT-like, 1 TinyStories-like")
+    ap.add_argument("--corpus-dir", default=os.environ.get("BPE355_BENCH_DIR", tempfile.gettempdir()))
+    ap.add_argument("--keep-corpus", action="store_true")
+    ap.add_argument("--no-device-resident", action="store_true")
     ap.add_argument("--no-encode", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-mb", type=float, default=16.0)
@@ -55,131 +69,192 @@ def parse():
     return ap.parse_args()
 
 
+def write_corpus(L, path: pathlib.Path, n: int, seed: int, flavour: int):
+    """the generator's bytes [0, n) into `path` through a shared mapping (page-cache warm)"""
+    tmp = path.with_suffix(".part")
+    with open(tmp, "wb+") as f:
+        f.truncate(n)
+        with mmap.mmap(f.fileno(), n) as m:
+            buf = (ctypes.c_char * n).from_buffer(m)
+            rc = L.bpe_synth_corpus_host(ctypes.addressof(buf), n, seed, flavour, 0, 16)
+            del buf
+            assert rc == 0, rc
+    os.replace(tmp, path)
+
+
 def main():
     args = parse()
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    multiproc = env_world > 1
+    if multiproc and args.gpus != env_world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world} ranks were launched")
     import torch
     import torch.distributed as dist
-    from bpe_amd import _lib, train_bpe_device, Tokenizer
+    import bpe_amd
+    from bpe_amd import _lib, train_bpe, train_bpe_device, Tokenizer
+    from bpe_amd.train import last_train_stats
 
+    n_dev = torch.cuda.device_count()
+    if not multiproc and args.gpus > n_dev:
+        sys.exit(f"bench.py: --gpus {args.gpus} but only {n_dev} GPU(s) are visible to this process")
     torch.cuda.set_device(local_rank)
     L = _lib.lib()
     _lib.require_device()
     comm = None
-    if world > 1:
+    if multiproc:
         from bpe_amd.dist import Communicator
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         comm = Communicator.from_torch(local_rank)   # RCCL: one all-gather of the word tables
-
-    # ---------------------------------------------------------------- corpus slab in HBM
-    blocks = max(1, int(args.bytes) // BLOCK)
-    n = blocks * BLOCK
-    corpus = torch.empty(n, dtype=torch.uint8, device="cuda")
-    torch.cuda.synchronize()
-    _lib.check(L.bpe_synth_corpus_device(ctypes.c_void_p(corpus.data_ptr()), n, args.seed,
-                                         args.flavour, rank * blocks, None), "synth")
-    torch.cuda.synchronize()
+    else:
+        bpe_amd.set_num_gpus(args.gpus)
 
     def barrier():
-        if world > 1:
+        if multiproc:
             dist.barrier()
 
-    def train_once():
-        return train_bpe_device(corpus.data_ptr(), n, args.vocab, [EOT], comm=comm)
+    def max_over_ranks(x: float) -> float:
+        if not multiproc:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
-    from bpe_amd.train import last_train_stats
+    # ---------------------------------------------------------------- the corpus file
+    n = max(1, int(args.bytes) // BLOCK) * BLOCK
+    path = pathlib.Path(args.corpus_dir) / f"bpe355_bench_s{args.seed}_f{args.flavour}_{n}.txt"
+    if rank == 0 and not (path.exists() and path.stat().st_size == n):
+        t = time.perf_counter()
+        write_corpus(L, path, n, args.seed, args.flavour)
+        print(f"[bench] wrote {n / 1e9:.2f} GB corpus to {path} in {time.perf_counter() - t:.1f}s",
+              file=sys.stderr, flush=True)
+    barrier()
+
+    def train_file():
+        if multiproc:
+            return train_bpe(path, args.vocab, [EOT], comm=comm, split_file=True)
+        return train_bpe(path, args.vocab, [EOT])
+
+    # ---------------------------------------------------------------- end to end: file -> merges
     L.bpe_set_timing(0)
     for _ in range(args.warmup):
-        vocab, merges = train_once()
+        vocab, merges = train_file()
     L.bpe_set_timing(0 if args.no_timing else 1)
     stats = []
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        vocab, merges = train_once()
+        vocab, merges = train_file()
         stats.append(last_train_stats())
     torch.cuda.synchronize()
     barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(time.perf_counter() - t0)
     L.bpe_set_timing(0)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    n_gpus = int(stats[-1]["n_gpus"])
     ms_per_step = elapsed / args.steps * 1e3
-    total_bytes = n * world
-    value = total_bytes / (elapsed / args.steps) / 1e6
-
-    merge_ms = sum(s["t_merge_ms"] for s in stats) / len(stats)
+    value = n / (elapsed / args.steps) / 1e6
     rounds = len(merges)
-    # dominant kernel (event-timed on the library's stream during the timed steps)
-    k_merge_ms = sum(s["merge_kernel_ms"] for s in stats)
-    k_merge_launch = sum(s["merge_kernel_launches"] for s in stats)
-    k_merge_bytes = sum(s["merge_kernel_bytes"] for s in stats)
-    k_count_ms = sum(s["count_kernel_ms"] for s in stats)
-    k_count_bytes = sum(s["count_kernel_bytes"] for s in stats)
+    avg = {k: sum(s[k] for s in stats) / len(stats) for k in stats[0]}
+
+    # dominant kernel: k_count_words (device time per launch, event-timed on the library's
+    # stream) vs the merge loop's trips
     roofline = None
-    if k_merge_ms > 0 or k_count_ms > 0:
-        # the merge kernel is event-timed on a sample of its launches: compare per-step
-        # estimates (one launch per trip when rounds are batched, else one per round)
-        trips = sum(s.get("n_trips", 0) for s in stats) / len(stats)
-        merge_launches = trips if trips > 0 else rounds
-        merge_step_ms = k_merge_ms / max(1, k_merge_launch) * merge_launches
-        count_step_ms = k_count_ms / len(stats)
-        if merge_step_ms >= count_step_ms:
-            kname = "k_merge_batch" if trips > 0 else "k_merge"
-            kms, kb, kl = k_merge_ms, k_merge_bytes, k_merge_launch
-        else:
-            kname, kms, kb, kl = "k_count_words", k_count_ms, k_count_bytes, len(stats)
+    if avg["count_kernel_ms"] > 0:
+        kms = avg["count_kernel_ms"]
+        kb = avg["count_kernel_bytes"]
         achieved = kb / (kms / 1e3) / 1e9
         traffic = None
         tf = ROOT / "profiles" / "traffic.json"
         if tf.exists():
-            traffic = json.loads(tf.read_text()).get(kname)
+            traffic = json.loads(tf.read_text()).get("k_count_words")
         roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": kname,
-                    "launches_per_step": round(merge_launches) if kname != "k_count_words" else 1,
-                    "timed_launches": kl,
-                    "avg_launch_us": round(kms / kl * 1e3, 3),
-                    "bytes_per_launch": kb / kl}
+                    "kernel": "k_count_words", "launches_per_step": 1,
+                    "timed_launches": len(stats), "avg_launch_us": round(kms * 1e3, 3),
+                    "bytes_per_launch": kb,
+                    "note": "rank 0's slab when n_gpus > 1" if n_gpus > 1 else None}
+    trips = avg["n_trips"]
+    merge_loop = {
+        "rounds": rounds, "trips": int(trips),
+        "ms": round(avg["t_merge_ms"], 2),
+        "us_per_trip": round(avg["t_merge_ms"] * 1e3 / trips, 2) if trips else None,
+        "us_per_round": round(avg["t_merge_ms"] * 1e3 / max(1, rounds), 3),
+        "k_merge_batch_us": (round(avg["merge_kernel_ms"] * 1e3 / avg["merge_kernel_launches"], 2)
+                             if avg["merge_kernel_launches"] else None),
+        "k_merge_batch_bytes_per_launch": (round(avg["merge_kernel_bytes"] / avg["merge_kernel_launches"])
+                                           if avg["merge_kernel_launches"] else None),
+    }
 
-    # ---------------------------------------------------------------- encode MB/s
+    # ---------------------------------------------------------------- corpus resident in HBM
+    device_resident = None
+    corpus = None
+    need_corpus = not (args.no_device_resident and args.no_encode)
+    if need_corpus and (multiproc or n_gpus == 1):
+        world = env_world
+        blocks = n // BLOCK
+        b0, b1 = blocks * rank // world, blocks * (rank + 1) // world
+        slab = (b1 - b0) * BLOCK
+        corpus = torch.empty(max(1, slab), dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        _lib.check(L.bpe_synth_corpus_device(ctypes.c_void_p(corpus.data_ptr()), slab, args.seed,
+                                             args.flavour, b0, None), "synth")
+        torch.cuda.synchronize()
+    if corpus is not None and not args.no_device_resident:
+        def train_dev():
+            return train_bpe_device(corpus.data_ptr(), slab, args.vocab, [EOT], comm=comm)
+        for _ in range(args.warmup):
+            v2, m2 = train_dev()
+        dstats = []
+        barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            v2, m2 = train_dev()
+            dstats.append(last_train_stats())
+        torch.cuda.synchronize()
+        barrier()
+        el = max_over_ranks(time.perf_counter() - t1)
+        assert m2 == merges and v2 == vocab, "device-resident result differs from the file result"
+        s0 = dstats[-1]
+        device_resident = {
+            "value": round(n / (el / args.steps) / 1e6, 2), "unit": "MB/s",
+            "ms_per_step": round(el / args.steps * 1e3, 2),
+            "phases_ms": {k: round(s0[k], 2) for k in ("t_prepare_ms", "t_count_ms", "t_exchange_ms",
+                                                        "t_words_ms", "t_merge_ms", "t_total_ms")}}
+
+    # ---------------------------------------------------------------- encode MB/s (device)
     encode = None
-    if not args.no_encode:
+    if corpus is not None and not args.no_encode:
         tok = Tokenizer(vocab, merges, [EOT])
         h = tok._device()
-        out = torch.empty(n, dtype=torch.int32, device="cuda")
+        out = torch.empty(slab, dtype=torch.int32, device="cuda")
         n_out = ctypes.c_size_t(0)
-        _lib.check(L.bpe_tok_encode_device(h, ctypes.c_void_p(corpus.data_ptr()), n,
-                                           ctypes.c_void_p(out.data_ptr()), ctypes.byref(n_out),
-                                           None), "encode")  # warm-up pass
+
+        def enc():
+            _lib.check(L.bpe_tok_encode_device(h, ctypes.c_void_p(corpus.data_ptr()), slab,
+                                               ctypes.c_void_p(out.data_ptr()), ctypes.byref(n_out),
+                                               None), "encode")
+        enc()   # warm-up pass
         barrier()
         torch.cuda.synchronize()
         te = time.perf_counter()
-        _lib.check(L.bpe_tok_encode_device(h, ctypes.c_void_p(corpus.data_ptr()), n,
-                                           ctypes.c_void_p(out.data_ptr()), ctypes.byref(n_out),
-                                           None), "encode")
+        enc()
         torch.cuda.synchronize()
         barrier()
-        te = time.perf_counter() - te
-        if world > 1:
-            t = torch.tensor([te], dtype=torch.float64, device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            te = float(t.item())
-        encode = {"value": round(total_bytes / te / 1e6, 1), "unit": "MB/s",
-                  "ids_per_gpu": int(n_out.value), "seconds": round(te, 4)}
+        te = max_over_ranks(time.perf_counter() - te)
+        encode = {"value": round(n / te / 1e6, 1), "unit": "MB/s", "ids_rank0": int(n_out.value),
+                  "seconds": round(te, 4), "scope": "corpus in HBM -> ids in HBM"}
         del out
 
     # ---------------------------------------------------------------- CPU baseline (rank 0, N=1)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
         from oracle import cpu_ref
         m = min(n, int(args.cpu_sample_mb * 1e6) // BLOCK * BLOCK)
-        text = corpus[:m].cpu().numpy().tobytes().decode("utf-8")
+        with open(path, "rb") as f:
+            text = f.read(m).decode("utf-8")
         t0c = time.perf_counter()
         _, cmerges, info = cpu_ref.train(text, args.vocab, [EOT], deadline=t0c + args.cpu_cap_s)
         per_round = info["t_merge_s"] / max(1, info["rounds_done"])
@@ -191,37 +266,43 @@ def main():
                           f"{info['rounds_done']}/{info['rounds_total']} merge rounds in "
                           f"{info['t_merge_s']:.1f}s measured, rest extrapolated at "
                           f"{per_round * 1e3:.1f} ms/round"),
+               "rounds_measured_frac": round(info["rounds_done"] / max(1, info["rounds_total"]), 4),
                "merges_per_s": round(1.0 / per_round, 2) if per_round > 0 else None}
 
     if rank == 0:
         s0 = stats[-1]
+        par = "1 GPU"
+        if n_gpus > 1:
+            par = (f"{n_gpus} GPUs ({'one process per GPU, RCCL' if multiproc else 'one process, RCCL'}): "
+                   "one slab of the file per GPU, one all-gather of the unique-word tables, merge "
+                   "loop on the union")
         line = {
-            "metric": "BPE train input MB/s (32k vocab)",
-            "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
+            "metric": "BPE train input MB/s (32k vocab), train_bpe(path) end to end",
+            "value": round(value, 2), "unit": "MB/s", "n_gpus": n_gpus, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
-            "data": "synthetic (bpe_synth_corpus_device OWT-like, random-free deterministic text)",
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic (bpe_synth_corpus_host OWT-like deterministic text, page-cache-warm file)",
             "config": {"workload": "train_bpe OWT-sized synthetic corpus, vocab 32000, "
                                    "special <|endoftext|> (BASELINE configs[2])",
-                       "bytes_per_gpu": n, "vocab_size": args.vocab, "merges": rounds,
-                       "seed": args.seed, "flavour": args.flavour,
-                       "parallelism": (f"corpus slabs x{world}, " + (
-                           "RCCL all-reduce of the pair deltas per merge round"
-                           if os.environ.get("BPE355_EXCHANGE") == "rounds" else
-                           "one RCCL all-gather of the unique-word tables, then every rank "
-                           "trains on their union")) if world > 1 else "1 GPU"},
-            "merges_per_s": round(rounds / (merge_ms / 1e3), 1) if merge_ms else None,
+                       "corpus_bytes": n, "vocab_size": args.vocab, "merges": rounds,
+                       "seed": args.seed, "flavour": args.flavour, "parallelism": par},
+            "merges_per_s": round(rounds / (avg["t_merge_ms"] / 1e3), 1) if avg["t_merge_ms"] else None,
+            "device_resident": device_resident,
+            "merge_loop": merge_loop,
             "encode": encode,
             "roofline": roofline,
             "cpu_baseline": cpu,
-            "phases_ms": {k: round(s0[k], 2) for k in ("t_prepare_ms", "t_count_ms", "t_exchange_ms",
-                                                        "t_words_ms", "t_merge_ms", "t_total_ms")},
+            "phases_ms": {k: round(s0[k], 2) for k in ("t_load_ms", "t_prepare_ms", "t_count_ms",
+                                                        "t_exchange_ms", "t_words_ms", "t_merge_ms",
+                                                        "t_total_ms")},
             "counters": {k: s0[k] for k in ("n_pretokens", "n_words", "n_exchanged_words",
                                             "n_pairs_final", "n_rebuilds", "n_rounds_device",
-                                            "n_rounds_host", "n_index_builds")},
+                                            "n_rounds_host", "n_index_builds", "n_trips")},
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+        if not args.keep_corpus:
+            path.unlink(missing_ok=True)
+    if multiproc:
         dist.barrier()
         comm.close()
         dist.destroy_process_group()

@@ -6,7 +6,9 @@
  * ctypes (binding: transformer-lm_amd/bpe_amd/_lib.py):
  *
  *   bpe_train_file / bpe_train_buffer   <- train_bpe(input_path, vocab_size, special_tokens)
- *                                          reference models/tokenizer/train.py:142-231
+ *                                          reference models/tokenizer/train.py:142-231 (its
+ *                                          OWT caller, perf/bpe/util.py:16, is one process:
+ *                                          n_gpus spreads that one call over the node's GPUs)
  *   bpe_tok_create                      <- Tokenizer.__init__(vocab, merges, special_tokens)
  *                                          reference models/tokenizer/tokenizer.py:12-38
  *   bpe_tok_encode                      <- Tokenizer.encode(text)
@@ -34,7 +36,7 @@
 extern "C" {
 #endif
 
-#define BPE355_ABI_VERSION 1
+#define BPE355_ABI_VERSION 2
 
 enum {
     BPE_OK = 0,
@@ -71,15 +73,29 @@ int bpe_comm_init_host(bpe_host_allreduce_fn fn, void* ctx, int nranks, int rank
 void bpe_comm_free(bpe_comm* comm);
 
 /* ---------------------------------------------------------------- training */
-/* train_bpe(input_path, vocab_size, special_tokens): reads the file like the reference's
- * open(path, "r", encoding="utf-8").read() (strict UTF-8, universal newlines).  With a comm,
- * each rank passes ITS slab of the corpus (slabs must be cut at pre-token boundaries, see
- * bpe_safe_split) and all ranks obtain the identical, global result. */
+/* train_bpe(input_path, vocab_size, special_tokens) (reference train.py:142-231): reads the
+ * file like the reference's open(path, "r", encoding="utf-8").read() (train.py:22: strict
+ * UTF-8, universal newlines; a pipe or FIFO is read to EOF).  The file is read by a pool of
+ * host threads into pinned staging and copied to HBM while the next piece is read.
+ * n_gpus: devices of THIS process to use (<= 0: every visible device).  With more than one,
+ * each device takes one slab of the file cut at safe split points, counts its words, one RCCL
+ * all-gather merges the word tables and the first device trains on the union.  The result is
+ * identical for every n_gpus.  Errors: BPE_E_IO (errno: ENOENT, EISDIR, ...), BPE_E_UTF8. */
 int bpe_train_file(const char* path, int vocab_size, const char* const* specials, int n_specials,
-                   bpe_comm* comm, bpe_result** out);
-/* same, raw file bytes in host memory */
+                   int n_gpus, bpe_result** out);
+/* One rank of a multi-process job (one process per GPU, comm from bpe_comm_init):
+ * split = 0: the file is this rank's slab (slabs cut at pre-token boundaries, bpe_safe_split);
+ * split = 1: the file is the whole corpus and this rank reads its share of it.
+ * All ranks obtain the identical, global result. */
+int bpe_train_file_comm(const char* path, int vocab_size, const char* const* specials,
+                        int n_specials, bpe_comm* comm, int split, bpe_result** out);
+/* train_bpe on raw file bytes in host memory (this rank's slab when comm is set) */
 int bpe_train_buffer(const uint8_t* data, size_t n, int vocab_size, const char* const* specials,
                      int n_specials, bpe_comm* comm, bpe_result** out);
+/* same, spread over n_gpus devices of this process as bpe_train_file does */
+int bpe_train_buffer_gpus(const uint8_t* data, size_t n, int vocab_size,
+                          const char* const* specials, int n_specials, int n_gpus,
+                          bpe_result** out);
 /* same, raw bytes already resident in device memory (d_data on the current device; it is not
  * modified).  stream may be NULL (the library's own stream). */
 int bpe_train_device(const uint8_t* d_data, size_t n, int vocab_size, const char* const* specials,
@@ -115,6 +131,8 @@ typedef struct {
     int64_t n_rounds_batched; /* rounds taken in trips of more than one merge */
     double t_exchange_ms;     /* multi-GPU word-table exchange (0 on one rank) */
     int64_t n_exchanged_words; /* local unique words of all ranks gathered (before dedupe) */
+    double t_load_ms;         /* file / host buffer -> HBM (0 when the corpus starts in HBM) */
+    int64_t n_gpus;           /* devices (ranks) that took part */
 } bpe_train_stats;
 int bpe_result_stats(const bpe_result* r, bpe_train_stats* out);
 void bpe_result_free(bpe_result* r);
@@ -184,6 +202,10 @@ size_t bpe_safe_split(const uint8_t* data, size_t n, size_t pos);
  * Every 4096-byte block boundary is a safe split point, so slabs of whole blocks shard it. */
 int bpe_synth_corpus_device(uint8_t* d_out, size_t n, uint64_t seed, int flavour,
                             uint64_t first_block, void* hip_stream);
+/* The same bytes written by the host (n_threads CPU threads), for the oracle side of the
+ * large parity checks; needs no device. */
+int bpe_synth_corpus_host(uint8_t* out, size_t n, uint64_t seed, int flavour,
+                          uint64_t first_block, int n_threads);
 
 #ifdef __cplusplus
 }

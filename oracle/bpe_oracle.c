@@ -432,20 +432,17 @@ typedef struct { strtab set; } ovocab;   /* insertion order == id order */
 static void vocab_add(ovocab* v, const uint8_t* p, size_t n) { st_intern(&v->set, p, n, NULL); }
 
 /* ------------------------------------------------------------ train */
-int oracle_train_text(const uint8_t* text, size_t n, int vocab_size,
-                      const uint8_t* specials_blob, size_t specials_n, oracle_blob* out) {
-    speclist sp;
-    int rc = parse_specials(specials_blob, specials_n, &sp);
-    if (rc) return rc;
+/* The merge loop of train.py:155-231 over a word -> count table (`words` is consumed). */
+static int train_words(strtab* words_in, const speclist* spp, int vocab_size, oracle_blob* out) {
+    const speclist sp = *spp;
+    strtab words = *words_in;
+    memset(words_in, 0, sizeof(*words_in));
 
     /* Vocab(special_tokens): specials in order, then the 256 bytes, deduplicated (vocab.py:2-12) */
     ovocab V; st_init(&V.set, 1 << 10);
     for (size_t i = 0; i < sp.count; i++) vocab_add(&V, sp.p[i], sp.n[i]);
     for (int b = 0; b < 256; b++) { uint8_t x = (uint8_t)b; vocab_add(&V, &x, 1); }
     long rounds = (long)vocab_size - (long)V.set.n;          /* train.py:183 */
-
-    strtab words;
-    count_words(text, n, &sp, &words);                        /* train.py:155 */
 
     trainer T; memset(&T, 0, sizeof(T));
     st_init(&T.tok, 1 << 10);
@@ -560,8 +557,83 @@ int oracle_train_text(const uint8_t* text, size_t n, int vocab_size,
     free(idx.s);
     free(T.pairs.s); free(T.hp.h);
     st_free(&T.tok); st_free(&words); st_free(&V.set);
-    free(sp.p); free(sp.n);
     return OR_OK;
+}
+
+int oracle_train_text(const uint8_t* text, size_t n, int vocab_size,
+                      const uint8_t* specials_blob, size_t specials_n, oracle_blob* out) {
+    speclist sp;
+    int rc = parse_specials(specials_blob, specials_n, &sp);
+    if (rc) return rc;
+    strtab words;
+    count_words(text, n, &sp, &words);                        /* train.py:155 */
+    rc = train_words(&words, &sp, vocab_size, out);
+    free(sp.p); free(sp.n);
+    return rc;
+}
+
+/* ------------------------------------------------------------ chunked counting */
+/* extract_subword_frequencies (train.py:16-28) over a corpus fed in pieces.  Each piece must
+ * end at a safe split point (a U+0020 between two ASCII non-space bytes, as
+ * bpe_safe_split and the synthetic generator's 4 KiB block boundaries are): cutting there
+ * changes neither the pre-token multiset nor the \r\n translation, so the sum of the
+ * pieces' counts equals the whole text's. */
+struct oracle_counter {
+    speclist sp;
+    uint8_t* sp_blob;
+    strtab words;
+};
+
+oracle_counter* oracle_counter_new(const uint8_t* specials_blob, size_t specials_n) {
+    oracle_counter* c = calloc(1, sizeof(*c));
+    c->sp_blob = malloc(specials_n ? specials_n : 1);
+    if (specials_n) memcpy(c->sp_blob, specials_blob, specials_n);
+    if (parse_specials(c->sp_blob, specials_n, &c->sp)) { free(c->sp_blob); free(c); return NULL; }
+    st_init(&c->words, 1 << 12);
+    return c;
+}
+
+int oracle_counter_feed(oracle_counter* c, const uint8_t* raw, size_t n, size_t* err_pos) {
+    uint8_t* text; size_t tn;
+    int rc = oracle_decode_text(raw, n, &text, &tn, err_pos);
+    if (rc) return rc;
+    count_ctx cc = {text, &c->words, &c->sp};
+    pretokenize(text, tn, count_span, &cc);
+    free(text);
+    return OR_OK;
+}
+
+int oracle_counter_absorb(oracle_counter* dst, const oracle_counter* src) {
+    for (size_t i = 0; i < src->words.n; i++) {
+        size_t id = st_intern(&dst->words, st_bytes(&src->words, i), src->words.len[i], NULL);
+        dst->words.val[id] += src->words.val[i];
+    }
+    return OR_OK;
+}
+
+int oracle_counter_words(const oracle_counter* c, oracle_blob* out) {
+    bbuf ob = {0};
+    bb_u32(&ob, (uint32_t)c->words.n);
+    for (size_t i = 0; i < c->words.n; i++) {
+        bb_u32(&ob, c->words.len[i]);
+        bb_put(&ob, st_bytes(&c->words, i), c->words.len[i]);
+        bb_u64(&ob, (uint64_t)c->words.val[i]);
+    }
+    out->data = ob.p; out->n = ob.n;
+    return OR_OK;
+}
+
+int oracle_counter_train(oracle_counter* c, int vocab_size, oracle_blob* out) {
+    int rc = train_words(&c->words, &c->sp, vocab_size, out);
+    st_init(&c->words, 1 << 12);
+    return rc;
+}
+
+void oracle_counter_free(oracle_counter* c) {
+    if (!c) return;
+    st_free(&c->words);
+    free(c->sp.p); free(c->sp.n); free(c->sp_blob);
+    free(c);
 }
 
 int oracle_train_raw(const uint8_t* raw, size_t n, int vocab_size, const uint8_t* specials_blob,

@@ -34,6 +34,16 @@ int oracle_pretokenize(const uint8_t* text, size_t n, oracle_blob* out);
 int oracle_encode(const uint8_t* vocab, size_t vocab_n, const uint8_t* merges, size_t merges_n,
                   const uint8_t* specials, size_t specials_n, int specials_is_none,
                   const uint8_t* text, size_t n, oracle_blob* out);
+/* Chunked word counting + training (large corpora that do not fit in memory twice).  Each
+ * fed piece must end at a safe split point (see bpe_oracle.c).  _train consumes the counts;
+ * _words returns them as oracle_word_counts does. */
+typedef struct oracle_counter oracle_counter;
+oracle_counter* oracle_counter_new(const uint8_t* specials, size_t specials_n);
+int oracle_counter_feed(oracle_counter* c, const uint8_t* raw, size_t n, size_t* err_pos);
+int oracle_counter_absorb(oracle_counter* dst, const oracle_counter* src);
+int oracle_counter_words(const oracle_counter* c, oracle_blob* out);
+int oracle_counter_train(oracle_counter* c, int vocab_size, oracle_blob* out);
+void oracle_counter_free(oracle_counter* c);
 void oracle_free(oracle_blob* b);
 
 #ifdef __cplusplus

@@ -53,6 +53,14 @@ def lib():
                                          ctypes.POINTER(ctypes.c_size_t),
                                          ctypes.POINTER(ctypes.c_size_t)]
         L.oracle_free.argtypes = [ctypes.POINTER(_Blob)]
+        L.oracle_counter_new.restype = ctypes.c_void_p
+        L.oracle_counter_new.argtypes = [u8p, ctypes.c_size_t]
+        L.oracle_counter_feed.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                          ctypes.POINTER(ctypes.c_size_t)]
+        L.oracle_counter_absorb.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_counter_words.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Blob)]
+        L.oracle_counter_train.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(_Blob)]
+        L.oracle_counter_free.argtypes = [ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -128,11 +136,7 @@ def decode_text(data: bytes) -> bytes:
     return res
 
 
-def word_counts(text: bytes, specials=()):
-    blob = _Blob()
-    sb = specials_blob(specials)
-    _check(lib().oracle_word_counts(text, len(text), sb, len(sb), ctypes.byref(blob)), "words")
-    data = _take(blob)
+def _parse_words(data: bytes):
     off = 4
     out = {}
     for _ in range(struct.unpack_from("<I", data, 0)[0]):
@@ -143,6 +147,50 @@ def word_counts(text: bytes, specials=()):
         out[w] = struct.unpack_from("<Q", data, off)[0]
         off += 8
     return out
+
+
+def word_counts(text: bytes, specials=()):
+    blob = _Blob()
+    sb = specials_blob(specials)
+    _check(lib().oracle_word_counts(text, len(text), sb, len(sb), ctypes.byref(blob)), "words")
+    return _parse_words(_take(blob))
+
+
+class Counter:
+    """extract_subword_frequencies (reference train.py:16-28) over a corpus fed in pieces that
+    each end at a safe split point; .train() then runs the merge loop (train.py:155-231).
+    feed() releases the GIL (ctypes), so one Counter per thread counts in parallel."""
+
+    def __init__(self, specials=()):
+        sb = specials_blob(specials)
+        self._h = lib().oracle_counter_new(sb, len(sb))
+        if not self._h:
+            raise ValueError("bad specials")
+
+    def feed(self, addr: int, n: int):
+        err = ctypes.c_size_t(0)
+        _check(lib().oracle_counter_feed(self._h, ctypes.c_void_p(addr), n, ctypes.byref(err)),
+               "feed", err.value)
+
+    def absorb(self, other: "Counter"):
+        _check(lib().oracle_counter_absorb(self._h, other._h), "absorb")
+
+    def words(self):
+        blob = _Blob()
+        _check(lib().oracle_counter_words(self._h, ctypes.byref(blob)), "words")
+        return _parse_words(_take(blob))
+
+    def train(self, vocab_size: int):
+        blob = _Blob()
+        _check(lib().oracle_counter_train(self._h, vocab_size, ctypes.byref(blob)), "train")
+        return parse_train_blob(_take(blob))
+
+    def close(self):
+        if self._h:
+            lib().oracle_counter_free(self._h)
+            self._h = None
+
+    __del__ = close
 
 
 def pretokenize(text: bytes):

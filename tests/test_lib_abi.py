@@ -23,7 +23,7 @@ def test_library_loads_and_exports_header():
     missing = [n for n in header_functions() if not hasattr(L, n)]
     assert not missing, missing
     assert set(header_functions()) == set(_lib.SYMBOLS)
-    assert L.bpe_abi_version() == 1
+    assert L.bpe_abi_version() == 2
 
 
 def test_no_cpu_fallback():

@@ -39,6 +39,7 @@ class TrainStats(ctypes.Structure):
         ("n_rounds_host", ctypes.c_int64), ("n_index_builds", ctypes.c_int64),
         ("n_trips", ctypes.c_int64), ("n_rounds_batched", ctypes.c_int64),
         ("t_exchange_ms", ctypes.c_double), ("n_exchanged_words", ctypes.c_int64),
+        ("t_load_ms", ctypes.c_double), ("n_gpus", ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -66,9 +67,15 @@ _SIGS = [
                                           ctypes.c_int, ctypes.POINTER(_P)]),
     ("bpe_comm_free", None, [_P]),
     ("bpe_train_file", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
-                                      ctypes.c_int, _P, ctypes.POINTER(_P)]),
+                                      ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
+    ("bpe_train_file_comm", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, _P,
+                                           ctypes.c_int, ctypes.POINTER(_P)]),
     ("bpe_train_buffer", ctypes.c_int, [_U8P, _SZ, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                         ctypes.c_int, _P, ctypes.POINTER(_P)]),
+    ("bpe_train_buffer_gpus", ctypes.c_int, [_U8P, _SZ, ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
+                                             ctypes.c_int, ctypes.POINTER(_P)]),
     ("bpe_train_device", ctypes.c_int, [_P, _SZ, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                         ctypes.c_int, _P, _P, ctypes.POINTER(_P)]),
     ("bpe_result_n_merges", ctypes.c_int64, [_P]),
@@ -96,6 +103,8 @@ _SIGS = [
     ("bpe_safe_split", _SZ, [_U8P, _SZ, _SZ]),
     ("bpe_synth_corpus_device", ctypes.c_int, [_P, _SZ, ctypes.c_uint64, ctypes.c_int,
                                                ctypes.c_uint64, _P]),
+    ("bpe_synth_corpus_host", ctypes.c_int, [_P, _SZ, ctypes.c_uint64, ctypes.c_int,
+                                             ctypes.c_uint64, ctypes.c_int]),
 ]
 SYMBOLS = [s[0] for s in _SIGS]
 

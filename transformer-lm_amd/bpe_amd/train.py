@@ -13,9 +13,25 @@ from typing import List
 
 from . import _lib
 
-__all__ = ["train_bpe", "train_bpe_bytes", "last_train_stats"]
+__all__ = ["train_bpe", "train_bpe_bytes", "train_bpe_device", "last_train_stats", "set_num_gpus",
+           "num_gpus"]
 
 _last_stats: dict = {}
+_num_gpus: int | None = None
+
+
+def set_num_gpus(n: int | None):
+    """GPUs of this process that train_bpe / train_bpe_bytes use (<= 0: every visible one;
+    None: back to the default, the BPE355_GPUS environment variable or 1).  The reference's
+    signature has no such argument (train.py:142), so it is a module setting."""
+    global _num_gpus
+    _num_gpus = None if n is None else int(n)
+
+
+def num_gpus() -> int:
+    if _num_gpus is not None:
+        return _num_gpus
+    return int(os.environ.get("BPE355_GPUS", "1"))
 
 
 def last_train_stats() -> dict:
@@ -32,17 +48,22 @@ def _finish(rc, res, what):
 
 
 def train_bpe(input_path: str | os.PathLike, vocab_size: int, special_tokens: List[str] = [],
-              comm=None):
+              comm=None, split_file: bool = False):
     """Train a byte-level BPE on the file at input_path (reference train.py:142-231).
 
-    comm: optional bpe_amd.dist.Communicator when each rank passes its own corpus slab.
+    Without comm: one process on num_gpus() devices (set_num_gpus / BPE355_GPUS).
+    comm: a bpe_amd.dist.Communicator (one process per GPU); the file is this rank's slab, or
+    with split_file=True the whole corpus, of which each rank reads its share.
     """
     L = _lib.lib()
     arr, n, _keep = _lib.c_strings(special_tokens)
     res = ctypes.c_void_p()
     path = os.fsencode(os.fspath(input_path))
-    rc = L.bpe_train_file(path, int(vocab_size), arr, n, comm.handle if comm else None,
-                          ctypes.byref(res))
+    if comm is not None:
+        rc = L.bpe_train_file_comm(path, int(vocab_size), arr, n, comm.handle, int(split_file),
+                                   ctypes.byref(res))
+    else:
+        rc = L.bpe_train_file(path, int(vocab_size), arr, n, num_gpus(), ctypes.byref(res))
     return _finish(rc, res, f"train_bpe({os.fspath(input_path)!r})")
 
 
@@ -51,8 +72,12 @@ def train_bpe_bytes(data: bytes, vocab_size: int, special_tokens: List[str] = []
     L = _lib.lib()
     arr, n, _keep = _lib.c_strings(special_tokens)
     res = ctypes.c_void_p()
-    rc = L.bpe_train_buffer(data, len(data), int(vocab_size), arr, n,
-                            comm.handle if comm else None, ctypes.byref(res))
+    if comm is not None or num_gpus() == 1:
+        rc = L.bpe_train_buffer(data, len(data), int(vocab_size), arr, n,
+                                comm.handle if comm else None, ctypes.byref(res))
+    else:
+        rc = L.bpe_train_buffer_gpus(data, len(data), int(vocab_size), arr, n, num_gpus(),
+                                     ctypes.byref(res))
     return _finish(rc, res, "train_bpe_bytes")
 
 

@@ -8,6 +8,7 @@
 #include <string>
 #include <vector>
 
+#include "drive.h"
 #include "internal.h"
 
 namespace bpe {
@@ -34,6 +35,7 @@ int guarded(F&& f) {
         return BPE_OK;
     } catch (const Error& e) {
         g_err = e.msg;
+        g_errno = e.sys_errno;
         return e.code;
     } catch (const std::bad_alloc&) {
         g_err = "host allocation failed";
@@ -168,38 +170,71 @@ int bpe_train_device(const uint8_t* d_data, size_t n, int vocab_size, const char
 
 int bpe_train_buffer(const uint8_t* data, size_t n, int vocab_size, const char* const* specials,
                      int n_specials, bpe_comm* comm, bpe_result** out) {
-    bpe::DevBuf<uint8_t> d;
-    int rc = bpe::guarded([&] {
+    return bpe::guarded([&] {
+        BPE_REQUIRE(out, BPE_E_ARG, "out is NULL");
+        *out = nullptr;
         BPE_REQUIRE(!n || data, BPE_E_ARG, "data is NULL");
         bpe::DeviceGuard::require();
-        d.alloc(std::max<size_t>(n, 1));
-        if (n) BPE_HIP(hipMemcpy(d.p, data, n, hipMemcpyHostToDevice));
+        auto sp = bpe::to_specials(specials, n_specials);
+        const bpe::Source src = bpe::Source::memory(data, n);
+        bpe::TrainOutput to;
+        if (comm) bpe::train_source_comm(src, false, vocab_size, sp, comm->impl.get(), to);
+        else bpe::train_source(src, vocab_size, sp, 1, to);
+        auto r = std::make_unique<bpe_result>();
+        finish_result(to, sp, r.get());
+        *out = r.release();
     });
-    if (rc) return rc;
-    return train_common(d.p, n, vocab_size, specials, n_specials, comm, nullptr, out);
+}
+
+int bpe_train_buffer_gpus(const uint8_t* data, size_t n, int vocab_size, const char* const* specials,
+                          int n_specials, int n_gpus, bpe_result** out) {
+    return bpe::guarded([&] {
+        BPE_REQUIRE(out, BPE_E_ARG, "out is NULL");
+        *out = nullptr;
+        BPE_REQUIRE(!n || data, BPE_E_ARG, "data is NULL");
+        bpe::DeviceGuard::require();
+        auto sp = bpe::to_specials(specials, n_specials);
+        const bpe::Source src = bpe::Source::memory(data, n);
+        bpe::TrainOutput to;
+        bpe::train_source(src, vocab_size, sp, n_gpus, to);
+        auto r = std::make_unique<bpe_result>();
+        finish_result(to, sp, r.get());
+        *out = r.release();
+    });
 }
 
 int bpe_train_file(const char* path, int vocab_size, const char* const* specials, int n_specials,
-                   bpe_comm* comm, bpe_result** out) {
-    std::string data;
-    int rc = bpe::guarded([&] {
+                   int n_gpus, bpe_result** out) {
+    return bpe::guarded([&] {
+        BPE_REQUIRE(out, BPE_E_ARG, "out is NULL");
+        *out = nullptr;
         BPE_REQUIRE(path, BPE_E_ARG, "path is NULL");
-        FILE* f = std::fopen(path, "rb");
-        if (!f) {
-            bpe::g_errno = errno;
-            throw bpe::Error{BPE_E_IO, std::string("cannot open ") + path + ": " + std::strerror(errno)};
-        }
-        std::fseek(f, 0, SEEK_END);
-        const long sz = std::ftell(f);
-        std::fseek(f, 0, SEEK_SET);
-        data.resize(sz > 0 ? (size_t)sz : 0);
-        const size_t got = data.empty() ? 0 : std::fread(&data[0], 1, data.size(), f);
-        std::fclose(f);
-        BPE_REQUIRE(got == data.size(), BPE_E_IO, std::string("short read on ") + path);
+        auto sp = bpe::to_specials(specials, n_specials);
+        const bpe::Source src = bpe::Source::open_path(path);   // FileNotFoundError before any GPU check
+        bpe::DeviceGuard::require();
+        bpe::TrainOutput to;
+        bpe::train_source(src, vocab_size, sp, n_gpus, to);
+        auto r = std::make_unique<bpe_result>();
+        finish_result(to, sp, r.get());
+        *out = r.release();
     });
-    if (rc) return rc;
-    return bpe_train_buffer(reinterpret_cast<const uint8_t*>(data.data()), data.size(), vocab_size,
-                            specials, n_specials, comm, out);
+}
+
+int bpe_train_file_comm(const char* path, int vocab_size, const char* const* specials, int n_specials,
+                        bpe_comm* comm, int split, bpe_result** out) {
+    return bpe::guarded([&] {
+        BPE_REQUIRE(out, BPE_E_ARG, "out is NULL");
+        *out = nullptr;
+        BPE_REQUIRE(path, BPE_E_ARG, "path is NULL");
+        auto sp = bpe::to_specials(specials, n_specials);
+        const bpe::Source src = bpe::Source::open_path(path);
+        bpe::DeviceGuard::require();
+        bpe::TrainOutput to;
+        bpe::train_source_comm(src, split != 0, vocab_size, sp, comm ? comm->impl.get() : nullptr, to);
+        auto r = std::make_unique<bpe_result>();
+        finish_result(to, sp, r.get());
+        *out = r.release();
+    });
 }
 
 int64_t bpe_result_n_merges(const bpe_result* r) { return r ? r->n_merges : -1; }

@@ -17,6 +17,7 @@ void set_error(int code, const std::string& msg);
 struct Error {
     int code;
     std::string msg;
+    int sys_errno = 0;      // for BPE_E_IO: errno, reported by bpe_last_errno on the calling thread
 };
 
 #define BPE_HIP(expr)                                                                     \

@@ -5,7 +5,9 @@
 // exercised by several processes that share one GPU (tests).
 #include <rccl/rccl.h>
 
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <memory>
 #include <vector>
 
@@ -67,7 +69,58 @@ struct HostComm final : Comm {
     }
 };
 
+// Ranks that are threads of one process (tests of the multi-device driver on a one-GPU box:
+// several ranks may share a device, which RCCL refuses).  A generation-counted barrier: the sum
+// of an operation is published when the last rank arrives; a rank cannot start the next
+// operation's sum before every rank has taken this one's result, because that needs them all.
+struct InProcShared {
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    std::vector<int64_t> acc, result;
+};
+
+struct InProcComm final : Comm {
+    std::shared_ptr<InProcShared> sh;
+    std::vector<int64_t> h;
+    InProcComm(std::shared_ptr<InProcShared> s, int n, int r, int dev) : sh(std::move(s)) {
+        nranks = n;
+        rank = r;
+        device = dev;
+    }
+    void allreduce_i64(int64_t* d_buf, size_t count, hipStream_t stream) override {
+        if (count == 0) return;
+        h.resize(count);
+        BPE_HIP(hipMemcpyAsync(h.data(), d_buf, count * 8, hipMemcpyDeviceToHost, stream));
+        BPE_HIP(hipStreamSynchronize(stream));
+        {
+            std::unique_lock<std::mutex> lk(sh->m);
+            const uint64_t g = sh->gen;
+            if (sh->arrived == 0) sh->acc.assign(count, 0);
+            BPE_REQUIRE(sh->acc.size() == count, BPE_E_RCCL, "in-process all-reduce: ranks disagree on the size");
+            for (size_t i = 0; i < count; ++i) sh->acc[i] += h[i];
+            if (++sh->arrived == nranks) {
+                sh->result.swap(sh->acc);
+                sh->arrived = 0;
+                ++sh->gen;
+                sh->cv.notify_all();
+            } else {
+                sh->cv.wait(lk, [&] { return sh->gen != g; });
+            }
+            h = sh->result;
+        }
+        BPE_HIP(hipMemcpyAsync(d_buf, h.data(), count * 8, hipMemcpyHostToDevice, stream));
+        BPE_HIP(hipStreamSynchronize(stream));
+    }
+};
+
 }  // namespace
+
+std::shared_ptr<void> make_inproc_group() { return std::make_shared<InProcShared>(); }
+std::unique_ptr<Comm> make_inproc_comm(const std::shared_ptr<void>& group, int nranks, int rank, int device) {
+    return std::make_unique<InProcComm>(std::static_pointer_cast<InProcShared>(group), nranks, rank, device);
+}
 
 std::unique_ptr<Comm> make_rccl_comm(const uint8_t id[128], int nranks, int rank, int device) {
     return std::make_unique<RcclComm>(id, nranks, rank, device);

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -42,6 +43,47 @@ struct WordCounts {
 void count_words(const uint8_t* d_text, size_t n, WordCounts& wc, hipStream_t stream,
                  float* kernel_ms);
 
+// The same count over a text that arrives in segments [lo, hi) cut at safe split points
+// (text.hip): range() enqueues one launch per segment into one table; finish() returns false
+// when the table overflowed (then recount everything with a larger table).
+struct CountPass {
+    WordCounts wc;
+    DevBuf<unsigned> status;
+    DevBuf<unsigned long long> ntok, fill;
+    const uint8_t* text = nullptr;
+    size_t total = 0;
+    hipStream_t s = nullptr;
+    bool timed = false;
+    const unsigned long long* gate = nullptr;   // device flag: skip the launches unless ~0
+    double kernel_ms = 0;        // summed device time of the launches (when timed)
+    std::vector<hipEvent_t> ev;
+    static size_t initial_cap(size_t n);
+    void begin(const uint8_t* d_text, size_t n, size_t cap, hipStream_t stream, bool timing);
+    void range(size_t lo, size_t hi);
+    bool finish();
+    ~CountPass();
+};
+
+// Strict UTF-8 validation by segment (the first bad byte, and whether any \r is present).
+struct ValidatePass {
+    DevBuf<unsigned long long> flags;
+    const uint8_t* text = nullptr;
+    size_t total = 0;
+    hipStream_t s = nullptr;
+    void begin(const uint8_t* d_text, size_t n, hipStream_t stream);
+    void range(size_t lo, size_t hi);
+    void finish(unsigned long long* err_pos, bool* has_cr);   // err_pos ~0: none
+};
+
+// A corpus already validated and counted (the overlapped file path, drive.hip)
+struct Prepared {
+    const uint8_t* text = nullptr;
+    size_t n = 0;
+    WordCounts wc;
+    double t_prepare_ms = 0, t_count_ms = 0, load_ms = 0;
+    float count_kernel_ms = 0;
+};
+
 // ---------------------------------------------------------------- multi-GPU word exchange
 // Replace this rank's word table by the union of every rank's (counts summed), whose words'
 // bytes live in `all` (exchange.hip).  One all-gather; afterwards no rank needs the others.
@@ -55,9 +97,19 @@ struct TrainOutput {
     std::vector<std::pair<std::string, std::string>> merges;     // byte pairs, in order
     bpe_train_stats stats{};
 };
+struct TrainOpts {
+    size_t slab_offset = 0;     // this slab's first byte in the whole corpus (error positions)
+    bool merge_loop = true;     // false: stop after the word exchange (another rank trains)
+    bool has_pending = false;   // an error this rank hit before training (e.g. reading its
+    Error pending{0, ""};       // slab); raised by every rank together, before any collective
+};
+std::unique_ptr<Comm> make_rccl_comm(const uint8_t id[128], int nranks, int rank, int device);
+// ranks that are threads of one process, possibly sharing a device (tests; comm.hip)
+std::shared_ptr<void> make_inproc_group();
+std::unique_ptr<Comm> make_inproc_comm(const std::shared_ptr<void>& group, int nranks, int rank, int device);
 void train_on_device(const uint8_t* d_raw, size_t n, int vocab_size,
                      const std::vector<std::string>& specials, Comm* comm, hipStream_t stream,
-                     TrainOutput& out);
+                     TrainOutput& out, const TrainOpts& opt = TrainOpts{}, Prepared* pre = nullptr);
 
 bool timing_enabled();
 

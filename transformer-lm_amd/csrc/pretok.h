@@ -67,6 +67,7 @@ __device__ __forceinline__ int class_at(const Src& s, Idx i, int* len) {
              (s[i + 3] & 0x3Fu);
         *len = 4;
     }
+    cp = cp < 0x110000u ? cp : 0x10FFFFu;   // never past the tables, even on unvalidated bytes
     const unsigned pg = BPE_UC_PAGE[cp >> 8];
     return (BPE_UC_BITS[pg][(cp & 255u) >> 2] >> ((cp & 3u) * 2)) & 3;
 }

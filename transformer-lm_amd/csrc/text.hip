@@ -64,11 +64,15 @@ __device__ __forceinline__ bool byte_ok(const uint8_t* __restrict__ s, size_t n,
 
 constexpr int kValidateBytes = 16;
 
-__global__ void k_validate(const uint8_t* __restrict__ s, size_t n,
+// Units [u0, u1) of kValidateBytes (global positions: unit u is s[16u, 16u + 16)), with the
+// text taken to end at n.  A segment of a corpus that is still arriving validates its units
+// with n = the segment's end, a safe split point: its last byte is ASCII, so no well-formed
+// sequence crosses it and an ill-formed one is ill-formed whatever follows.
+__global__ void k_validate(const uint8_t* __restrict__ s, size_t n, size_t u0, size_t u1,
                            unsigned long long* __restrict__ err_pos, unsigned* __restrict__ has_cr) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t t = u0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t lo = t * kValidateBytes;
-    if (lo >= n) return;
+    if (t >= u1 || lo >= n) return;
     bool cr = false;
     if (lo + kValidateBytes <= n && (((uintptr_t)(s + lo)) & 15) == 0) {
         const uint4 v = *reinterpret_cast<const uint4*>(s + lo);
@@ -178,7 +182,7 @@ const uint8_t* prepare_text(const uint8_t* d_in, size_t n, DevBuf<uint8_t>& scra
     BPE_HIP(hipMemcpyAsync(flags.p, h_init, sizeof(h_init), hipMemcpyHostToDevice, stream));
     const size_t threads = (n + kValidateBytes - 1) / kValidateBytes;
     hipLaunchKernelGGL(k_validate, dim3(ceil_div(threads, 256)), dim3(256), 0, stream, d_in, n,
-                       flags.p, reinterpret_cast<unsigned*>(flags.p + 1));
+                       (size_t)0, threads, flags.p, reinterpret_cast<unsigned*>(flags.p + 1));
     BPE_HIP(hipGetLastError());
     unsigned long long h[2];
     BPE_HIP(hipMemcpyAsync(h, flags.p, sizeof(h), hipMemcpyDeviceToHost, stream));
@@ -231,13 +235,21 @@ constexpr unsigned kKeep = 2;        // an entry stays if it was hit this often 
 // published only after its bytes are written); the rest, and cache conflicts, go to the global
 // table.  The cache is flushed once at the end.  If the table passes max_fill keys, every
 // workgroup stops early and the host recounts with a larger table.
+//
+// A launch counts the text [lo, n) (lo = 0, or a safe split point: a token start) over the
+// kChunk-aligned chunks chunk0 .. chunk0 + n_chunks - 1, so a corpus arriving in segments is
+// counted segment by segment into one table, with the same tokens as one pass over it.
 template <bool kAligned>
-__global__ void __launch_bounds__(256, 3) k_count_words(const uint8_t* __restrict__ s, size_t n,
-                                                     size_t n_chunks, unsigned long long* __restrict__ kv,
+__global__ void __launch_bounds__(256, 3) k_count_words(const uint8_t* __restrict__ s, size_t lo, size_t n,
+                                                     size_t chunk0, size_t n_chunks, unsigned long long* __restrict__ kv,
                                                      unsigned long long* __restrict__ pos, size_t mask, unsigned long long max_fill,
                                                      unsigned long long* __restrict__ fill,
                                                      unsigned* __restrict__ status,
-                                                     unsigned long long* __restrict__ n_tok, int mode) {
+                                                     unsigned long long* __restrict__ n_tok, int mode,
+                                                     const unsigned long long* __restrict__ gate) {
+    // a segment is counted only behind a clean validation of everything before it (gate: the
+    // first bad byte, ~0 = none): ill-formed UTF-8 is never scanned
+    if (gate && *gate != ~0ULL) return;
     __shared__ unsigned long long c_key[kCache];
     __shared__ uint64_t c_lo[kCache], c_hi[kCache];
     __shared__ unsigned c_cnt[kCache];
@@ -298,7 +310,7 @@ __global__ void __launch_bounds__(256, 3) k_count_words(const uint8_t* __restric
             inserted += global_add(s, s, gpos, len, 0, 0, hash_word(s, gpos, len), 1, kv, pos, mask, status);
         }
     };
-    if (blockIdx.x < n_chunks) stage_fetch<kAligned>(pre, s, n, (size_t)blockIdx.x * kChunk, tid);
+    if (blockIdx.x < n_chunks) stage_fetch<kAligned>(pre, s, n, (chunk0 + blockIdx.x) * kChunk, tid);
     for (size_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
         __syncthreads();   // the previous chunk's scan is done with buf
         stage_store(pre, tid);
@@ -309,9 +321,10 @@ __global__ void __launch_bounds__(256, 3) k_count_words(const uint8_t* __restric
             break;
         }
         if (c + gridDim.x < n_chunks)   // in flight during the scan
-            stage_fetch<kAligned>(pre, s, n, (c + gridDim.x) * kChunk, tid);
+            stage_fetch<kAligned>(pre, s, n, (chunk0 + c + gridDim.x) * kChunk, tid);
 
-        const size_t base = c * kChunk;
+        const size_t base = (chunk0 + c) * kChunk;
+        const uint32_t rlo = lo > base ? (uint32_t)(lo - base) : 0u;   // the text starts here
         const size_t rem = n - base;
         const bool text_ends = rem <= (size_t)kWin;          // the window reaches the end of text
         const uint32_t nloc = text_ends ? (uint32_t)rem : (uint32_t)kWin;
@@ -320,7 +333,7 @@ __global__ void __launch_bounds__(256, 3) k_count_words(const uint8_t* __restric
         // window only (kNotFound: it lies past the window)
         const LdsText L{};
         auto find_start = [&](uint32_t r) -> uint32_t {
-            if (c == 0 && r == 0) return 0;
+            if (base <= lo && r <= rlo) return rlo;   // the text (or segment) start
             if (r >= nloc) return text_ends ? nloc : kNotFound;
             if (r == 0) {   // position 0's left neighbour is the previous chunk's last byte
                 if (nloc > 1 && L[0] == 0x20 && ascii_nonspace(s[base - 1]) && ascii_nonspace(L[1]))
@@ -346,7 +359,7 @@ __global__ void __launch_bounds__(256, 3) k_count_words(const uint8_t* __restric
             // slow path (rare): no safe point in the rest of the window -- scan global memory
             // from r0 to the first safe point past this thread's nominal end
             const size_t hi = base + (size_t)tid * 64 + 64;
-            for (size_t p = base + r0; p < n;) {
+            for (size_t p = base + r0; p < n;) {   // (tokens end at n: a safe point or the end)
                 if (p >= hi && is_safe_point(s, n, p)) break;
                 const size_t e = token_end(s, n, p);
                 count_token(s, p, e - p, p);
@@ -417,70 +430,153 @@ __global__ void __launch_bounds__(256, 3) k_count_words(const uint8_t* __restric
     }
 }
 
-void count_words(const uint8_t* d_text, size_t n, WordCounts& wc, hipStream_t stream,
-                 float* kernel_ms) {
-    BPE_REQUIRE(n < (1ULL << 40) - 1, BPE_E_LIMIT, "corpus slab larger than 1 TiB");
-    // first guess ~1 slot per KiB of a large corpus (7.4 M words in 11.9 GB of OWT-like text:
-    // load 0.46), 1 per 16 bytes below 64 MiB (small texts have many more unique words per
-    // byte); the kernel stops early past load 1/2 and the count reruns with 4x the slots
-    size_t cap = next_pow2(std::max<size_t>(1 << 16, n < (1u << 26) ? n / 16 : n / 1024));
-    DevBuf<unsigned> status(1);
-    DevBuf<unsigned long long> ntok(3), fill(1);
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (kernel_ms) {
-        BPE_HIP(hipEventCreate(&e0));
-        BPE_HIP(hipEventCreate(&e1));
-    }
-    const size_t n_chunks = (n + kChunk - 1) / kChunk;
-    const bool aligned = (reinterpret_cast<uintptr_t>(d_text) & 15u) == 0;
-    // one resident wave of persistent workgroups: every workgroup takes the same number of
-    // chunks, so a second, queued wave would nearly double the time
+namespace {
+
+// per-launch grid of the persistent counter: one resident wave of workgroups (every workgroup
+// takes the same number of chunks, so a second, queued wave would nearly double the time)
+unsigned count_grid(size_t n_chunks, bool aligned) {
     auto kern = aligned ? k_count_words<true> : k_count_words<false>;
-    int per_cu = 0, dev = 0, n_cu = 0;
-    BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, kPadded));
-    BPE_HIP(hipGetDevice(&dev));
-    BPE_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    static int per_cu = 0, n_cu = 0;
+    if (!per_cu) {
+        int dev = 0;
+        BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, kPadded));
+        BPE_HIP(hipGetDevice(&dev));
+        BPE_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
     unsigned grid = (unsigned)std::min<size_t>(std::max<size_t>(n_chunks, 1),
                                                (size_t)std::max(1, per_cu) * std::max(1, n_cu));
     if (const char* e = std::getenv("BPE355_STREAM_WG"))   // test knob: fewer workgroups, each
         grid = std::max(1u, std::min(grid, (unsigned)std::atoi(e)));   // streaming many chunks
+    return grid;
+}
+
+// first guess ~1 slot per KiB of a large corpus (7.4 M words in 11.9 GB of OWT-like text:
+// load 0.46), 1 per 16 bytes below 64 MiB (small texts have many more unique words per byte);
+// the kernel stops early past load 1/2 and the count reruns with 4x the slots
+size_t first_cap(size_t n) {
+    size_t cap = next_pow2(std::max<size_t>(1 << 16, n < (1u << 26) ? n / 16 : n / 1024));
+    if (const char* e = std::getenv("BPE355_WORD_CAP_LOG2"))   // test knob: force the regrow path
+        cap = size_t(1) << std::max(8, std::min(34, std::atoi(e)));
+    return cap;
+}
+
+}  // namespace
+
+void CountPass::begin(const uint8_t* d_text, size_t n, size_t cap, hipStream_t stream, bool timing) {
+    BPE_REQUIRE(n < (1ULL << 40) - 1, BPE_E_LIMIT, "corpus slab larger than 1 TiB");
+    text = d_text;
+    total = n;
+    s = stream;
+    timed = timing;
+    kernel_ms = 0;
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    ev.clear();
+    if (!status.p) {
+        status.alloc(1);
+        ntok.alloc(3);
+        fill.alloc(1);
+    }
+    wc.kv.alloc(2 * cap);
+    wc.pos.alloc(cap);
+    wc.cap = cap;
+    BPE_HIP(hipMemsetAsync(wc.kv.p, 0, wc.kv.bytes(), s));
+    BPE_HIP(hipMemsetAsync(status.p, 0, 4, s));
+    BPE_HIP(hipMemsetAsync(ntok.p, 0, 24, s));
+    BPE_HIP(hipMemsetAsync(fill.p, 0, 8, s));
+}
+
+void CountPass::range(size_t lo, size_t hi) {
+    if (hi <= lo) return;
+    const size_t c0 = lo / kChunk, c1 = (hi + kChunk - 1) / kChunk;
+    const bool aligned = (reinterpret_cast<uintptr_t>(text) & 15u) == 0;
+    auto kern = aligned ? k_count_words<true> : k_count_words<false>;
+    const unsigned grid = count_grid(c1 - c0, aligned);
     // analysis knob: 1 = scan only, 2 = LDS word cache only (counts incomplete: timing only)
     static const int count_mode = std::getenv("BPE355_COUNT_MODE") ? std::atoi(std::getenv("BPE355_COUNT_MODE")) : 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (timed) {
+        BPE_HIP(hipEventCreate(&e0));
+        BPE_HIP(hipEventCreate(&e1));
+        ev.push_back(e0);
+        ev.push_back(e1);
+    }
+    // timed launch: the events are stamped by the kernel's own dispatch packet (the interval
+    // rocprofv3 reports), not by marker packets around it
+    hipExtLaunchKernelGGL(kern, dim3(grid), dim3(256), kPadded, s, e0, e1, 0, text, lo, hi, c0, c1 - c0,
+                          wc.kv.p, wc.pos.p, wc.cap - 1, (unsigned long long)(wc.cap / 2), fill.p, status.p,
+                          ntok.p, count_mode, gate);
+    BPE_HIP(hipGetLastError());
+}
+
+bool CountPass::finish() {
+    unsigned st = 0;
+    BPE_HIP(hipMemcpyAsync(&st, status.p, 4, hipMemcpyDeviceToHost, s));
+    BPE_HIP(hipMemcpyAsync(&wc.n_pretokens, ntok.p, 8, hipMemcpyDeviceToHost, s));
+    BPE_HIP(hipStreamSynchronize(s));
+    if (st & 2u) throw Error{BPE_E_LIMIT, "a pre-token is longer than 16 MiB"};
+    for (size_t i = 0; i + 1 < ev.size(); i += 2) {
+        float ms = 0;
+        BPE_HIP(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+        kernel_ms += ms;
+    }
+    if (std::getenv("BPE355_TRACE")) {
+        unsigned long long d[3];
+        BPE_HIP(hipMemcpy(d, ntok.p, 24, hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "[bpe355] count: cap %zu pretokens %llu cache-miss %llu long %llu launches %zu\n",
+                     wc.cap, d[0], d[1], d[2], ev.size() / 2);
+    }
+    return !(st & 1u);
+}
+
+CountPass::~CountPass() {
+    for (auto& e : ev) (void)hipEventDestroy(e);
+}
+
+size_t CountPass::initial_cap(size_t n) { return first_cap(n); }
+
+void count_words(const uint8_t* d_text, size_t n, WordCounts& wc, hipStream_t stream,
+                 float* kernel_ms) {
+    CountPass cp;
+    size_t cap = first_cap(n);
     for (int attempt = 0;; ++attempt) {
-        wc.kv.alloc(2 * cap);
-        wc.pos.alloc(cap);
-        wc.cap = cap;
-        BPE_HIP(hipMemsetAsync(wc.kv.p, 0, wc.kv.bytes(), stream));
-        BPE_HIP(hipMemsetAsync(status.p, 0, 4, stream));
-        BPE_HIP(hipMemsetAsync(ntok.p, 0, 24, stream));
-        BPE_HIP(hipMemsetAsync(fill.p, 0, 8, stream));
-        if (n) {
-            // timed launch: the events are stamped by the kernel's own dispatch packet (the
-            // interval rocprofv3 reports), not by marker packets around it
-            hipExtLaunchKernelGGL(kern, dim3(grid), dim3(256), kPadded, stream,
-                                  kernel_ms ? e0 : nullptr, kernel_ms ? e1 : nullptr, 0,
-                                  d_text, n, n_chunks, wc.kv.p, wc.pos.p, cap - 1,
-                                  (unsigned long long)(cap / 2), fill.p, status.p, ntok.p, count_mode);
-            BPE_HIP(hipGetLastError());
-        }
-        unsigned st = 0;
-        BPE_HIP(hipMemcpyAsync(&st, status.p, 4, hipMemcpyDeviceToHost, stream));
-        BPE_HIP(hipMemcpyAsync(&wc.n_pretokens, ntok.p, 8, hipMemcpyDeviceToHost, stream));
-        BPE_HIP(hipStreamSynchronize(stream));
-        if (st & 2u) throw Error{BPE_E_LIMIT, "a pre-token is longer than 16 MiB"};
-        if (kernel_ms && n) BPE_HIP(hipEventElapsedTime(kernel_ms, e0, e1));
-        if (std::getenv("BPE355_TRACE")) {
-            unsigned long long d[3];
-            BPE_HIP(hipMemcpy(d, ntok.p, 24, hipMemcpyDeviceToHost));
-            std::fprintf(stderr, "[bpe355] count: cap %zu pretokens %llu cache-miss %llu long %llu grid %u\n",
-                         cap, d[0], d[1], d[2], grid);
-        }
-        if (!(st & 1u)) break;
-        BPE_REQUIRE(attempt < 6, BPE_E_NOMEM, "word table overflow");
+        cp.begin(d_text, n, cap, stream, kernel_ms != nullptr);
+        cp.range(0, n);
+        if (cp.finish()) break;
+        BPE_REQUIRE(attempt < 8, BPE_E_NOMEM, "word table overflow");
         cap *= 4;  // the table filled up: grow and recount
     }
-    if (e0) (void)hipEventDestroy(e0);
-    if (e1) (void)hipEventDestroy(e1);
+    if (kernel_ms) *kernel_ms = (float)cp.kernel_ms;
+    wc = std::move(cp.wc);
+}
+
+// ------------------------------------------------------------------ validation by segment
+void ValidatePass::begin(const uint8_t* d_text, size_t n, hipStream_t stream) {
+    text = d_text;
+    total = n;
+    s = stream;
+    if (!flags.p) flags.alloc(2);
+    const unsigned long long h_init[2] = {~0ULL, 0ULL};
+    BPE_HIP(hipMemcpyAsync(flags.p, h_init, sizeof(h_init), hipMemcpyHostToDevice, s));
+    BPE_HIP(hipStreamSynchronize(s));
+}
+
+void ValidatePass::range(size_t lo, size_t hi) {
+    // units [lo / 16, hi / 16) against a text that ends at hi; the last segment (hi = total)
+    // takes the partial unit too
+    const size_t u0 = lo / kValidateBytes;
+    const size_t u1 = hi == total ? (hi + kValidateBytes - 1) / kValidateBytes : hi / kValidateBytes;
+    if (u1 <= u0) return;
+    hipLaunchKernelGGL(k_validate, dim3(ceil_div(u1 - u0, 256)), dim3(256), 0, s, text, hi, u0, u1, flags.p,
+                       reinterpret_cast<unsigned*>(flags.p + 1));
+    BPE_HIP(hipGetLastError());
+}
+
+void ValidatePass::finish(unsigned long long* err_pos, bool* has_cr) {
+    unsigned long long h[2];
+    BPE_HIP(hipMemcpyAsync(h, flags.p, sizeof(h), hipMemcpyDeviceToHost, s));
+    BPE_HIP(hipStreamSynchronize(s));
+    *err_pos = h[0];
+    *has_cr = (unsigned)h[1] != 0;
 }
 
 }  // namespace bpe

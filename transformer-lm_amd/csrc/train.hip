@@ -2540,7 +2540,11 @@ void MergeLoop<TokT>::run() {
         BPE_HIP(hipStreamSynchronize(s_));
         for (int64_t v : ml) max_len_ = std::max<unsigned>(max_len_, (unsigned)v);
     }
-    alloc_pairs(size_t(1) << 22);
+    // test knob BPE355_PAIR_CAP_LOG2: a smaller first table (>= 2^18 holds the 65 536 byte pairs
+    // at load 1/2), so moderate corpora exercise grow_pairs / k_rehash as the bench corpus does
+    int pair_log2 = 22;
+    if (const char* e = std::getenv("BPE355_PAIR_CAP_LOG2")) pair_log2 = std::max(18, std::min(30, std::atoi(e)));
+    alloc_pairs(size_t(1) << pair_log2);
     const unsigned n_single_keep = hs_.n_single;
     memset(&hs_, 0, sizeof(hs_));
     hs_.n_single = n_single_keep;
@@ -2926,16 +2930,85 @@ void MergeLoop<TokT>::exhaustion() {
 
 }  // namespace
 
+namespace {
+
+// Several ranks: an error one rank met before the first collective (reading or validating its
+// slab) is raised by every rank, so none waits in a collective another never reaches.  The
+// error of the earliest slab wins; a UTF-8 position is reported in whole-corpus bytes.
+void agree_on_errors(Comm* comm, const Error* mine, hipStream_t stream) {
+    const int R = comm->nranks;
+    std::vector<int64_t> v(3 * (size_t)R, 0);
+    if (mine) {
+        v[3 * comm->rank] = mine->code;
+        v[3 * comm->rank + 1] = mine->sys_errno;
+        const size_t p = mine->msg.find("position ");
+        v[3 * comm->rank + 2] = p == std::string::npos ? 0 : std::stoll(mine->msg.substr(p + 9));
+    }
+    DevBuf<int64_t> d(v.size());
+    BPE_HIP(hipMemcpyAsync(d.p, v.data(), v.size() * 8, hipMemcpyHostToDevice, stream));
+    comm->allreduce_i64(d.p, v.size(), stream);
+    BPE_HIP(hipMemcpyAsync(v.data(), d.p, v.size() * 8, hipMemcpyDeviceToHost, stream));
+    BPE_HIP(hipStreamSynchronize(stream));
+    for (int r = 0; r < R; ++r) {
+        const int code = (int)v[3 * r];
+        if (!code) continue;
+        if (r == comm->rank && mine) throw *mine;
+        if (code == BPE_E_UTF8)
+            throw Error{code, "'utf-8' codec can't decode byte at position " + std::to_string(v[3 * r + 2])};
+        throw Error{code, "rank " + std::to_string(r) + " failed before training (code " + std::to_string(code) + ")",
+                    (int)v[3 * r + 1]};
+    }
+}
+
+}  // namespace
+
 void train_on_device(const uint8_t* d_raw, size_t n, int vocab_size,
                      const std::vector<std::string>& specials, Comm* comm, hipStream_t stream,
-                     TrainOutput& out) {
+                     TrainOutput& out, const TrainOpts& opt, Prepared* pre) {
     const auto t0 = std::chrono::steady_clock::now();
     out = TrainOutput{};
     DevBuf<uint8_t> scratch;
     size_t tn = 0;
-    const uint8_t* text = prepare_text(d_raw, n, scratch, &tn, stream);
-    out.stats.t_prepare_ms = ms_since(t0);
-    out.stats.n_bytes = (int64_t)tn;
+    const uint8_t* text = nullptr;
+    const bool several = comm && comm->nranks > 1;
+    WordCounts wc;
+    float count_ms = 0;
+    std::chrono::steady_clock::time_point t1;
+    {
+        Error err{0, ""};
+        bool failed = opt.has_pending;
+        if (failed) err = opt.pending;
+        if (!failed && pre) {   // validated and counted while the corpus arrived (drive.hip)
+            text = pre->text;
+            tn = pre->n;
+            wc = std::move(pre->wc);
+            count_ms = pre->count_kernel_ms;
+            out.stats.t_prepare_ms = pre->t_prepare_ms;
+            out.stats.n_bytes = (int64_t)tn;
+            t1 = std::chrono::steady_clock::now() - std::chrono::duration_cast<std::chrono::steady_clock::duration>(
+                                                         std::chrono::duration<double, std::milli>(pre->t_count_ms));
+        } else if (!failed) {
+            try {
+                text = prepare_text(d_raw, n, scratch, &tn, stream);
+                out.stats.t_prepare_ms = ms_since(t0);
+                out.stats.n_bytes = (int64_t)tn;
+                t1 = std::chrono::steady_clock::now();
+                count_words(text, tn, wc, stream, timing_enabled() ? &count_ms : nullptr);
+            } catch (const Error& e) {
+                if (!several && !opt.slab_offset) throw;
+                err = e;
+                failed = true;
+            }
+        }
+        if (failed && err.code == BPE_E_UTF8 && opt.slab_offset) {
+            const size_t p = err.msg.find("position ");
+            if (p != std::string::npos)
+                err.msg = "'utf-8' codec can't decode byte at position " +
+                          std::to_string(std::stoull(err.msg.substr(p + 9)) + opt.slab_offset);
+        }
+        if (several) agree_on_errors(comm, failed ? &err : nullptr, stream);
+        else if (failed) throw err;
+    }
 
     // len(vocab) at loop start: Vocab(special_tokens) = specials then the 256 bytes, deduped
     std::set<std::string> base;
@@ -2943,10 +3016,6 @@ void train_on_device(const uint8_t* d_raw, size_t n, int vocab_size,
     for (int b = 0; b < 256; ++b) base.insert(std::string(1, (char)b));
     const long long rounds = (long long)vocab_size - (long long)base.size();
 
-    auto t1 = std::chrono::steady_clock::now();
-    WordCounts wc;
-    float count_ms = 0;
-    count_words(text, tn, wc, stream, timing_enabled() ? &count_ms : nullptr);
     out.stats.t_count_ms = ms_since(t1);
     out.stats.count_kernel_ms = count_ms;
     out.stats.count_kernel_bytes = (double)tn;
@@ -2972,6 +3041,10 @@ void train_on_device(const uint8_t* d_raw, size_t n, int vocab_size,
         loop_comm = nullptr;
         out.stats.t_exchange_ms = ms_since(te);
         out.stats.n_exchanged_words = (int64_t)uw;
+    }
+    if (!opt.merge_loop) {
+        out.stats.t_total_ms = ms_since(t0);
+        return;
     }
     auto go = [&](auto tag) {
         using TokT = decltype(tag);
