@@ -101,6 +101,15 @@ int bpe_train_buffer_gpus(const uint8_t* data, size_t n, int vocab_size,
 int bpe_train_device(const uint8_t* d_data, size_t n, int vocab_size, const char* const* specials,
                      int n_specials, bpe_comm* comm, void* hip_stream, bpe_result** out);
 
+/* extract_subword_frequencies (reference train.py:16-28) on the device, for checking the
+ * pre-tokenizer + counter on its own: the multi-byte pre-tokens of the text-mode-decoded
+ * bytes and their counts (1-byte words carry no pairs and are not counted; pre-tokens equal to
+ * a special are skipped, train.py:25).  *blob: (u32 len, bytes, u64 count) records in no
+ * particular order, malloc'ed; release with bpe_blob_free. */
+int bpe_word_counts(const uint8_t* data, size_t n, const char* const* specials, int n_specials,
+                    uint8_t** blob, size_t* blob_n);
+void bpe_blob_free(uint8_t* blob);
+
 int64_t bpe_result_n_merges(const bpe_result* r);
 int64_t bpe_result_n_vocab(const bpe_result* r);
 /* blob views owned by the result */

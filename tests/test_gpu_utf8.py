@@ -9,6 +9,8 @@ import random
 
 import pytest
 
+import golden_cases as G
+
 pytestmark = pytest.mark.gpu
 
 bpe_amd = pytest.importorskip("bpe_amd")
@@ -83,3 +85,36 @@ def test_crlf_text_with_multibyte_characters():
     data = (_text(rng, 2000).decode() + "\r\n" + _text(rng, 2000).decode() + "\r").encode()
     vocab, merges = bpe_amd.train_bpe_bytes(data, 270, [])
     assert b"\r" not in b"".join(a + b for a, b in merges)
+
+
+# ------------------------------------------------------------------ A1 on its own
+def _device_word_counts(data: bytes, specials):
+    import ctypes
+    import struct
+    from bpe_amd import _lib
+    L = _lib.lib()
+    arr, k, _keep = _lib.c_strings(specials)
+    p, n = ctypes.c_void_p(), ctypes.c_size_t(0)
+    _lib.check(L.bpe_word_counts(data, len(data), arr, k, ctypes.byref(p), ctypes.byref(n)), "words")
+    try:
+        blob = ctypes.string_at(p, n.value) if n.value else b""
+    finally:
+        L.bpe_blob_free(p)
+    out, off = {}, 0
+    while off < len(blob):
+        ln = struct.unpack_from("<I", blob, off)[0]
+        w = blob[off + 4:off + 4 + ln]
+        out[w] = struct.unpack_from("<Q", blob, off + 4 + ln)[0]
+        off += 12 + ln
+    return out
+
+
+@pytest.mark.parametrize("name", G.names("words"))
+def test_device_word_counts_match_reference(name):
+    """the device pre-tokenizer + counter (k_validate, k_newline_map, k_count_words) against
+    the reference's extract_subword_frequencies table (train.py:16-28): every multi-byte word"""
+    o = G.load("words", name)
+    want = {bytes.fromhex(h): c for h, c in o["words"]}
+    want = {w: c for w, c in want.items() if len(w) > 1}
+    got = _device_word_counts(G.input_bytes(o["input"]), o["special_tokens"])
+    assert got == want

@@ -78,6 +78,9 @@ _SIGS = [
                                              ctypes.c_int, ctypes.POINTER(_P)]),
     ("bpe_train_device", ctypes.c_int, [_P, _SZ, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                         ctypes.c_int, _P, _P, ctypes.POINTER(_P)]),
+    ("bpe_word_counts", ctypes.c_int, [_U8P, _SZ, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
+                                       ctypes.POINTER(_P), ctypes.POINTER(_SZ)]),
+    ("bpe_blob_free", None, [_P]),
     ("bpe_result_n_merges", ctypes.c_int64, [_P]),
     ("bpe_result_n_vocab", ctypes.c_int64, [_P]),
     ("bpe_result_merges_blob", _SZ, [_P, ctypes.POINTER(_P)]),

@@ -1,6 +1,7 @@
 // C ABI of libbpe355 (include/bpe355.h): argument checking, error codes, result objects.
 #include <cerrno>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <memory>
@@ -236,6 +237,54 @@ int bpe_train_file_comm(const char* path, int vocab_size, const char* const* spe
         *out = r.release();
     });
 }
+
+int bpe_word_counts(const uint8_t* data, size_t n, const char* const* specials, int n_specials,
+                    uint8_t** blob, size_t* blob_n) {
+    return bpe::guarded([&] {
+        BPE_REQUIRE(blob && blob_n, BPE_E_ARG, "blob is NULL");
+        *blob = nullptr;
+        *blob_n = 0;
+        BPE_REQUIRE(!n || data, BPE_E_ARG, "data is NULL");
+        bpe::DeviceGuard::require();
+        auto sp = bpe::to_specials(specials, n_specials);
+        bpe::StreamHolder sh(nullptr);
+        bpe::DevBuf<uint8_t> d(std::max<size_t>(n, 1)), scratch;
+        if (n) BPE_HIP(hipMemcpyAsync(d.p, data, n, hipMemcpyHostToDevice, sh.s));
+        size_t tn = 0;
+        const uint8_t* text = bpe::prepare_text(d.p, n, scratch, &tn, sh.s);
+        bpe::WordCounts wc;
+        bpe::count_words(text, tn, wc, sh.s, nullptr);
+        // the table as the merge loop's word collection reads it (k_collect_words): inline keys
+        // hold len and bytes, the others len << 40 | offset + 1 of the first occurrence
+        std::vector<unsigned long long> kv(2 * wc.cap), pos(wc.cap);
+        std::string t(tn, '\0');
+        BPE_HIP(hipMemcpyAsync(kv.data(), wc.kv.p, kv.size() * 8, hipMemcpyDeviceToHost, sh.s));
+        BPE_HIP(hipMemcpyAsync(pos.data(), wc.pos.p, pos.size() * 8, hipMemcpyDeviceToHost, sh.s));
+        if (tn) BPE_HIP(hipMemcpyAsync(&t[0], text, tn, hipMemcpyDeviceToHost, sh.s));
+        BPE_HIP(hipStreamSynchronize(sh.s));
+        std::unordered_set<std::string> skip(sp.begin(), sp.end());
+        std::string out;
+        for (size_t i = 0; i < wc.cap; ++i) {
+            const unsigned long long k = kv[2 * i];
+            if (!k) continue;
+            const bool inl = (k >> 63) != 0;
+            const size_t len = inl ? (size_t)((k >> 56) & 0x7f) : (size_t)(k >> 40);
+            const size_t off = inl ? (size_t)pos[i] : (size_t)((k & ((1ULL << 40) - 1)) - 1);
+            const std::string w = t.substr(off, len);
+            if (skip.count(w)) continue;
+            bpe::put_u32(out, (uint32_t)len);
+            out += w;
+            const unsigned long long c = kv[2 * i + 1];
+            out.append(reinterpret_cast<const char*>(&c), 8);
+        }
+        *blob = static_cast<uint8_t*>(std::malloc(std::max<size_t>(out.size(), 1)));
+        BPE_REQUIRE(*blob, BPE_E_NOMEM, "host allocation failed");
+        std::memcpy(*blob, out.data(), out.size());
+        *blob_n = out.size();
+    });
+}
+
+void bpe_blob_free(uint8_t* blob) { std::free(blob); }
 
 int64_t bpe_result_n_merges(const bpe_result* r) { return r ? r->n_merges : -1; }
 int64_t bpe_result_n_vocab(const bpe_result* r) { return r ? r->n_vocab : -1; }
