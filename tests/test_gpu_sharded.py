@@ -1,13 +1,17 @@
-"""Sharded (multi-rank) training on the GPU, 2 processes sharing one MI355X.
+"""Sharded (multi-rank) training on the GPU.
 
-RCCL refuses two ranks on one device, so the collectives go through the library's host-staged
-communicator (bpe_comm_init_host) backed by torch.distributed/gloo; everything else is the same
-HIP code the RCCL path runs.  Both exchange modes are covered:
-  words  (default)  one all-gather of the slabs' unique-word tables, then each rank trains on
-                    the union (exchange.hip);
+A one-GPU box cannot hold two RCCL ranks, so the ranks here are threads of this process that
+share the device and exchange through the library's in-process communicator
+(BPE355_INPROC_RANKS=1, csrc/comm.hip InProcComm); the slab cutting, the collectives' call
+pattern and every kernel are the ones the RCCL path runs.  Both exchange modes are covered:
+  words  (default)  one all-gather of the slabs' unique-word tables, then rank 0 trains on the
+                    union (exchange.hip);
   rounds            local word tables, one all-reduce of the delta cells per merge round, a
-                    replicated pair table and argmax.
-Every rank must end with exactly the unsharded result.
+                    replicated pair table and argmax on every rank (the driver checks that all
+                    ranks chose the same merges).
+The result must be exactly the unsharded one.  (Round 1 ran these as two processes sharing the
+card through a gloo-backed host communicator; the multi-process protocol is covered on CPU by
+test_dist_gloo.py, and one real RCCL rank by test_rccl_comm_single_rank_forced below.)
 """
 import multiprocessing as mp
 import os
@@ -19,81 +23,40 @@ from oracle import oracle
 
 pytestmark = pytest.mark.gpu
 
-
-def _worker(rank, world, port, slab, vocab_size, specials, q, mode):
-    import torch.distributed as dist
-    from bpe_amd import train_bpe_bytes
-    from bpe_amd.dist import HostCommunicator
-
-    os.environ["BPE355_EXCHANGE"] = mode
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    import datetime
-    dist.init_process_group("gloo", rank=rank, world_size=world,
-                            timeout=datetime.timedelta(seconds=180))
-    try:
-        with HostCommunicator() as comm:
-            vocab, merges = train_bpe_bytes(slab, vocab_size, specials, comm=comm)
-        q.put((rank, (vocab, merges)))
-    except Exception as e:  # noqa: BLE001
-        q.put((rank, repr(e)))
-    finally:
-        dist.destroy_process_group()
+bpe_amd = pytest.importorskip("bpe_amd")
 
 
-def _safe_cuts(data, world):
-    from bpe_amd.dist import slab_bounds
-    return slab_bounds(data, world)
-
-
-def run_sharded(data, world, vocab_size, specials, mode="words"):
-    import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    cuts = _safe_cuts(data, world)
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, data[cuts[r]:cuts[r + 1]],
-                                               vocab_size, specials, q, mode)) for r in range(world)]
-    for p in procs:
-        p.start()
-    out = {}
-    try:
-        for _ in procs:
-            r, v = q.get(timeout=400)
-            out[r] = v
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
-    return out
+@pytest.fixture
+def ranks(monkeypatch):
+    def set_(n, mode):
+        monkeypatch.setenv("BPE355_INPROC_RANKS", "1")
+        monkeypatch.setenv("BPE355_EXCHANGE", mode)
+        bpe_amd.set_num_gpus(n)
+    yield set_
+    bpe_amd.set_num_gpus(None)
 
 
 @pytest.mark.parametrize("mode", ["words", "rounds"])
 @pytest.mark.parametrize("name", ["corpus_en_1000", "tiny_1200", "synth_mixed_200k"])
-def test_sharded_gpu_matches_reference(name, mode):
+def test_sharded_gpu_matches_reference(name, mode, ranks):
     o, vocab, merges = G.train_expect(name)
     data = G.input_bytes(o["input"])
-    out = run_sharded(data, 2, o["vocab_size"], o["special_tokens"], mode)
-    for r in (0, 1):
-        assert not isinstance(out[r], str), out[r]
-        assert out[r][1] == merges
-        assert out[r][0] == vocab
+    ranks(2, mode)
+    got_vocab, got_merges = bpe_amd.train_bpe_bytes(data, o["vocab_size"], o["special_tokens"])
+    assert bpe_amd.last_train_stats()["n_gpus"] == 2
+    assert got_merges == merges
+    assert got_vocab == vocab
 
 
-@pytest.mark.parametrize("mode", ["words", "rounds"])
-def test_sharded_gpu_synthetic_vs_oracle(mode):
+@pytest.mark.parametrize("mode,n", [("words", 2), ("rounds", 2), ("rounds", 3)])
+def test_sharded_gpu_synthetic_vs_oracle(mode, n, ranks):
     import synth_text
     data = synth_text.generate(31, 4_000_000, "ascii").encode("utf-8")
     want = oracle.train_raw(data, 5000, ["<|endoftext|>"])
-    out = run_sharded(data, 2, 5000, ["<|endoftext|>"], mode)
-    for r in (0, 1):
-        assert not isinstance(out[r], str), out[r]
-        assert out[r][1] == want[1]
-        assert out[r][0] == want[0]
+    ranks(n, mode)
+    got = bpe_amd.train_bpe_bytes(data, 5000, ["<|endoftext|>"])
+    assert got[1] == want[1]
+    assert got[0] == want[0]
 
 
 def _rccl_worker(port, q, force):

@@ -439,7 +439,8 @@ void train_source(const Source& src, int vocab_size, const std::vector<std::stri
             DevBuf<uint8_t> d(std::max<size_t>(len, 1));
             TrainOpts opt;
             opt.slab_offset = cut[r];
-            opt.merge_loop = r == 0;   // every rank holds the union; one trains on it
+            // every rank holds the union and one trains on it; per-round exchange: all of them
+            opt.merge_loop = r == 0 || per_round_exchange();
             Prepared pre;
             bool counted = false;
             try {
@@ -462,6 +463,10 @@ void train_source(const Source& src, int vocab_size, const std::vector<std::stri
     for (auto& x : th) x.join();
     for (auto& e : errs)
         if (e) std::rethrow_exception(e);
+    if (per_round_exchange())   // every rank ran the replicated argmax: they must agree exactly
+        for (int r = 1; r < g; ++r)
+            BPE_REQUIRE(outs[r].merges == outs[0].merges, BPE_E_RCCL,
+                        "rank " + std::to_string(r) + " chose different merges than rank 0");
     out = std::move(outs[0]);
     out.stats.t_load_ms = *std::max_element(load_ms.begin(), load_ms.end());
     out.stats.t_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

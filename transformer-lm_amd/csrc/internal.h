@@ -107,6 +107,9 @@ std::unique_ptr<Comm> make_rccl_comm(const uint8_t id[128], int nranks, int rank
 // ranks that are threads of one process, possibly sharing a device (tests; comm.hip)
 std::shared_ptr<void> make_inproc_group();
 std::unique_ptr<Comm> make_inproc_comm(const std::shared_ptr<void>& group, int nranks, int rank, int device);
+// BPE355_EXCHANGE=rounds: several ranks keep their slabs' words and all-reduce the pair deltas
+// every round, so every rank runs the merge loop (default: one word-table exchange)
+bool per_round_exchange();
 void train_on_device(const uint8_t* d_raw, size_t n, int vocab_size,
                      const std::vector<std::string>& specials, Comm* comm, hipStream_t stream,
                      TrainOutput& out, const TrainOpts& opt = TrainOpts{}, Prepared* pre = nullptr);

@@ -2962,6 +2962,11 @@ void agree_on_errors(Comm* comm, const Error* mine, hipStream_t stream) {
 
 }  // namespace
 
+bool per_round_exchange() {
+    const char* ex = std::getenv("BPE355_EXCHANGE");
+    return ex && std::string(ex) == "rounds";
+}
+
 void train_on_device(const uint8_t* d_raw, size_t n, int vocab_size,
                      const std::vector<std::string>& specials, Comm* comm, hipStream_t stream,
                      TrainOutput& out, const TrainOpts& opt, Prepared* pre) {
@@ -3031,8 +3036,7 @@ void train_on_device(const uint8_t* d_raw, size_t n, int vocab_size,
     // on a 1-rank communicator too (tests the collective on a single-GPU box).
     DevBuf<uint8_t> union_text;
     Comm* loop_comm = comm;
-    const char* ex = std::getenv("BPE355_EXCHANGE");
-    const bool per_round = ex && std::string(ex) == "rounds";
+    const bool per_round = per_round_exchange();
     if (comm && !per_round && (comm->nranks > 1 || std::getenv("BPE355_FORCE_EXCHANGE"))) {
         auto te = std::chrono::steady_clock::now();
         uint64_t uw = 0;
