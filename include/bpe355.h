@@ -142,6 +142,8 @@ typedef struct {
     int64_t n_exchanged_words; /* local unique words of all ranks gathered (before dedupe) */
     double t_load_ms;         /* file / host buffer -> HBM (0 when the corpus starts in HBM) */
     int64_t n_gpus;           /* devices (ranks) that took part */
+    double count_reduce_ms;   /* device time aggregating the counter's spilled records */
+    int64_t n_count_records;  /* pre-tokens (or cache entries) spilled as records by the counter */
 } bpe_train_stats;
 int bpe_result_stats(const bpe_result* r, bpe_train_stats* out);
 void bpe_result_free(bpe_result* r);

@@ -1,0 +1,100 @@
+"""The byte-parallel counter (csrc/count.hip: token-start masks, LDS word cache, record spill and
+by-bin LDS aggregation) against the oracle's word table (reference train.py:16-28), on the paths
+the bench corpus takes and on the ones only knobs reach on small inputs:
+
+  * records on (BPE355_REC_POOL: the pool, in records; the bench turns it on past 256 MB);
+  * the pool spent (a tiny pool: most misses fall back to the global table);
+  * few workgroups each streaming many chunks (BPE355_STREAM_WG): pages fill and turn over;
+  * the file path's segment launches (BPE355_SEG_MB) continuing each workgroup's page;
+  * an unaligned device pointer (the byte-wise staging path);
+  * adversarial text (every pattern branch, multi-byte characters at every alignment).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+import synth_text
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+bpe_amd = pytest.importorskip("bpe_amd")
+from bpe_amd import _lib  # noqa: E402
+from bpe_amd.train import last_train_stats  # noqa: E402
+from test_gpu_utf8 import _device_word_counts  # noqa: E402
+
+EOT = ["<|endoftext|>"]
+
+
+@pytest.fixture
+def knob(monkeypatch):
+    def set_(k, v):
+        monkeypatch.setenv(k, str(v))
+    return set_
+
+
+def _synth(seed, flavour, n):
+    buf = np.empty(n, dtype=np.uint8)
+    assert _lib.lib().bpe_synth_corpus_host(buf.ctypes.data, n, seed, flavour, 0, 8) == 0
+    return buf.tobytes()
+
+
+def _want_words(data, specials):
+    text = data.replace(b"\r\n", b"\n").replace(b"\r", b"\n")
+    return {w: c for w, c in oracle.word_counts(text, specials).items() if len(w) > 1}
+
+
+@pytest.mark.parametrize("pool", [None, "1e8", "150000"])
+@pytest.mark.parametrize("seed,flavour,n", [(31, 0, 12 << 20), (32, 1, 5 << 20)])
+def test_word_table_vs_oracle(knob, pool, seed, flavour, n):
+    if pool:
+        knob("BPE355_REC_POOL", pool)
+    data = _synth(seed, flavour, n)
+    assert _device_word_counts(data, EOT) == _want_words(data, EOT)
+
+
+@pytest.mark.parametrize("flavour", ["mixed", "space", "ascii"])
+def test_adversarial_text_records(knob, flavour):
+    knob("BPE355_REC_POOL", "1e8")
+    data = synth_text.generate(77, 3_000_000, flavour).encode("utf-8")
+    assert _device_word_counts(data, EOT) == _want_words(data, EOT)
+
+
+def test_page_turnover_few_workgroups(knob):
+    knob("BPE355_REC_POOL", "1e8")
+    knob("BPE355_STREAM_WG", 3)
+    data = _synth(33, 0, 24 << 20)
+    assert _device_word_counts(data, EOT) == _want_words(data, EOT)
+
+
+def test_train_records_vs_oracle(knob):
+    knob("BPE355_REC_POOL", "1e8")
+    data = _synth(34, 0, 16 << 20)
+    got = bpe_amd.train_bpe_bytes(data, 6000, EOT)
+    assert last_train_stats()["n_count_records"] > 0
+    assert got == oracle.train_raw(data, 6000, EOT)
+
+
+def test_file_segments_records(knob, tmp_path):
+    knob("BPE355_REC_POOL", "1e8")
+    knob("BPE355_SEG_MB", 4)
+    data = _synth(35, 1, 40 << 20)
+    p = tmp_path / "c.txt"
+    p.write_bytes(data)
+    got = bpe_amd.train_bpe(p, 4000, EOT)
+    assert last_train_stats()["n_count_records"] > 0
+    assert got == oracle.train_raw(data, 4000, EOT)
+
+
+@pytest.mark.parametrize("shift", [1, 3, 7])
+def test_unaligned_device_text(shift):
+    import torch
+    data = synth_text.generate(78, 400_000, "mixed").encode("utf-8").replace(b"\r", b" ")
+    buf = torch.zeros(len(data) + 16, dtype=torch.uint8, device="cuda")
+    buf[shift:shift + len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    torch.cuda.synchronize()
+    got = bpe_amd.train_bpe_device(buf.data_ptr() + shift, len(data), 1500, EOT)
+    assert got == oracle.train_raw(data, 1500, EOT)

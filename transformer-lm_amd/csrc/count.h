@@ -1,0 +1,60 @@
+// The byte-parallel counter (count.hip) and its record pool, used by CountPass (text.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+
+#include "internal.h"
+
+namespace bpe {
+
+constexpr int kPageRecs = 65536;   // records per pool page (one workgroup appends to a page)
+
+// Device view of the record pool: SoA records {packed bytes lo, hi, len | offset << 5 | count
+// << 45}, in pages owned one at a time by a counting workgroup.
+struct RecPool {
+    uint64_t* lo;
+    uint64_t* hi;
+    uint64_t* meta;
+    unsigned* page_used;   // records in each page (written when a workgroup leaves the page)
+    unsigned* n_pages;     // pages handed out
+    unsigned max_pages;
+    int* wg_page;          // per counting workgroup: its current page (-2 none yet, -1 pool spent)
+    unsigned* wg_used;
+    int on;
+};
+
+// Three parallel u64 arrays of one capacity, on one device.  Large record arrays are kept across
+// training calls (ScratchArrays::take / give): freeing and re-allocating tens of GB per call
+// stalls the host for hundreds of ms (the driver clears fresh VRAM).
+struct Arrays3 {
+    DevBuf<uint64_t> a, b, c;
+    size_t cap = 0;
+    int dev = -1;
+};
+std::unique_ptr<Arrays3> scratch_take(size_t cap);   // exclusive until given back
+void scratch_give(std::unique_ptr<Arrays3> x);
+
+struct RecPoolOwner {
+    std::unique_ptr<Arrays3> rec;    // the pool: lo, hi, meta
+    DevBuf<unsigned> page_used, n_pages, wg_used;
+    DevBuf<int> wg_page;
+    unsigned max_pages = 0, n_wg = 0, pages_used = 0;
+    unsigned long long records = 0;
+    void init(size_t n_bytes, unsigned grid, hipStream_t s);
+    ~RecPoolOwner();
+    RecPool dev() const;
+    // aggregate every record into the word table (one global add per distinct word per bin)
+    void reduce(const uint8_t* text, const WordCounts& wc, unsigned long long* fill, unsigned* status,
+                hipStream_t s);
+};
+
+unsigned count2_grid(size_t n_chunks);
+void count2_launch(const uint8_t* text, size_t lo, size_t hi, size_t c0, size_t nc, unsigned grid,
+                   const WordCounts& wc, unsigned long long* fill, unsigned* status, unsigned long long* ntok,
+                   const RecPool& R, const unsigned long long* gate, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+
+}  // namespace bpe

@@ -259,11 +259,8 @@ struct ChunkTrack {
 };
 
 size_t segment_bytes() {
-    static const size_t b = [] {
-        const char* e = std::getenv("BPE355_SEG_MB");   // experiment knob
-        return (size_t)(e ? std::max(1, std::atoi(e)) : 256) << 20;   // 256/512/1024 MB: 690/720/790 ms steps
-    }();
-    return b;
+    const char* e = std::getenv("BPE355_SEG_MB");   // experiment / test knob
+    return (size_t)(e ? std::max(1, std::atoi(e)) : 256) << 20;   // 256/512/1024 MB: 690/720/790 ms steps
 }
 
 // safe cut points splitting src[off, off + len) into segments of ~seg bytes (relative to off)

@@ -37,6 +37,8 @@ struct WordCounts {
     DevBuf<unsigned long long> pos;   // cap: an occurrence of each inline-keyed word
     size_t cap = 0;
     uint64_t n_pretokens = 0;         // multi-byte pre-tokens seen
+    uint64_t n_records = 0;           // cache misses spilled as records (count.hip)
+    double reduce_ms = 0;             // device time of their aggregation (when timed)
 };
 // Pre-tokenize text[0..n) with the GPT-2 pattern and count the multi-byte words.
 // (Single-byte words carry no pairs and cannot affect training.)
@@ -46,8 +48,12 @@ void count_words(const uint8_t* d_text, size_t n, WordCounts& wc, hipStream_t st
 // The same count over a text that arrives in segments [lo, hi) cut at safe split points
 // (text.hip): range() enqueues one launch per segment into one table; finish() returns false
 // when the table overflowed (then recount everything with a larger table).
+struct RecPoolOwner;
 struct CountPass {
     WordCounts wc;
+    bool v2 = true;                       // the byte-parallel counter (count.hip); BPE355_COUNT_V1: the serial one
+    std::unique_ptr<RecPoolOwner> rec;    // its record pool (large texts)
+    unsigned grid2 = 0;
     DevBuf<unsigned> status;
     DevBuf<unsigned long long> ntok, fill;
     const uint8_t* text = nullptr;
@@ -61,6 +67,7 @@ struct CountPass {
     void begin(const uint8_t* d_text, size_t n, size_t cap, hipStream_t stream, bool timing);
     void range(size_t lo, size_t hi);
     bool finish();
+    CountPass();
     ~CountPass();
 };
 

@@ -17,6 +17,7 @@
 
 #include <hip/hip_ext.h>
 
+#include "count.h"
 #include "internal.h"
 #include "pretok.h"
 #include "stage.h"
@@ -483,6 +484,18 @@ void CountPass::begin(const uint8_t* d_text, size_t n, size_t cap, hipStream_t s
     BPE_HIP(hipMemsetAsync(status.p, 0, 4, s));
     BPE_HIP(hipMemsetAsync(ntok.p, 0, 24, s));
     BPE_HIP(hipMemsetAsync(fill.p, 0, 8, s));
+    static const bool v1 = std::getenv("BPE355_COUNT_V1") != nullptr;   // A/B knob: the serial counter
+    v2 = !v1;
+    rec.reset();
+    if (v2) {
+        grid2 = count2_grid((n + kChunk - 1) / kChunk);
+        // misses spill as records (aggregated in LDS by bin afterwards) when the text is large
+        // enough for the per-workgroup pages to pay off; BPE355_REC_POOL forces it (tests)
+        if (n >= (size_t(256) << 20) || std::getenv("BPE355_REC_POOL")) {
+            rec = std::make_unique<RecPoolOwner>();
+            rec->init(n, grid2, s);
+        }
+    }
 }
 
 void CountPass::range(size_t lo, size_t hi) {
@@ -500,6 +513,12 @@ void CountPass::range(size_t lo, size_t hi) {
         ev.push_back(e0);
         ev.push_back(e1);
     }
+    if (v2) {
+        RecPool R{};
+        if (rec) R = rec->dev();
+        count2_launch(text, lo, hi, c0, c1 - c0, grid2, wc, fill.p, status.p, ntok.p, R, gate, s, e0, e1);
+        return;
+    }
     // timed launch: the events are stamped by the kernel's own dispatch packet (the interval
     // rocprofv3 reports), not by marker packets around it
     hipExtLaunchKernelGGL(kern, dim3(grid), dim3(256), kPadded, s, e0, e1, 0, text, lo, hi, c0, c1 - c0,
@@ -509,6 +528,26 @@ void CountPass::range(size_t lo, size_t hi) {
 }
 
 bool CountPass::finish() {
+    if (rec) {   // aggregate the spilled records into the table
+        hipEvent_t r0 = nullptr, r1 = nullptr;
+        if (timed) {
+            BPE_HIP(hipEventCreate(&r0));
+            BPE_HIP(hipEventCreate(&r1));
+            BPE_HIP(hipEventRecord(r0, s));
+        }
+        rec->reduce(text, wc, fill.p, status.p, s);
+        wc.n_records = rec->records;
+        if (timed) {
+            BPE_HIP(hipEventRecord(r1, s));
+            BPE_HIP(hipEventSynchronize(r1));
+            float ms = 0;
+            BPE_HIP(hipEventElapsedTime(&ms, r0, r1));
+            wc.reduce_ms = ms;
+            (void)hipEventDestroy(r0);
+            (void)hipEventDestroy(r1);
+        }
+        rec.reset();   // the pool's memory goes back before the merge loop
+    }
     unsigned st = 0;
     BPE_HIP(hipMemcpyAsync(&st, status.p, 4, hipMemcpyDeviceToHost, s));
     BPE_HIP(hipMemcpyAsync(&wc.n_pretokens, ntok.p, 8, hipMemcpyDeviceToHost, s));
@@ -522,11 +561,13 @@ bool CountPass::finish() {
     if (std::getenv("BPE355_TRACE")) {
         unsigned long long d[3];
         BPE_HIP(hipMemcpy(d, ntok.p, 24, hipMemcpyDeviceToHost));
-        std::fprintf(stderr, "[bpe355] count: cap %zu pretokens %llu cache-miss %llu long %llu launches %zu\n",
-                     wc.cap, d[0], d[1], d[2], ev.size() / 2);
+        std::fprintf(stderr, "[bpe355] count: cap %zu pretokens %llu cache-miss %llu long %llu launches %zu records %llu\n",
+                     wc.cap, d[0], d[1], d[2], ev.size() / 2, (unsigned long long)wc.n_records);
     }
     return !(st & 1u);
 }
+
+CountPass::CountPass() = default;
 
 CountPass::~CountPass() {
     for (auto& e : ev) (void)hipEventDestroy(e);
