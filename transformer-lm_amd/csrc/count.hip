@@ -36,9 +36,29 @@ namespace bpe {
 
 namespace {
 
+// classes of the code points below U+0800 (every 2-byte character), 2 bits each, in LDS: the
+// corpus's non-ASCII characters are mostly these; the rest go through the global tables
+__shared__ uint32_t g_cls2[2048 / 16];
+
 struct DevTab {
     __device__ static unsigned page(unsigned i) { return BPE_UC_PAGE[i]; }
     __device__ static unsigned bits(unsigned pg, unsigned i) { return BPE_UC_BITS[pg][i]; }
+    __device__ static int cls(uint32_t cp) {
+        return cp < 2048u ? (int)((g_cls2[cp >> 4] >> (2 * (cp & 15u))) & 3u) : uc_class<DevTab>(cp);
+    }
+};
+
+__device__ __forceinline__ void load_cls2(int tid, int nthreads) {
+    for (int i = tid; i < 2048 / 16; i += nthreads) {
+        uint32_t x = 0;
+        for (int k = 0; k < 16; ++k) x |= (uint32_t)uc_class<DevTab>((uint32_t)(16 * i + k)) << (2 * k);
+        g_cls2[i] = x;
+    }
+}
+
+// the stage as text positions relative to the chunk start (pretok.h's serial scanner)
+struct StageText {
+    __device__ __forceinline__ uint8_t operator[](uint32_t r) const;
 };
 
 constexpr int kPre = 16;                          // staged bytes before the chunk
@@ -46,7 +66,6 @@ constexpr int kPost = 16;                         // staged bytes after the halo
 constexpr int kStage = kPre + kWin + kPost;       // 17 440
 constexpr int kSVec = (kStage + 4095) / 4096;     // 16-B loads per thread per chunk
 constexpr int kWords = kChunk / 64;               // mask words of the chunk
-constexpr int kHaloWords = kHalo / 64;            // mask words of the halo
 constexpr int kCache2 = 1024;                     // LDS word-cache entries (2-way sets)
 constexpr int kEpoch2 = 4;                        // chunks between cache evictions
 constexpr unsigned kKeep2 = 2;                    // an entry stays if hit this often per epoch
@@ -58,6 +77,8 @@ constexpr int kBinBits = 12;
 constexpr int kBins = 1 << kBinBits;
 
 __device__ __forceinline__ unsigned rec_bin(uint64_t h) { return (unsigned)(h >> (64 - kBinBits)); }
+
+__device__ __forceinline__ uint8_t StageText::operator[](uint32_t r) const { return g_stage[kPre + r]; }
 
 // 16 bytes at g that straddle the text start or end (the first and last chunks only)
 __device__ __noinline__ uint4 fetch_edge(const uint8_t* __restrict__ s, size_t n, long long g) {
@@ -126,10 +147,10 @@ __global__ void __launch_bounds__(256) k_count2(const uint8_t* __restrict__ s, s
                                                 unsigned long long* __restrict__ pos, size_t mask,
                                                 unsigned long long max_fill, unsigned long long* __restrict__ fill,
                                                 unsigned* __restrict__ status, unsigned long long* __restrict__ n_tok,
-                                                RecPool R, const unsigned long long* __restrict__ gate) {
+                                                RecPool R, const unsigned long long* __restrict__ gate, int mode) {
     // a segment is counted only behind a clean validation of everything before it
     if (gate && *gate != ~0ULL) return;
-    __shared__ uint64_t s_mask[kWords + kHaloWords];
+    __shared__ uint64_t s_mask[kWords];
     __shared__ unsigned long long c_key[kCache2];
     __shared__ uint64_t c_lo[kCache2], c_hi[kCache2];
     __shared__ unsigned c_cnt[kCache2];
@@ -139,6 +160,7 @@ __global__ void __launch_bounds__(256) k_count2(const uint8_t* __restrict__ s, s
     __shared__ unsigned s_used;
     const int tid = threadIdx.x;
     for (int i = tid; i < kCache2; i += blockDim.x) { c_key[i] = 0; c_cnt[i] = 0; c_mark[i] = 0; }
+    load_cls2(tid, blockDim.x);
     if (tid == 0) {
         s_page = R.on ? R.wg_page[blockIdx.x] : -1;
         s_used = R.on ? R.wg_used[blockIdx.x] : 0u;
@@ -198,12 +220,14 @@ __global__ void __launch_bounds__(256) k_count2(const uint8_t* __restrict__ s, s
             return m;
         };
         s_mask[tid] = mask_word(tid);
-        if (tid < kHaloWords) s_mask[kWords + tid] = mask_word(kWords + tid);
         // the next chunk's loads fly during the token phase (not the register-heavy mask phase)
         if (c + gridDim.x < n_chunks) fetch2<kAligned>(pre, s, n, (chunk0 + c + gridDim.x) * kChunk, tid);
         __syncthreads();
 
         // ---- the pre-tokens that start in this thread's 64 bytes
+        // (analysis knob BPE355_COUNT_MODE, timing only -- counts are then incomplete: 1 masks
+        // only, 2 + token bounds, 3 + packing and hashing, 4 + the LDS cache, misses dropped)
+        if (mode == 1) continue;
         const size_t rem = n > base ? n - base : 0;
         const uint32_t tend = rem < (size_t)kWin ? (uint32_t)rem : (uint32_t)kWin;   // staged text end
         uint64_t m = s_mask[tid];
@@ -215,16 +239,22 @@ __global__ void __launch_bounds__(256) k_count2(const uint8_t* __restrict__ s, s
                 e = 64u * tid + (uint32_t)__builtin_ctzll(m);
             } else {
                 e = ~(size_t)0;
-                for (int w = tid + 1; w < kWords + kHaloWords; ++w) {
+                for (int w = tid + 1; w < kWords; ++w) {
                     const uint64_t x = s_mask[w];
                     if (x) { e = 64u * w + (uint32_t)__builtin_ctzll(x); break; }
                 }
-                if (e == ~(size_t)0)   // no start in the staged window: the text ends, or a long token
-                    e = rem <= (size_t)kWin ? (size_t)tend : token_end(s, n, base + r) - base;
+                if (e == ~(size_t)0) {
+                    // the chunk's last pre-token: the serial scanner over the staged halo, trusted
+                    // when it stops clear of the staged end (it looks one character ahead), else
+                    // over the text itself
+                    e = token_end(StageText{}, tend, r);
+                    if (e + 4 > tend && tend < rem) e = token_end(s, n, base + r) - base;
+                }
             }
             const size_t len = e - r;
             if (len < 2) continue;
             ++ntok;
+            if (mode == 2) continue;
             const size_t gpos = base + r;
             if (len > (size_t)kInline) {
                 ++n_long;
@@ -236,6 +266,7 @@ __global__ void __launch_bounds__(256) k_count2(const uint8_t* __restrict__ s, s
             uint64_t wl, wh;
             pack_stage(kPre + (int)r, (int)len, wl, wh);
             const uint64_t h = short_hash(wl, wh, len);
+            if (mode == 3) { n_miss += h & 1; continue; }
             const unsigned ls = (unsigned)(h >> 40) & (kCache2 - 2);
             const unsigned long long mine = ((unsigned long long)len << 40) | (gpos + 1);
             bool done = false;
@@ -264,7 +295,7 @@ __global__ void __launch_bounds__(256) k_count2(const uint8_t* __restrict__ s, s
             }
             if (!done) {
                 ++n_miss;
-                spill(wl, wh, len, gpos, 1);
+                if (mode != 4) spill(wl, wh, len, gpos, 1);
             }
         }
         // epoch end: entries hit fewer than kKeep2 times since the last epoch leave the cache
@@ -337,8 +368,18 @@ __global__ void __launch_bounds__(1024) k_rec_hist(RecPool R, unsigned n_pages, 
     __syncthreads();
     const unsigned used = R.page_used[pg];
     const size_t g0 = (size_t)pg * kPageRecs;
-    for (unsigned i = threadIdx.x; i < used; i += blockDim.x)
-        atomicAdd(&h[rec_bin(rec_hash(R.lo[g0 + i], R.hi[g0 + i], R.meta[g0 + i]))], 1u);
+    constexpr int U = 4;
+    for (unsigned i0 = threadIdx.x; i0 < used; i0 += U * blockDim.x) {
+        unsigned bin[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const unsigned i = i0 + u * blockDim.x;
+            bin[u] = i < used ? rec_bin(rec_hash(R.lo[g0 + i], R.hi[g0 + i], R.meta[g0 + i])) : ~0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (bin[u] != ~0u) atomicAdd(&h[bin[u]], 1u);
+    }
     __syncthreads();
     for (int i = threadIdx.x; i < kBins; i += blockDim.x) hist[(size_t)i * n_pages + pg] = h[i];
 }
@@ -392,12 +433,22 @@ __global__ void __launch_bounds__(1024) k_rec_scatter(RecPool R, unsigned n_page
     __syncthreads();
     const unsigned used = R.page_used[pg];
     const size_t g0 = (size_t)pg * kPageRecs;
-    for (unsigned i = threadIdx.x; i < used; i += blockDim.x) {
-        const uint64_t a = R.lo[g0 + i], b = R.hi[g0 + i], m = R.meta[g0 + i];
-        const unsigned long long p = atomicAdd(&cur[rec_bin(rec_hash(a, b, m))], 1ULL);
-        olo[p] = a;
-        ohi[p] = b;
-        ometa[p] = m;
+    constexpr int U = 4;   // records per thread per step: their loads are all in flight together
+    for (unsigned i0 = threadIdx.x; i0 < used; i0 += U * blockDim.x) {
+        uint64_t a[U], b[U], m[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const unsigned i = i0 + u * blockDim.x;
+            if (i < used) { a[u] = R.lo[g0 + i]; b[u] = R.hi[g0 + i]; m[u] = R.meta[g0 + i]; }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (i0 + u * blockDim.x >= used) break;
+            const unsigned long long p = atomicAdd(&cur[rec_bin(rec_hash(a[u], b[u], m[u]))], 1ULL);
+            olo[p] = a[u];
+            ohi[p] = b[u];
+            ometa[p] = m[u];
+        }
     }
 }
 
@@ -418,8 +469,18 @@ __global__ void __launch_bounds__(1024) k_rec_reduce(const uint64_t* __restrict_
     __syncthreads();
     const unsigned long long b0 = base[blockIdx.x], b1 = base[blockIdx.x + 1];
     unsigned long long inserted = 0;
-    for (unsigned long long i = b0 + threadIdx.x; i < b1; i += blockDim.x) {
-        const uint64_t wl = rlo[i], wh = rhi[i], m = rmeta[i];
+    constexpr int U = 4;
+    for (unsigned long long i0 = b0 + threadIdx.x; i0 < b1; i0 += U * blockDim.x) {
+      uint64_t ul[U], uh[U], um[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+          const unsigned long long i = i0 + (unsigned long long)u * blockDim.x;
+          if (i < b1) { ul[u] = rlo[i]; uh[u] = rhi[i]; um[u] = rmeta[i]; }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (i0 + (unsigned long long)u * blockDim.x >= b1) break;
+        const uint64_t wl = ul[u], wh = uh[u], m = um[u];
         const size_t len = (size_t)(m & 31u);
         const size_t off = (size_t)((m >> 5) & kOffMask);
         const unsigned long long c = m >> 45;
@@ -454,6 +515,7 @@ __global__ void __launch_bounds__(1024) k_rec_reduce(const uint64_t* __restrict_
             table_add(s, s, off, len, wl, wh, h, c, kv, pos, mask, status, &ins);
             inserted += ins;
         }
+      }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kRedSlots; i += blockDim.x) {
@@ -495,10 +557,11 @@ unsigned count2_grid(size_t n_chunks) {
 void count2_launch(const uint8_t* text, size_t lo, size_t hi, size_t c0, size_t nc, unsigned grid,
                    const WordCounts& wc, unsigned long long* fill, unsigned* status, unsigned long long* ntok,
                    const RecPool& R, const unsigned long long* gate, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    static const int mode = std::getenv("BPE355_COUNT_MODE") ? std::atoi(std::getenv("BPE355_COUNT_MODE")) : 0;
     const bool aligned = (reinterpret_cast<uintptr_t>(text) & 15u) == 0;
     auto kern = aligned ? k_count2<true> : k_count2<false>;
     hipExtLaunchKernelGGL(kern, dim3(grid), dim3(256), kStage, s, e0, e1, 0, text, lo, hi, c0, nc, wc.kv.p, wc.pos.p,
-                          wc.cap - 1, (unsigned long long)(wc.cap / 2), fill, status, ntok, R, gate);
+                          wc.cap - 1, (unsigned long long)(wc.cap / 2), fill, status, ntok, R, gate, mode);
     BPE_HIP(hipGetLastError());
 }
 

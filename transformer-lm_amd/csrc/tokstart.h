@@ -34,7 +34,8 @@ constexpr int kStartWin = kStartPre + 64 + 16;     // 88 bytes: the block and it
 
 __host__ __device__ __forceinline__ u128 bit128(int j) { return (u128)1 << j; }
 
-// class of a code point through the generated regex tables (Tab::page / Tab::bits)
+// class of a code point through the generated regex tables (Tab::page / Tab::bits); Tab::cls(cp)
+// may answer from a faster table first
 template <class Tab>
 __host__ __device__ __forceinline__ int uc_class(uint32_t cp) {
     cp = cp < 0x110000u ? cp : 0x10FFFFu;
@@ -106,7 +107,7 @@ __host__ __device__ __forceinline__ uint64_t token_starts64(const Win& w, int vh
         if (b < 0xE0u) cp = ((b & 0x1Fu) << 6) | (b1 & 0x3Fu);
         else if (b < 0xF0u) cp = ((b & 0x0Fu) << 12) | ((b1 & 0x3Fu) << 6) | (b2 & 0x3Fu);
         else cp = ((b & 0x07u) << 18) | ((b1 & 0x3Fu) << 12) | ((b2 & 0x3Fu) << 6) | (b3 & 0x3Fu);
-        const int c = uc_class<Tab>(cp);
+        const int c = Tab::cls(cp);
         const u128 m = bit128(j);
         if (c == CLS_LETTER) L |= m;
         else if (c == CLS_NUMBER) N |= m;

@@ -14,6 +14,7 @@ namespace hosttab {
 struct Tab {
     static unsigned page(unsigned i) { return BPE_UC_PAGE[i]; }
     static unsigned bits(unsigned pg, unsigned i) { return BPE_UC_BITS[pg][i]; }
+    static int cls(uint32_t cp) { return uc_class<Tab>(cp); }
 };
 }  // namespace hosttab
 }  // namespace bpe
