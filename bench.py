@@ -66,6 +66,9 @@ def parse():
     ap.add_argument("--cpu-sample-mb", type=float, default=16.0)
     ap.add_argument("--cpu-cap-s", type=float, default=20.0)
     ap.add_argument("--no-timing", action="store_true", help="skip per-launch HIP event timing")
+    ap.add_argument("--no-file", action="store_true",
+                    help="profiling runs: skip the file path (every k_count2 launch then covers the whole "
+                         "corpus); the line then reports the HBM-resident rate")
     return ap.parse_args()
 
 
@@ -124,7 +127,8 @@ def main():
     # ---------------------------------------------------------------- the corpus file
     n = max(1, int(args.bytes) // BLOCK) * BLOCK
     path = pathlib.Path(args.corpus_dir) / f"bpe355_bench_s{args.seed}_f{args.flavour}_{n}.txt"
-    if rank == 0 and not (path.exists() and path.stat().st_size == n):
+    need_file = not args.no_file or not args.no_cpu_baseline
+    if need_file and rank == 0 and not (path.exists() and path.stat().st_size == n):
         t = time.perf_counter()
         write_corpus(L, path, n, args.seed, args.flavour)
         print(f"[bench] wrote {n / 1e9:.2f} GB corpus to {path} in {time.perf_counter() - t:.1f}s",
@@ -137,55 +141,45 @@ def main():
         return train_bpe(path, args.vocab, [EOT])
 
     # ---------------------------------------------------------------- end to end: file -> merges
-    L.bpe_set_timing(0)
-    for _ in range(args.warmup):
-        vocab, merges = train_file()
-    L.bpe_set_timing(0 if args.no_timing else 1)
     stats = []
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        vocab, merges = train_file()
-        stats.append(last_train_stats())
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0)
-    L.bpe_set_timing(0)
-    n_gpus = int(stats[-1]["n_gpus"])
-    ms_per_step = elapsed / args.steps * 1e3
-    value = n / (elapsed / args.steps) / 1e6
-    rounds = len(merges)
-    avg = {k: sum(s[k] for s in stats) / len(stats) for k in stats[0]}
+    elapsed = 0.0
+    if not args.no_file:
+        L.bpe_set_timing(0)
+        for _ in range(args.warmup):
+            vocab, merges = train_file()
+        L.bpe_set_timing(0 if args.no_timing else 1)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            vocab, merges = train_file()
+            stats.append(last_train_stats())
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = max_over_ranks(time.perf_counter() - t0)
+        L.bpe_set_timing(0)
 
-    # dominant kernel: k_count_words (device time per launch, event-timed on the library's
-    # stream) vs the merge loop's trips
-    roofline = None
-    if avg["count_kernel_ms"] > 0:
-        kms = avg["count_kernel_ms"]
-        kb = avg["count_kernel_bytes"]
+    def roofline_of(st, per_step_launches, note):
+        """dominant kernel k_count2: algorithmic bytes (the corpus, read once) / its device time,
+        event-timed on the library's stream by the launches' own dispatch packets"""
+        a = {k: sum(x[k] for x in st) / len(st) for k in st[0]}
+        if a["count_kernel_ms"] <= 0:
+            return None
+        kms, kb = a["count_kernel_ms"], a["count_kernel_bytes"]
         achieved = kb / (kms / 1e3) / 1e9
         traffic = None
         tf = ROOT / "profiles" / "traffic.json"
         if tf.exists():
-            traffic = json.loads(tf.read_text()).get("k_count_words")
-        roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": "k_count_words", "launches_per_step": 1,
-                    "timed_launches": len(stats), "avg_launch_us": round(kms * 1e3, 3),
-                    "bytes_per_launch": kb,
-                    "note": "rank 0's slab when n_gpus > 1" if n_gpus > 1 else None}
-    trips = avg["n_trips"]
-    merge_loop = {
-        "rounds": rounds, "trips": int(trips),
-        "ms": round(avg["t_merge_ms"], 2),
-        "us_per_trip": round(avg["t_merge_ms"] * 1e3 / trips, 2) if trips else None,
-        "us_per_round": round(avg["t_merge_ms"] * 1e3 / max(1, rounds), 3),
-        "k_merge_batch_us": (round(avg["merge_kernel_ms"] * 1e3 / avg["merge_kernel_launches"], 2)
-                             if avg["merge_kernel_launches"] else None),
-        "k_merge_batch_bytes_per_launch": (round(avg["merge_kernel_bytes"] / avg["merge_kernel_launches"])
-                                           if avg["merge_kernel_launches"] else None),
-    }
+            traffic = json.loads(tf.read_text()).get("k_count2")
+        return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": "k_count2", "launches_per_step": per_step_launches,
+                "timed_launches": len(st) * (per_step_launches or 1), "avg_launch_us": round(kms * 1e3, 3),
+                "bytes_per_launch": kb, "note": note}
+    if not args.no_file:
+        n_gpus = int(stats[-1]["n_gpus"])
+    else:
+        n_gpus = env_world if multiproc else 1
 
     # ---------------------------------------------------------------- corpus resident in HBM
     device_resident = None
@@ -201,12 +195,13 @@ def main():
         _lib.check(L.bpe_synth_corpus_device(ctypes.c_void_p(corpus.data_ptr()), slab, args.seed,
                                              args.flavour, b0, None), "synth")
         torch.cuda.synchronize()
+    dstats = []
     if corpus is not None and not args.no_device_resident:
         def train_dev():
             return train_bpe_device(corpus.data_ptr(), slab, args.vocab, [EOT], comm=comm)
         for _ in range(args.warmup):
             v2, m2 = train_dev()
-        dstats = []
+        L.bpe_set_timing(0 if args.no_timing else 1)
         barrier()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
@@ -216,6 +211,11 @@ def main():
         torch.cuda.synchronize()
         barrier()
         el = max_over_ranks(time.perf_counter() - t1)
+        L.bpe_set_timing(0)
+        if args.no_file:
+            vocab, merges = v2, m2
+            elapsed = el
+            stats = dstats
         assert m2 == merges and v2 == vocab, "device-resident result differs from the file result"
         s0 = dstats[-1]
         device_resident = {
@@ -223,6 +223,29 @@ def main():
             "ms_per_step": round(el / args.steps * 1e3, 2),
             "phases_ms": {k: round(s0[k], 2) for k in ("t_prepare_ms", "t_count_ms", "t_exchange_ms",
                                                         "t_words_ms", "t_merge_ms", "t_total_ms")}}
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = n / (elapsed / args.steps) / 1e6
+    rounds = len(merges)
+    avg = {k: sum(x[k] for x in stats) / len(stats) for k in stats[0]}
+    trips = avg["n_trips"]
+    merge_loop = {
+        "rounds": rounds, "trips": int(trips),
+        "ms": round(avg["t_merge_ms"], 2),
+        "us_per_trip": round(avg["t_merge_ms"] * 1e3 / trips, 2) if trips else None,
+        "us_per_round": round(avg["t_merge_ms"] * 1e3 / max(1, rounds), 3),
+        "k_merge_batch_us": (round(avg["merge_kernel_ms"] * 1e3 / avg["merge_kernel_launches"], 2)
+                             if avg["merge_kernel_launches"] else None),
+        "k_merge_batch_bytes_per_launch": (round(avg["merge_kernel_bytes"] / avg["merge_kernel_launches"])
+                                           if avg["merge_kernel_launches"] else None),
+    }
+    # the roofline line: k_count2 over the HBM-resident corpus (one launch per step, the launches
+    # rocprofv3 --no-file profiles see); without that run, the file path's per-segment launches
+    if dstats:
+        roofline = roofline_of(dstats, 1, ("corpus in HBM, one launch per step" +
+                                           ("; rank 0's slab" if n_gpus > 1 else "")))
+    else:
+        roofline = roofline_of(stats, None, "file path: summed over its per-segment launches")
 
     # ---------------------------------------------------------------- encode MB/s (device)
     encode = None
@@ -277,7 +300,8 @@ def main():
                    "one slab of the file per GPU, one all-gather of the unique-word tables, merge "
                    "loop on the union")
         line = {
-            "metric": "BPE train input MB/s (32k vocab), train_bpe(path) end to end",
+            "metric": ("BPE train input MB/s (32k vocab), train_bpe(path) end to end" if not args.no_file else
+                       "BPE train input MB/s (32k vocab), corpus in HBM (profiling run, --no-file)"),
             "value": round(value, 2), "unit": "MB/s", "n_gpus": n_gpus, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int64",
@@ -300,7 +324,7 @@ def main():
                                             "n_rounds_host", "n_index_builds", "n_trips")},
         }
         print(json.dumps(line), flush=True)
-        if not args.keep_corpus:
+        if not args.keep_corpus and need_file:
             path.unlink(missing_ok=True)
     if multiproc:
         dist.barrier()

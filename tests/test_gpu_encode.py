@@ -64,3 +64,22 @@ def test_encode_bench_corpus_sample_vs_oracle():
     want = oracle.encode(vocab, merges, ["<|endoftext|>"], text)
     assert len(got) == len(want)
     assert got == want
+
+
+def test_missing_special_after_save_and_from_files(tmp_path):
+    """A special missing from the vocab is added by the reference's quirk (tokenizer.py:35-38:
+    self.vocab[bytes] = len(self.vocab)); after save() / from_files() that entry comes back keyed
+    by bytes (so vocab_inv also holds id -> bytes), the quirk runs again and the special keeps its
+    id.  Encode must not trip over the inverted entry and must use that id."""
+    import bpe_amd
+    vocab, merges = bpe_amd.train_bpe(gpt2_files.FIXTURES / "corpus.en", 300, [])
+    sp = "<|x|>"
+    v = len(vocab)   # the id the missing special gets
+    tok = bpe_amd.Tokenizer(vocab, merges, [sp])
+    text = "the cat<|x|>sat on the mat<|x|>"
+    ids1 = tok.encode(text)
+    assert ids1.count(v) == 2
+    tok.save(str(tmp_path), "t")
+    tok2 = bpe_amd.Tokenizer.from_files(str(tmp_path / "t-vocab.pkl"), str(tmp_path / "t-merges.pkl"), [sp])
+    assert tok2.vocab_inv[sp.encode()] == v and tok2.vocab_inv[v] == sp.encode()
+    assert tok2.encode(text) == ids1

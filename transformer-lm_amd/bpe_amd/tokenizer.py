@@ -81,7 +81,11 @@ class Tokenizer:
     def _device(self):
         if self._handle is None:
             L = _lib.lib()
-            inv = [(i, b) for b, i in self.vocab_inv.items()]
+            # bytes -> int entries only: after save()/from_files() a missing special added by
+            # the reference quirk (self.vocab[b] = len(vocab), tokenizer.py:35-38) comes back as
+            # an int -> bytes entry of vocab_inv, which the reference's encode never consults
+            inv = [(i, b) for b, i in self.vocab_inv.items()
+                   if isinstance(b, (bytes, bytearray)) and isinstance(i, int)]
             vb = _lib.vocab_blob(dict(inv) if len({i for i, _ in inv}) == len(inv) else {})
             if len({i for i, _ in inv}) != len(inv):
                 # several byte strings share an id: pass the pairs as they are

@@ -68,6 +68,46 @@ PinnedPool& pool() {
     return *p;
 }
 
+// Device buffers for the corpus, kept across training calls (per device, checked out by one
+// call at a time): a fresh multi-GB allocation per call costs tens of ms (the driver clears it).
+struct CorpusBuf {
+    DevBuf<uint8_t> b;
+    int dev = -1;
+};
+struct CorpusCache {
+    std::mutex m;
+    std::vector<std::unique_ptr<CorpusBuf>> free_;
+};
+CorpusCache& corpus_cache() {
+    static CorpusCache* c = new CorpusCache;   // lives as long as the process
+    return *c;
+}
+std::unique_ptr<CorpusBuf> corpus_take(size_t n) {
+    int dev = 0;
+    BPE_HIP(hipGetDevice(&dev));
+    std::unique_ptr<CorpusBuf> x;
+    {
+        std::lock_guard<std::mutex> g(corpus_cache().m);
+        auto& f = corpus_cache().free_;
+        for (size_t i = 0; i < f.size(); ++i)
+            if (f[i]->dev == dev) {   // this device's buffer: reuse it if it is large enough
+                x = std::move(f[i]);
+                f.erase(f.begin() + i);
+                break;
+            }
+    }
+    if (x && x->b.n >= n) return x;
+    if (!x) x = std::make_unique<CorpusBuf>();
+    x->b.release();
+    x->b.alloc(n);
+    x->dev = dev;
+    return x;
+}
+void corpus_give(std::unique_ptr<CorpusBuf> x) {
+    std::lock_guard<std::mutex> g(corpus_cache().m);
+    corpus_cache().free_.push_back(std::move(x));
+}
+
 [[noreturn]] void io_error(int en, const std::string& what) {
     throw Error{BPE_E_IO, what + ": " + std::strerror(en), en};
 }
@@ -398,19 +438,19 @@ void train_source(const Source& src, int vocab_size, const std::vector<std::stri
         hipStream_t s = nullptr;
         BPE_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
         struct SGuard { hipStream_t s; ~SGuard() { (void)hipStreamDestroy(s); } } sg{s};
-        DevBuf<uint8_t> d(std::max<size_t>(src.size, 1));
+        std::unique_ptr<CorpusBuf> d = corpus_take(std::max<size_t>(src.size, 1));
         const double a_ms = ms();
         Prepared pre;
-        const bool counted = load_and_count(src, 0, src.size, d.p, dev[0], io_threads(), s, pre);
+        const bool counted = load_and_count(src, 0, src.size, d->b.p, dev[0], io_threads(), s, pre);
         const double load_ms = counted ? a_ms + pre.load_ms : ms();
         const double before_train = ms();
-        train_on_device(d.p, src.size, vocab_size, specials, nullptr, s, out, TrainOpts{}, counted ? &pre : nullptr);
+        train_on_device(d->b.p, src.size, vocab_size, specials, nullptr, s, out, TrainOpts{}, counted ? &pre : nullptr);
         if (dtrace) {
             const double tr = ms();
-            d.release();
-            std::fprintf(stderr, "[bpe355 drive] alloc %.1f stage %.1f train %.1f free %.1f ms\n", a_ms,
-                         load_ms - a_ms, tr - load_ms, ms() - tr);
+            std::fprintf(stderr, "[bpe355 drive] alloc %.1f stage %.1f train %.1f ms\n", a_ms, load_ms - a_ms,
+                         tr - load_ms);
         }
+        corpus_give(std::move(d));
         out.stats.t_load_ms = load_ms;
         out.stats.t_total_ms += before_train;
         out.stats.n_gpus = 1;
@@ -433,7 +473,8 @@ void train_source(const Source& src, int vocab_size, const std::vector<std::stri
             BPE_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
             struct SGuard { hipStream_t s; ~SGuard() { (void)hipStreamDestroy(s); } } sg{s};
             const size_t len = cut[r + 1] - cut[r];
-            DevBuf<uint8_t> d(std::max<size_t>(len, 1));
+            std::unique_ptr<CorpusBuf> dbuf = corpus_take(std::max<size_t>(len, 1));
+            uint8_t* const d = dbuf->b.p;
             TrainOpts opt;
             opt.slab_offset = cut[r];
             // every rank holds the union and one trains on it; per-round exchange: all of them
@@ -441,15 +482,16 @@ void train_source(const Source& src, int vocab_size, const std::vector<std::stri
             Prepared pre;
             bool counted = false;
             try {
-                counted = load_and_count(src, cut[r], len, d.p, dev[r], per, s, pre);
+                counted = load_and_count(src, cut[r], len, d, dev[r], per, s, pre);
             } catch (const Error& e) {
                 opt.pending = e;   // reported by all ranks together, before any collective
                 opt.has_pending = true;
             }
             load_ms[r] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             auto comm = inproc ? make_inproc_comm(group, g, r, dev[r]) : make_rccl_comm(id, g, r, dev[r]);
-            train_on_device(d.p, len, vocab_size, specials, comm.get(), s, outs[r], opt, counted ? &pre : nullptr);
+            train_on_device(d, len, vocab_size, specials, comm.get(), s, outs[r], opt, counted ? &pre : nullptr);
             BPE_HIP(hipStreamSynchronize(s));
+            corpus_give(std::move(dbuf));
         } catch (...) {
             errs[r] = std::current_exception();
         }
@@ -487,20 +529,22 @@ void train_source_comm(const Source& src, bool split, int vocab_size, const std:
     hipStream_t s = nullptr;
     BPE_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     struct SGuard { hipStream_t s; ~SGuard() { (void)hipStreamDestroy(s); } } sg{s};
-    DevBuf<uint8_t> d(std::max<size_t>(hi - lo, 1));
+    std::unique_ptr<CorpusBuf> dbuf = corpus_take(std::max<size_t>(hi - lo, 1));
+    uint8_t* const d = dbuf->b.p;
     TrainOpts opt;
     opt.slab_offset = lo;
     Prepared pre;
     bool counted = false;
     try {
-        counted = load_and_count(src, lo, hi - lo, d.p, dev, io_threads(), s, pre);
+        counted = load_and_count(src, lo, hi - lo, d, dev, io_threads(), s, pre);
     } catch (const Error& e) {
         if (!comm || comm->nranks == 1) throw;
         opt.pending = e;
         opt.has_pending = true;
     }
     const double before_train = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    train_on_device(d.p, hi - lo, vocab_size, specials, comm, s, out, opt, counted ? &pre : nullptr);
+    train_on_device(d, hi - lo, vocab_size, specials, comm, s, out, opt, counted ? &pre : nullptr);
+    corpus_give(std::move(dbuf));
     out.stats.t_load_ms = counted ? pre.load_ms : before_train;
     out.stats.t_total_ms += before_train;
     out.stats.n_gpus = comm ? comm->nranks : 1;
