@@ -176,6 +176,11 @@ int bpe_tok_encode_chunks(bpe_tokenizer* tok, const uint8_t* utf8, size_t n, con
                           size_t n_starts, uint32_t* ids_out, size_t cap, size_t* n_out);
 int bpe_tok_encode_chunks_device(bpe_tokenizer* tok, const uint8_t* d_utf8, size_t n, const uint64_t* starts,
                                  size_t n_starts, uint32_t* d_out, size_t* n_out, void* hip_stream);
+/* encode(text) on n_gpus devices of this process (<= 0: every visible one; SURVEY.md 8b's n_gpus):
+ * the text is cut at safe split points that no special token spans, each device encodes its
+ * piece, the ids are concatenated -- identical to bpe_tok_encode (tokenizer.py:111-138). */
+int bpe_tok_encode_gpus(bpe_tokenizer* tok, const uint8_t* utf8, size_t n, uint32_t* ids_out, size_t cap,
+                        size_t* n_out, int n_gpus);
 void bpe_tok_free(bpe_tokenizer* tok);
 
 /* ---------------------------------------------------------------- decode */

@@ -83,3 +83,30 @@ def test_missing_special_after_save_and_from_files(tmp_path):
     tok2 = bpe_amd.Tokenizer.from_files(str(tmp_path / "t-vocab.pkl"), str(tmp_path / "t-merges.pkl"), [sp])
     assert tok2.vocab_inv[sp.encode()] == v and tok2.vocab_inv[v] == sp.encode()
     assert tok2.encode(text) == ids1
+
+
+@pytest.mark.parametrize("ranks", [2, 3, 5])
+def test_encode_several_devices_equals_one(ranks, monkeypatch):
+    """bpe_tok_encode_gpus: the text cut at safe points no special spans, one device per piece,
+    ids concatenated -- equal to the single-device encode and to the oracle.  A special with
+    spaces inside ("<|end of doc|>") puts safe points inside its occurrences, which the cuts must
+    avoid.  The ranks share this box's one GPU (BPE355_INPROC_RANKS)."""
+    import bpe_amd
+    import synth_text
+    monkeypatch.setenv("BPE355_INPROC_RANKS", "1")
+    specials = ["<|endoftext|>", "<|end of doc|>"]
+    vocab, merges = bpe_amd.train_bpe(gpt2_files.FIXTURES / "corpus.en", 600, specials)
+    parts = []
+    for i in range(40):
+        parts.append(synth_text.generate(90 + i, 3000, "mixed" if i % 2 else "ascii"))
+        parts.append(specials[i % 2])
+    text = "".join(parts)
+    tok = bpe_amd.Tokenizer(vocab, merges, specials)
+    one = tok.encode(text)
+    try:
+        bpe_amd.set_num_gpus(ranks)
+        many = tok.encode(text)
+    finally:
+        bpe_amd.set_num_gpus(None)
+    assert many == one
+    assert one == oracle.encode(vocab, merges, specials, text)

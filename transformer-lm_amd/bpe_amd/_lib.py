@@ -94,6 +94,7 @@ _SIGS = [
     ("bpe_tok_special_id", ctypes.c_int64, [_P, ctypes.c_int]),
     ("bpe_tok_encode", ctypes.c_int, [_P, _U8P, _SZ, _P, _SZ, ctypes.POINTER(_SZ)]),
     ("bpe_tok_encode_device", ctypes.c_int, [_P, _P, _SZ, _P, ctypes.POINTER(_SZ), _P]),
+    ("bpe_tok_encode_gpus", ctypes.c_int, [_P, _U8P, _SZ, _P, _SZ, ctypes.POINTER(_SZ), ctypes.c_int]),
     ("bpe_tok_encode_chunks", ctypes.c_int, [_P, _U8P, _SZ, _P, _SZ, _P, _SZ, ctypes.POINTER(_SZ)]),
     ("bpe_tok_encode_chunks_device", ctypes.c_int, [_P, _P, _SZ, _P, _SZ, _P, ctypes.POINTER(_SZ), _P]),
     ("bpe_tok_free", None, [_P]),

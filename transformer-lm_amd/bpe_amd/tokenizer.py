@@ -120,8 +120,13 @@ class Tokenizer:
         cap = max(1, len(data))
         out = (ctypes.c_uint32 * cap)()
         n_out = ctypes.c_size_t(0)
-        _lib.check(_lib.lib().bpe_tok_encode(h, data, len(data), out, cap, ctypes.byref(n_out)),
-                   "encode")
+        from .train import num_gpus
+        g = num_gpus()
+        if g == 1:
+            rc = _lib.lib().bpe_tok_encode(h, data, len(data), out, cap, ctypes.byref(n_out))
+        else:   # one process, several devices (bpe_amd.set_num_gpus / BPE355_GPUS)
+            rc = _lib.lib().bpe_tok_encode_gpus(h, data, len(data), out, cap, ctypes.byref(n_out), g)
+        _lib.check(rc, "encode")
         return list(out[: n_out.value])
 
     def encode_iterable(self, iterable: Iterable[str]) -> Iterator[int]:

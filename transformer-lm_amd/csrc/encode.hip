@@ -22,11 +22,15 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
+#include "drive.h"
 #include "internal.h"
 #include "pretok.h"
 #include "stage.h"
@@ -433,6 +437,13 @@ struct bpe_tokenizer {
     // re-allocating tens of GB per call costs up to seconds in the driver (measured 0.5 -> 2.8 s
     // for an 11.9 GB encode).  Calls on one handle are serialized on its stream.
     bpe::DevBuf<uint32_t> recs_cache;
+    // construction inputs, to build the same tables for the other ranks of a multi-device encode
+    // (bpe_tok_encode_gpus); those copies own their stream and record buffer
+    std::string vblob, mblob;
+    std::vector<std::string> sp_in;
+    int device = 0;
+    std::mutex copies_m;
+    std::vector<std::pair<long long, std::unique_ptr<bpe_tokenizer>>> copies;   // (rank << 8 | device)
     ~bpe_tokenizer() {
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -727,6 +738,92 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
     return total;
 }
 
+// ------------------------------------------------------------------ several devices
+// The tokenizer for rank r on device dev: the handle itself for rank 0 on its own device, else a
+// copy built from the same inputs (every rank owns its stream and record buffer, also when
+// ranks share a device in tests).  The caller has made `dev` current.
+bpe_tokenizer& tok_for_rank(bpe_tokenizer& T, int r, int dev) {
+    if (r == 0 && dev == T.device) return T;
+    const long long key = ((long long)r << 8) | dev;
+    std::lock_guard<std::mutex> g(T.copies_m);
+    for (auto& c : T.copies)
+        if (c.first == key) return *c.second;
+    auto U = std::make_unique<bpe_tokenizer>();
+    build_tokenizer(*U, reinterpret_cast<const uint8_t*>(T.vblob.data()), T.vblob.size(),
+                    reinterpret_cast<const uint8_t*>(T.mblob.data()), T.mblob.size(), T.sp_in);
+    U->device = dev;
+    T.copies.emplace_back(key, std::move(U));
+    return *T.copies.back().second;
+}
+
+// g + 1 cut points of text[0, n) for separate encodes whose ids concatenate to encode(text): safe
+// split points (a U+0020 between ASCII non-space bytes: the pre-tokens on both sides are those
+// of the whole, pretok.h) that no occurrence of any special token spans, so re.split's leftmost
+// matches (tokenizer.py:63-66) are those of the whole text too.  A slab with no such point is
+// empty (its neighbour takes the text).
+std::vector<size_t> encode_cuts(const uint8_t* t, size_t n, int g, const std::vector<std::string>& sp) {
+    std::vector<size_t> cut{0};
+    for (int r = 1; r < g; ++r) {
+        size_t p = n / (size_t)g * (size_t)r;
+        for (;;) {
+            p = p >= 1 ? bpe_safe_split(t, n, p) : 0;
+            if (p == 0 || p <= cut.back()) { p = cut.back(); break; }
+            bool spans = false;
+            for (const auto& x : sp) {
+                const size_t L = x.size();
+                for (size_t q = p + 1 > L ? p + 1 - L : 0; q < p && q + L <= n && !spans; ++q)
+                    spans = std::memcmp(t + q, x.data(), L) == 0;
+                if (spans) break;
+            }
+            if (!spans) break;
+            --p;   // a special spans it: look further back
+        }
+        cut.push_back(p);
+    }
+    cut.push_back(n);
+    return cut;
+}
+
+size_t encode_gpus(bpe_tokenizer& T, const uint8_t* utf8, size_t n, uint32_t* ids_out, int n_gpus) {
+    int cur = 0;
+    BPE_HIP(hipGetDevice(&cur));
+    const std::vector<int> dev = pick_devices(n_gpus);
+    const int g = (int)dev.size();
+    const std::vector<size_t> cut = encode_cuts(utf8, n, g, T.specials);
+    std::vector<std::vector<uint32_t>> ids(g);
+    std::vector<std::exception_ptr> errs(g);
+    auto work = [&](int r) {
+        try {
+            BPE_HIP(hipSetDevice(dev[r]));
+            const size_t len = cut[r + 1] - cut[r];
+            if (len == 0) return;
+            bpe_tokenizer& U = tok_for_rank(T, r, dev[r]);
+            DevBuf<uint8_t> d_text(len);
+            DevBuf<uint32_t> d_out(len);
+            BPE_HIP(hipMemcpyAsync(d_text.p, utf8 + cut[r], len, hipMemcpyHostToDevice, U.stream));
+            const size_t m = encode_device(U, d_text.p, len, d_out.p, U.stream);
+            ids[r].resize(m);
+            if (m) BPE_HIP(hipMemcpyAsync(ids[r].data(), d_out.p, m * 4, hipMemcpyDeviceToHost, U.stream));
+            BPE_HIP(hipStreamSynchronize(U.stream));
+        } catch (...) {
+            errs[r] = std::current_exception();
+        }
+    };
+    std::vector<std::thread> th;
+    for (int r = 1; r < g; ++r) th.emplace_back(work, r);
+    work(0);
+    for (auto& x : th) x.join();
+    (void)hipSetDevice(cur);
+    for (auto& e : errs)   // the earliest slab's error: the one encode(text) would raise first
+        if (e) std::rethrow_exception(e);
+    size_t m = 0;
+    for (int r = 0; r < g; ++r) {
+        if (!ids[r].empty()) std::memcpy(ids_out + m, ids[r].data(), ids[r].size() * 4);
+        m += ids[r].size();
+    }
+    return m;
+}
+
 template <class F>
 int guarded_enc(F&& f) {
     try {
@@ -762,6 +859,10 @@ int bpe_tok_create(const uint8_t* vocab_blob, size_t vocab_n, const uint8_t* mer
         }
         auto T = std::make_unique<bpe_tokenizer>();
         bpe::build_tokenizer(*T, vocab_blob, vocab_n, merges_blob, merges_n, sp);
+        T->vblob.assign(reinterpret_cast<const char*>(vocab_blob), vocab_n);
+        T->mblob.assign(reinterpret_cast<const char*>(merges_blob), merges_n);
+        T->sp_in = sp;
+        BPE_HIP(hipGetDevice(&T->device));
         *out = T.release();
     });
 }
@@ -828,6 +929,17 @@ int bpe_tok_encode_chunks(bpe_tokenizer* tok, const uint8_t* utf8, size_t n, con
         if (m) BPE_HIP(hipMemcpyAsync(ids_out, d_out.p, m * 4, hipMemcpyDeviceToHost, tok->stream));
         BPE_HIP(hipStreamSynchronize(tok->stream));
         *n_out = m;
+    });
+}
+
+int bpe_tok_encode_gpus(bpe_tokenizer* tok, const uint8_t* utf8, size_t n, uint32_t* ids_out, size_t cap,
+                        size_t* n_out, int n_gpus) {
+    return bpe::guarded_enc([&] {
+        BPE_REQUIRE(tok && n_out && (n == 0 || (utf8 && ids_out)), BPE_E_ARG, "NULL argument");
+        BPE_REQUIRE(cap >= n, BPE_E_ARG, "ids_out capacity must be >= input bytes");
+        *n_out = 0;
+        if (n == 0) return;
+        *n_out = bpe::encode_gpus(*tok, utf8, n, ids_out, n_gpus);
     });
 }
 

@@ -1330,14 +1330,17 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
 
     unsigned singles = 0;
     const unsigned bid = blockIdx.x;
+    // the host may launch fewer blocks than the slot-class layout has (short posting lists late
+    // in training): every loop below strides over the nb blocks that exist
+    const unsigned nb = gridDim.x < W.lblk0 ? gridDim.x : W.lblk0;
     if (k == 1) {
         // one member: the per-round rewrite (index list or a scan of every slot)
         const BatchMember& M = B.m[0];
         const TokT ta = (TokT)M.a, tb = (TokT)M.b, tn = (TokT)M.nw;
         const DeltaSinkN<kLdsB> D{LRt, (LdsU64*)l_lr};
-        if (M.use_list && bid < W.lblk0) {
+        if (M.use_list && bid < nb) {
             const uint32_t* L = X.list + M.list_beg;
-            for (unsigned i = bid * blockDim.x + tid; i < M.list_len; i += W.lblk0 * blockDim.x) {
+            for (unsigned i = bid * blockDim.x + tid; i < M.list_len; i += nb * blockDim.x) {
                 const unsigned f = L[i];
                 if (f < W.off[1]) merge_one<TokT, 0>(W.c[0], f, ta, tb, tn, D, singles);
                 else if (f < W.off[2]) merge_one<TokT, 1>(W.c[1], f - W.off[1], ta, tb, tn, D, singles);
@@ -1345,22 +1348,24 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
                 else merge_one<TokT, 3>(W.c[3], f - W.off[3], ta, tb, tn, D, singles);
             }
         } else if (!M.use_list) {
-            if (bid < W.c[1].blk0) {
-                if (bid < W.c[0].blk0 + W.c[0].nblk)
-                    scan_class<TokT, 0>(W.c[0], bid - W.c[0].blk0, ta, tb, tn, D, singles);
-            } else if (bid < W.c[2].blk0) {
-                scan_class<TokT, 1>(W.c[1], bid - W.c[1].blk0, ta, tb, tn, D, singles);
-            } else if (bid < W.c[3].blk0) {
-                scan_class<TokT, 2>(W.c[2], bid - W.c[2].blk0, ta, tb, tn, D, singles);
-            } else if (bid < W.lblk0) {
-                scan_class<TokT, 3>(W.c[3], bid - W.c[3].blk0, ta, tb, tn, D, singles);
+            for (unsigned bb = bid; bb < W.lblk0; bb += nb) {
+                if (bb < W.c[1].blk0) {
+                    if (bb < W.c[0].blk0 + W.c[0].nblk)
+                        scan_class<TokT, 0>(W.c[0], bb - W.c[0].blk0, ta, tb, tn, D, singles);
+                } else if (bb < W.c[2].blk0) {
+                    scan_class<TokT, 1>(W.c[1], bb - W.c[1].blk0, ta, tb, tn, D, singles);
+                } else if (bb < W.c[3].blk0) {
+                    scan_class<TokT, 2>(W.c[2], bb - W.c[2].blk0, ta, tb, tn, D, singles);
+                } else {
+                    scan_class<TokT, 3>(W.c[3], bb - W.c[3].blk0, ta, tb, tn, D, singles);
+                }
             }
         }
-    } else if (bid < W.lblk0) {
+    } else if (bid < nb) {
         // several members: every word that can contain one of them, once, all members in order
         if (B.full_scan) {
             const unsigned total = W.off[kNumCls];
-            for (unsigned f = bid * blockDim.x + tid; f < total; f += W.lblk0 * blockDim.x) {
+            for (unsigned f = bid * blockDim.x + tid; f < total; f += nb * blockDim.x) {
                 if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f,  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles);
                 else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles);
                 else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles);
@@ -1368,7 +1373,7 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
             }
         } else {
             const unsigned total = B.list_pre[k];
-            for (unsigned i = bid * blockDim.x + tid; i < total; i += W.lblk0 * blockDim.x) {
+            for (unsigned i = bid * blockDim.x + tid; i < total; i += nb * blockDim.x) {
                 int j = 0;
                 while (j + 1 < k && i >= B.list_pre[j + 1]) ++j;
                 const unsigned f = X.list[B.m[j].list_beg + (i - B.list_pre[j])];
@@ -2137,6 +2142,7 @@ class MergeLoop {
     HostWords<TokT> words_;
     WordsDev<TokT> wdev_{};
     unsigned merge_grid_ = 1;
+    unsigned merge_grid_cur_ = 0;   // k_merge_batch blocks for the next block of trips (0: merge_grid_)
     double scan_bytes_ = 0, long_bytes_ = 0;
     unsigned long long long_tokens_ = 0;
     unsigned n_live_ = 0;
@@ -2168,6 +2174,7 @@ class MergeLoop {
     hipEvent_t blk_ev_[2] = {nullptr, nullptr};
     long long slot_base_[2] = {0, 0};   // trips launched before each slot's block
     void launch_block(int slot, bool timing, std::vector<hipEvent_t>& ev);
+    unsigned merge_grid() const;
     void finish_block(int slot, bool timing, std::vector<hipEvent_t>& ev, double& k1_ms, double& k1_bytes,
                       long long& k1_launches);
     DevBuf<unsigned long long> probe_;   // BPE355_PROBE stamps
@@ -2836,6 +2843,14 @@ void MergeLoop<TokT>::reset_tags() {
 // sees st->halt).  With timing on, k_merge_batch is event-timed on one trip in kTimingStride
 // (events stamped by its own dispatch packet).
 template <class TokT>
+unsigned MergeLoop<TokT>::merge_grid() const {
+    static const bool fixed = std::getenv("BPE355_MERGE_GRID_FIXED") != nullptr;   // A/B knob
+    // long words are handled by the blocks past the slot-class layout: those need the full grid
+    if (fixed || wdev_.ln > 0 || merge_grid_cur_ == 0) return merge_grid_;
+    return std::min(merge_grid_cur_, merge_grid_);
+}
+
+template <class TokT>
 void MergeLoop<TokT>::launch_block(int slot, bool timing, std::vector<hipEvent_t>& ev) {
     const size_t lr_member = 2ull * tok_cap_, lr_parity = (size_t)kMaxBatch * lr_member;
     const unsigned ntb = tok_cap_;
@@ -2848,7 +2863,7 @@ void MergeLoop<TokT>::launch_block(int slot, bool timing, std::vector<hipEvent_t
         hipLaunchKernelGGL(k_select, dim3(1), dim3(kSelThreads), 0, s_, st_.p, bs_.p, pairs(), toks(), idev_,
                            batch_.p, (const Partial*)part_.p, (const Partial*)list_.p, m_a_.p, m_b_.p, m_new_.p,
                            m_mode_.p, m_cnt_.p, ti, t);
-        hipExtLaunchKernelGGL(k_merge_batch<TokT>, dim3(merge_grid_), dim3(256), 0, s_,
+        hipExtLaunchKernelGGL(k_merge_batch<TokT>, dim3(merge_grid()), dim3(256), 0, s_,
                               timed ? e[0] : nullptr, timed ? e[1] : nullptr, 0,
                               st_.p, (const Batch*)batch_.p, pairs(), toks(), wdev_, idev_, LR_.p, lr_member,
                               lr_parity, tags_.p);
@@ -2871,6 +2886,17 @@ void MergeLoop<TokT>::finish_block(int slot, bool timing, std::vector<hipEvent_t
     hs_ = snap_st_[slot];
     const int* ti = snap_ti_ + (size_t)slot * 4 * kTrips;
     for (int t = 0; t < kTrips; ++t) trips_run_ += ti[4 * t + 1] > 0;
+    {   // size the merge grid of the blocks launched from now on by this block's largest trip:
+        // the members' list entries at one per thread, twice over for growth; a full scan (or
+        // a single member without a list) wants the whole layout.  Any grid is correct.
+        unsigned need = kMaxBatch;
+        for (int t = 0; t < kTrips; ++t) {
+            if (ti[4 * t + 1] <= 0) continue;
+            if (ti[4 * t + 2]) { need = merge_grid_; break; }
+            need = std::max(need, 2 * ceil_div((unsigned)ti[4 * t + 3], 256u));
+        }
+        merge_grid_cur_ = std::max<unsigned>(64, need);
+    }
     if (!timing) return;
     const double slot_avg = scan_bytes_ / std::max(1u, idev_.n_slot_words + words_.ln);
     for (int t = 0; t < kTrips; ++t) {
