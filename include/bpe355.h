@@ -115,6 +115,11 @@ int64_t bpe_result_n_vocab(const bpe_result* r);
 /* blob views owned by the result */
 size_t bpe_result_merges_blob(const bpe_result* r, const uint8_t** data);
 size_t bpe_result_vocab_blob(const bpe_result* r, const uint8_t** data);
+/* The same records flat: which = 0 merges (a0, b0, a1, b1, ...), 1 vocab in id order; *lens gets
+ * one length per record, *bytes their concatenation (*n_bytes long); returns the record count.
+ * (Host-side plumbing for the Python shim: one buffer sliced, not one parse per record.) */
+size_t bpe_result_flat(const bpe_result* r, int which, const uint32_t** lens, const uint8_t** bytes,
+                       size_t* n_bytes);
 
 typedef struct {
     double t_total_ms;        /* whole call, host wall clock */

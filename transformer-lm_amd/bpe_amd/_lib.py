@@ -7,6 +7,7 @@ or no gfx950 device is visible, every compute call raises.
 from __future__ import annotations
 
 import ctypes
+import itertools
 import errno as _errno
 import os
 import re
@@ -86,6 +87,8 @@ _SIGS = [
     ("bpe_result_n_vocab", ctypes.c_int64, [_P]),
     ("bpe_result_merges_blob", _SZ, [_P, ctypes.POINTER(_P)]),
     ("bpe_result_vocab_blob", _SZ, [_P, ctypes.POINTER(_P)]),
+    ("bpe_result_flat", ctypes.c_size_t, [_P, ctypes.c_int, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32)),
+                                           ctypes.POINTER(_P), ctypes.POINTER(_SZ)]),
     ("bpe_result_stats", ctypes.c_int, [_P, ctypes.POINTER(TrainStats)]),
     ("bpe_result_free", None, [_P]),
     ("bpe_set_timing", None, [ctypes.c_int]),
@@ -181,19 +184,23 @@ def iter_records(blob: bytes):
 def take_result(res: ctypes.c_void_p):
     """-> (vocab dict[int, bytes], merges list[tuple[bytes, bytes]], stats dict); frees res."""
     L = lib()
+    def flat(which):
+        lens, data, nb = ctypes.POINTER(ctypes.c_uint32)(), ctypes.c_void_p(), ctypes.c_size_t(0)
+        n = L.bpe_result_flat(res, which, ctypes.byref(lens), ctypes.byref(data), ctypes.byref(nb))
+        if n == 0:
+            return []
+        off = list(itertools.accumulate(lens[:n], initial=0))
+        buf = ctypes.string_at(data, nb.value)
+        return list(map(buf.__getitem__, map(slice, off[:-1], off[1:])))
     try:
-        p = ctypes.c_void_p()
-        n = L.bpe_result_merges_blob(res, ctypes.byref(p))
-        mb = ctypes.string_at(p, n) if n else b""
-        n = L.bpe_result_vocab_blob(res, ctypes.byref(p))
-        vb = ctypes.string_at(p, n) if n else b""
+        m = flat(0)
+        v = flat(1)
         st = TrainStats()
         check(L.bpe_result_stats(res, ctypes.byref(st)), "stats")
     finally:
         L.bpe_result_free(res)
-    it = iter_records(mb)
-    merges = [(a, next(it)) for a in it]
-    vocab = {i: b for i, b in enumerate(iter_records(vb))}
+    merges = list(zip(m[0::2], m[1::2]))
+    vocab = dict(enumerate(v))
     return vocab, merges, st.as_dict()
 
 

@@ -84,6 +84,9 @@ bool timing_enabled() { return g_timing; }
 
 struct bpe_result {
     std::string merges_blob, vocab_blob;
+    // the same records as (lengths, concatenated bytes): the Python shim slices one buffer
+    std::vector<uint32_t> flat_len[2];   // 0: merges (a, b, a, b, ...), 1: vocab in id order
+    std::string flat_bytes[2];
     int64_t n_merges = 0, n_vocab = 0;
     bpe_train_stats stats{};
 };
@@ -119,10 +122,16 @@ void finish_result(bpe::TrainOutput& out, const std::vector<std::string>& specia
         r->merges_blob += m.first;
         bpe::put_u32(r->merges_blob, (uint32_t)m.second.size());
         r->merges_blob += m.second;
+        r->flat_len[0].push_back((uint32_t)m.first.size());
+        r->flat_len[0].push_back((uint32_t)m.second.size());
+        r->flat_bytes[0] += m.first;
+        r->flat_bytes[0] += m.second;
     }
     for (const auto* s : ids) {
         bpe::put_u32(r->vocab_blob, (uint32_t)s->size());
         r->vocab_blob += *s;
+        r->flat_len[1].push_back((uint32_t)s->size());
+        r->flat_bytes[1] += *s;
     }
     r->stats = out.stats;
 }
@@ -285,6 +294,15 @@ int bpe_word_counts(const uint8_t* data, size_t n, const char* const* specials, 
 }
 
 void bpe_blob_free(uint8_t* blob) { std::free(blob); }
+
+size_t bpe_result_flat(const bpe_result* r, int which, const uint32_t** lens, const uint8_t** bytes,
+                       size_t* n_bytes) {
+    if (!r || which < 0 || which > 1 || !lens || !bytes || !n_bytes) return 0;
+    *lens = r->flat_len[which].data();
+    *bytes = reinterpret_cast<const uint8_t*>(r->flat_bytes[which].data());
+    *n_bytes = r->flat_bytes[which].size();
+    return r->flat_len[which].size();
+}
 
 int64_t bpe_result_n_merges(const bpe_result* r) { return r ? r->n_merges : -1; }
 int64_t bpe_result_n_vocab(const bpe_result* r) { return r ? r->n_vocab : -1; }

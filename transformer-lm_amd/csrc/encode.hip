@@ -34,6 +34,7 @@
 #include "internal.h"
 #include "pretok.h"
 #include "stage.h"
+#include "stage2.h"
 
 namespace bpe {
 namespace {
@@ -276,6 +277,231 @@ k_enc_scan(const uint8_t* __restrict__ s, size_t n, size_t n_chunks, const Seg* 
         t_count[gt] = k;
         // cache eviction every kEncEpoch chunks (see k_count_words)
         if ((c - blockIdx.x) / gridDim.x % kEncEpoch == kEncEpoch - 1) {
+            __syncthreads();
+            for (int i = tid; i < kEncCache; i += blockDim.x) {
+                const unsigned long long kk = c_key[i];
+                if (kk == 0 || kk == kBusy) continue;
+                const uint16_t hh = c_hit[i];
+                if ((uint16_t)(hh - c_mark[i]) >= kEncKeep) { c_mark[i] = hh; continue; }
+                c_key[i] = 0;
+                c_hit[i] = 0;
+                c_mark[i] = 0;
+            }
+        }
+        const unsigned long long ins = wave_sum(inserted);
+        inserted = 0;
+        if ((tid & 63) == 0) s_red[tid >> 6] = ins;
+        __syncthreads();
+        if (tid == 0) {
+            const unsigned long long b = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+            if (b) atomicAdd(fill, b);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ 2'. the byte-parallel scan
+// The same pass with tokstart.h's predicate: every thread turns its 64-byte block into a
+// token-start mask, evaluated once per segment that overlaps the block on a window clipped to
+// that segment (bytes before the segment start read '\n', the segment end is the text end: each
+// segment is pre-tokenized on its own, tokenizer.py:68-90); a special segment is one token.  The
+// thread then records the pre-tokens that start in its block at recs[block + k] (a 64-byte block
+// holds at most 64), its span is (block, k).  The segments of a chunk's window sit in LDS.
+constexpr int kSegLds = 64;
+
+struct ClipWin {   // one block's window with the bytes before window position lo read as '\n'
+    int r0, lo;
+    __device__ __forceinline__ uint32_t byte(int j) const { return j < lo ? 0x0Au : g_stage[r0 + j]; }
+    __device__ __forceinline__ uint32_t dword(int k) const {
+        const uint32_t x = *reinterpret_cast<const uint32_t*>(g_stage + r0 + 4 * k);
+        const int q = lo - 4 * k;   // bytes of this dword before the segment start
+        if (q <= 0) return x;
+        if (q >= 4) return 0x0A0A0A0Au;
+        const uint32_t m = (1u << (8 * q)) - 1u;
+        return (x & ~m) | (0x0A0A0A0Au & m);
+    }
+};
+
+template <bool kAligned>
+__global__ void __launch_bounds__(256, 3)
+k_enc_scan2(const uint8_t* __restrict__ s, size_t n, size_t n_chunks, const Seg* __restrict__ segs,
+            int nseg, unsigned long long* __restrict__ kv, unsigned long long* __restrict__ pos,
+            size_t mask, unsigned long long max_fill, unsigned long long* __restrict__ fill,
+            uint32_t* __restrict__ recs, unsigned long long* __restrict__ t_start,
+            uint32_t* __restrict__ t_count, unsigned* __restrict__ status, int use_cache) {
+    __shared__ uint64_t s_mask[kWords], s_spec[kWords];
+    __shared__ unsigned long long c_key[kEncCache];
+    __shared__ uint64_t c_lo[kEncCache], c_hi[kEncCache];
+    __shared__ uint32_t c_slot[kEncCache];
+    __shared__ uint16_t c_hit[kEncCache], c_mark[kEncCache];
+    __shared__ Seg s_seg[kSegLds];
+    __shared__ int s_seg0, s_segn;   // first segment of the chunk window and how many are in LDS (-1: too many)
+    __shared__ unsigned long long s_red[4];
+    __shared__ int s_stop;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kEncCache; i += blockDim.x) { c_key[i] = 0; c_hit[i] = 0; c_mark[i] = 0; }
+    load_cls2(tid, blockDim.x);
+    unsigned long long inserted = 0;
+
+    // one pre-token [p, p + len) of src (global position gp); returns its record
+    auto word_rec = [&](const auto& src, auto p, size_t len, size_t gp) -> uint32_t {
+        if (len >= (1ULL << 24)) { atomicOr(status, 2u); return 0u; }
+        bool ins = false;
+        if (len <= (size_t)kInline) {
+            uint64_t wl = 0, wh = 0;
+            for (uint32_t i = 0; i < (uint32_t)len; ++i) {
+                const uint64_t b = src[p + i];
+                if (i < 8) wl |= b << (8 * i);
+                else wh |= b << (8 * (i - 8));
+            }
+            const uint64_t h = short_hash(wl, wh, len);
+            const unsigned ls = (unsigned)(h >> 40) & (kEncCache - 2);
+            for (int way = 0; way < 2 && use_cache; ++way) {
+                const unsigned sl = ls + way;
+                const unsigned long long k = c_key[sl];
+                if (k != 0 && k != kBusy && (k >> 40) == len) {
+                    __asm__ volatile("" ::: "memory");
+                    if (c_lo[sl] == wl && c_hi[sl] == wh) {
+                        c_hit[sl] = (uint16_t)(c_hit[sl] + 1);   // a heuristic: races may drop hits
+                        return c_slot[sl];
+                    }
+                }
+            }
+            const size_t slot = table_add(s, s, gp, len, wl, wh, h, 0, kv, pos, mask, status, &ins);
+            inserted += ins;
+            if (slot == ~(size_t)0) return 0u;
+            for (int way = 0; way < 2 && use_cache; ++way) {   // cache it if a way is free
+                const unsigned sl = ls + way;
+                if (c_key[sl] == 0 && atomicCAS(&c_key[sl], 0ULL, kBusy) == 0) {
+                    c_lo[sl] = wl;
+                    c_hi[sl] = wh;
+                    c_slot[sl] = (uint32_t)slot;
+                    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    atomicExch(&c_key[sl], ((unsigned long long)len << 40) | (gp + 1));
+                    break;
+                }
+            }
+            return (uint32_t)slot;
+        }
+        const size_t slot = table_add(s, s, gp, len, 0, 0, hash_word(s, gp, len), 0, kv, pos, mask,
+                                      status, &ins);
+        inserted += ins;
+        return slot == ~(size_t)0 ? 0u : (uint32_t)slot;
+    };
+
+    uint4 pre[kSVec];
+    if (blockIdx.x < n_chunks) fetch2<kAligned>(pre, s, n, (size_t)blockIdx.x * kChunk, tid);
+    for (size_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+        __syncthreads();
+        store2(pre, tid);
+        const size_t base = c * kChunk;
+        if (tid < 64) {   // wave 0: the segments that overlap the staged window, into LDS
+            const size_t w0 = base >= (size_t)kPre ? base - kPre : 0, w1 = base + kWin + kPost;
+            const int k0 = seg_of(segs, nseg, w0);
+            const int i = k0 + tid;
+            Seg sg{};
+            if (i < nseg) sg = segs[i];
+            const bool in = i < nseg && sg.start < w1;
+            if (in) s_seg[tid] = sg;
+            const unsigned long long b = __ballot(in);
+            if (tid == 0) {
+                s_seg0 = k0;
+                s_segn = (b == ~0ULL && k0 + 64 < nseg && segs[k0 + 64].start < w1) ? -1 : __popcll(b);
+                s_stop = *(volatile unsigned long long*)fill > max_fill;
+            }
+        }
+        __syncthreads();
+        if (s_stop) {
+            if (tid == 0) atomicOr(status, 1u);
+            break;
+        }
+        const int seg0 = s_seg0, segn = s_segn;
+        auto seg_at = [&](int i) -> Seg { return segn >= 0 ? s_seg[i - seg0] : segs[i]; };
+        const int seg_end = segn >= 0 ? seg0 + segn : nseg;
+        auto seg_find = [&](size_t p) -> int {   // the segment holding position p
+            if (segn < 0) return seg_of(segs, nseg, p);
+            int lo = seg0, hi = seg_end - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s_seg[mid - seg0].start <= p) lo = mid;
+                else hi = mid - 1;
+            }
+            return lo;
+        };
+
+        // ---- token starts of this thread's block, per overlapping segment
+        const size_t blk = base + 64 * (size_t)tid;
+        uint64_t starts = 0, spec = 0;
+        if (blk < n) {
+            const long long wstart = (long long)blk - kStartPre;
+            const int r0 = kPre + 64 * tid - kStartPre;
+            for (int i = seg_find(blk); i < seg_end; ++i) {
+                const Seg sg = seg_at(i);
+                if (sg.start >= blk + 64) break;
+                if (sg.end <= blk) continue;
+                if (sg.special >= 0) {
+                    if (sg.start >= blk) {
+                        starts |= 1ULL << (sg.start - blk);
+                        spec |= 1ULL << (sg.start - blk);
+                    }
+                    continue;
+                }
+                const long long lo = (long long)sg.start - wstart, hi = (long long)sg.end - wstart;
+                uint64_t m = token_starts64<DevTab>(ClipWin{r0, lo > 0 ? (int)lo : 0},
+                                                    (int)(hi < kStartWin ? hi : kStartWin));
+                const int a = sg.start > blk ? (int)(sg.start - blk) : 0;
+                const int e = sg.end < blk + 64 ? (int)(sg.end - blk) : 64;
+                m &= (e >= 64 ? ~0ULL : ((1ULL << e) - 1)) & (~0ULL << a);
+                if (sg.start >= blk) m |= 1ULL << a;   // the segment starts a token
+                starts |= m;
+            }
+        }
+        s_mask[tid] = starts;
+        s_spec[tid] = spec;
+        if (c + gridDim.x < n_chunks) fetch2<kAligned>(pre, s, n, (c + gridDim.x) * kChunk, tid);
+        __syncthreads();
+
+        // ---- one record per pre-token that starts in the block
+        const size_t rem = n > base ? n - base : 0;
+        const uint32_t tend = rem < (size_t)kWin ? (uint32_t)rem : (uint32_t)kWin;
+        const size_t gt = c * 256 + tid;
+        uint32_t k = 0;
+        uint64_t m = starts;
+        while (m) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t r = 64u * tid + j;
+            const size_t gp = base + r;
+            size_t e;   // end (global)
+            if (m) {
+                e = base + 64u * tid + (uint32_t)__builtin_ctzll(m);
+            } else {
+                e = ~(size_t)0;
+                for (int w = tid + 1; w < kWords; ++w) {
+                    const uint64_t x = s_mask[w];
+                    if (x) { e = base + 64u * w + (uint32_t)__builtin_ctzll(x); break; }
+                }
+                if (e == ~(size_t)0) {   // the chunk's last pre-token: its segment decides
+                    const Seg sg = seg_at(seg_find(gp));
+                    if ((spec >> j) & 1ULL) {
+                        e = sg.end;
+                    } else {
+                        const size_t lim = sg.end < base + tend ? sg.end : base + tend;
+                        e = base + token_end(StageText{}, (uint32_t)(lim - base), r);
+                        if (lim != sg.end && e + 4 > lim) e = token_end(s, (size_t)sg.end, gp);
+                    }
+                }
+            }
+            uint32_t rec;
+            if ((spec >> j) & 1ULL) rec = kSpecialRec | (uint32_t)seg_at(seg_find(gp)).special;
+            else if (e - gp <= (size_t)kInline) rec = word_rec(StageText{}, r, e - gp, gp);
+            else rec = word_rec(s, gp, e - gp, gp);
+            if (e <= gp || k >= 64) { atomicOr(status, 16u); break; }
+            recs[blk + k] = rec;
+            ++k;
+        }
+        t_start[gt] = k ? blk : 0;
+        t_count[gt] = k;
+        if ((c - blockIdx.x) / gridDim.x % kEncEpoch == kEncEpoch - 1) {   // cache eviction
             __syncthreads();
             for (int i = tid; i < kEncCache; i += blockDim.x) {
                 const unsigned long long kk = c_key[i];
@@ -640,9 +866,12 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
     const size_t n_chunks = (n + kChunk - 1) / kChunk;
     const size_t n_spans = n_chunks * 256;
     const bool aligned = (reinterpret_cast<uintptr_t>(d_text) & 15u) == 0;
-    auto kern = aligned ? k_enc_scan<true> : k_enc_scan<false>;
+    static const bool v1 = std::getenv("BPE355_ENC_SCAN_V1") != nullptr;   // A/B knob: the serial scan
+    auto kern = v1 ? (aligned ? k_enc_scan<true> : k_enc_scan<false>)
+                   : (aligned ? k_enc_scan2<true> : k_enc_scan2<false>);
+    const int lds = v1 ? kPadded : kStage;
     int per_cu = 0, dev = 0, n_cu = 0;
-    BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, kPadded));
+    BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds));
     BPE_HIP(hipGetDevice(&dev));
     BPE_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
     unsigned sgrid = (unsigned)std::min<size_t>(n_chunks, (size_t)std::max(1, per_cu) * std::max(1, n_cu));
@@ -662,7 +891,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
         BPE_HIP(hipMemsetAsync(kv.p, 0, kv.bytes(), s));
         BPE_HIP(hipMemsetAsync(status.p, 0, 4, s));
         BPE_HIP(hipMemsetAsync(fill.p, 0, 8, s));
-        hipLaunchKernelGGL(kern, dim3(sgrid), dim3(256), kPadded, s, d_text, n, n_chunks, d_segs.p, nseg,
+        hipLaunchKernelGGL(kern, dim3(sgrid), dim3(256), lds, s, d_text, n, n_chunks, d_segs.p, nseg,
                            kv.p, pos.p, cap - 1, (unsigned long long)(cap / 2), fill.p, recs,
                            t_start.p, t_count.p, status.p,
                            std::getenv("BPE355_NOCACHE") ? 0 : 1);   // test knob: global table only

@@ -2844,9 +2844,12 @@ void MergeLoop<TokT>::reset_tags() {
 // (events stamped by its own dispatch packet).
 template <class TokT>
 unsigned MergeLoop<TokT>::merge_grid() const {
-    static const bool fixed = std::getenv("BPE355_MERGE_GRID_FIXED") != nullptr;   // A/B knob
+    // experiment knob: size the grid from the last block's trips (measured slower at the bench
+    // config, 531 vs 365 ms of merges: list sizes vary too much from one block of trips to the
+    // next), so the full layout is the default
+    static const bool adaptive = std::getenv("BPE355_MERGE_GRID_ADAPTIVE") != nullptr;
     // long words are handled by the blocks past the slot-class layout: those need the full grid
-    if (fixed || wdev_.ln > 0 || merge_grid_cur_ == 0) return merge_grid_;
+    if (!adaptive || wdev_.ln > 0 || merge_grid_cur_ == 0) return merge_grid_;
     return std::min(merge_grid_cur_, merge_grid_);
 }
 
