@@ -24,8 +24,13 @@ struct RecPool {
     unsigned max_pages;
     int* wg_page;          // per counting workgroup: its current page (-2 none yet, -1 pool spent)
     unsigned* wg_used;
+    unsigned* page_ch;     // per page: records per coarse bin (kCoarse), written with page_used
+    unsigned* wg_ch;       // per counting workgroup: its current page's coarse histogram
     int on;
 };
+
+constexpr int kCoarseBits = 6;   // first partition level: the top 6 bits of the word hash
+constexpr int kCoarse = 1 << kCoarseBits;
 
 // Three parallel u64 arrays of one capacity, on one device.  Large record arrays are kept across
 // training calls (ScratchArrays::take / give): freeing and re-allocating tens of GB per call
@@ -40,7 +45,7 @@ void scratch_give(std::unique_ptr<Arrays3> x);
 
 struct RecPoolOwner {
     std::unique_ptr<Arrays3> rec;    // the pool: lo, hi, meta
-    DevBuf<unsigned> page_used, n_pages, wg_used;
+    DevBuf<unsigned> page_used, n_pages, wg_used, page_ch, wg_ch;
     DevBuf<int> wg_page;
     unsigned max_pages = 0, n_wg = 0, pages_used = 0;
     unsigned long long records = 0;

@@ -64,8 +64,9 @@ __global__ void __launch_bounds__(256) k_count2(const uint8_t* __restrict__ s, s
     __shared__ unsigned c_cnt[kCache2];
     __shared__ uint16_t c_mark[kCache2];
     __shared__ unsigned long long s_red[4];
-    __shared__ int s_stop, s_page;
+    __shared__ int s_stop, s_page, s_old;
     __shared__ unsigned s_used;
+    __shared__ unsigned s_ch[kCoarse];   // the current page's records per coarse bin
     const int tid = threadIdx.x;
     for (int i = tid; i < kCache2; i += blockDim.x) { c_key[i] = 0; c_cnt[i] = 0; c_mark[i] = 0; }
     load_cls2(tid, blockDim.x);
@@ -73,13 +74,15 @@ __global__ void __launch_bounds__(256) k_count2(const uint8_t* __restrict__ s, s
         s_page = R.on ? R.wg_page[blockIdx.x] : -1;
         s_used = R.on ? R.wg_used[blockIdx.x] : 0u;
     }
+    if (tid < kCoarse) s_ch[tid] = R.on ? R.wg_ch[(size_t)blockIdx.x * kCoarse + tid] : 0u;
     unsigned long long ntok = 0, inserted = 0, n_miss = 0, n_long = 0;
 
     // a miss (or an evicted / flushed cache entry): a record in this workgroup's page, else the
     // global table
-    auto spill = [&](uint64_t wl, uint64_t wh, size_t len, size_t gpos, unsigned long long c) {
+    auto spill = [&](uint64_t wl, uint64_t wh, size_t len, size_t gpos, unsigned long long c, uint64_t h) {
         const int pg = s_page;
         if (pg >= 0 && c < (1ULL << kCntBits)) {
+            atomicAdd(&s_ch[h >> (64 - kCoarseBits)], 1u);
             const unsigned idx = atomicAdd(&s_used, 1u);
             const size_t gi = (size_t)pg * kPageRecs + idx;
             R.lo[gi] = wl;
@@ -88,7 +91,7 @@ __global__ void __launch_bounds__(256) k_count2(const uint8_t* __restrict__ s, s
             return;
         }
         bool ins;
-        table_add(s, s, gpos, len, wl, wh, short_hash(wl, wh, len), c, kv, pos, mask, status, &ins);
+        table_add(s, s, gpos, len, wl, wh, h, c, kv, pos, mask, status, &ins);
         inserted += ins;
     };
 
@@ -99,14 +102,20 @@ __global__ void __launch_bounds__(256) k_count2(const uint8_t* __restrict__ s, s
         store2(pre, tid);
         if (tid == 0) {
             s_stop = *(volatile unsigned long long*)fill > max_fill;
+            s_old = -3;
             if (R.on && s_page != -1 && (s_page == -2 || s_used + kRecReserve > (unsigned)kPageRecs)) {
                 if (s_page >= 0) R.page_used[s_page] = s_used;
+                s_old = s_page;
                 const unsigned pg = atomicAdd(R.n_pages, 1u);
                 s_page = pg < R.max_pages ? (int)pg : -1;   // -1: the pool is spent
                 s_used = 0;
             }
         }
         __syncthreads();
+        if (s_old != -3 && tid < kCoarse) {   // the page left behind: its coarse histogram
+            if (s_old >= 0) R.page_ch[(size_t)s_old * kCoarse + tid] = s_ch[tid];
+            s_ch[tid] = 0;   // (ordered before this chunk's spills by the mask phase's barrier)
+        }
         if (s_stop) {
             if (tid == 0) atomicOr(status, 1u);
             break;
@@ -203,7 +212,7 @@ __global__ void __launch_bounds__(256) k_count2(const uint8_t* __restrict__ s, s
             }
             if (!done) {
                 ++n_miss;
-                if (mode != 4) spill(wl, wh, len, gpos, 1);
+                if (mode != 4) spill(wl, wh, len, gpos, 1, h);
             }
         }
         // epoch end: entries hit fewer than kKeep2 times since the last epoch leave the cache
@@ -217,7 +226,8 @@ __global__ void __launch_bounds__(256) k_count2(const uint8_t* __restrict__ s, s
                     c_mark[i] = (uint16_t)cc;
                     continue;
                 }
-                spill(c_lo[i], c_hi[i], (size_t)(k >> 40), (size_t)(k & kOffMask) - 1, cc);
+                spill(c_lo[i], c_hi[i], (size_t)(k >> 40), (size_t)(k & kOffMask) - 1, cc,
+                      short_hash(c_lo[i], c_hi[i], (size_t)(k >> 40)));
                 c_key[i] = 0;
                 c_cnt[i] = 0;
                 c_mark[i] = 0;
@@ -236,13 +246,15 @@ __global__ void __launch_bounds__(256) k_count2(const uint8_t* __restrict__ s, s
     for (int i = tid; i < kCache2; i += blockDim.x) {   // flush the cache
         const unsigned long long k = c_key[i];
         if (k == 0 || k == kBusy) continue;
-        spill(c_lo[i], c_hi[i], (size_t)(k >> 40), (size_t)(k & kOffMask) - 1, c_cnt[i]);
+        spill(c_lo[i], c_hi[i], (size_t)(k >> 40), (size_t)(k & kOffMask) - 1, c_cnt[i],
+              short_hash(c_lo[i], c_hi[i], (size_t)(k >> 40)));
     }
     __syncthreads();
     if (tid == 0 && R.on) {   // the next launch's workgroup continues this page
         R.wg_page[blockIdx.x] = s_page;
         R.wg_used[blockIdx.x] = s_used;
     }
+    if (tid < kCoarse && R.on) R.wg_ch[(size_t)blockIdx.x * kCoarse + tid] = s_ch[tid];
     ntok = wave_sum(ntok);
     inserted = wave_sum(inserted);
     n_miss = wave_sum(n_miss);
@@ -265,99 +277,199 @@ __global__ void k_rec_retire(RecPool R, unsigned n_wg) {
     const unsigned b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= n_wg) return;
     const int pg = R.wg_page[b];
-    if (pg >= 0) R.page_used[pg] = R.wg_used[b];
+    if (pg < 0) return;
+    R.page_used[pg] = R.wg_used[b];
+    for (int c = 0; c < kCoarse; ++c) R.page_ch[(size_t)pg * kCoarse + c] = R.wg_ch[(size_t)b * kCoarse + c];
 }
 
-// per page: bin histogram, stored bin-major (hist[bin * n_pages + page])
-__global__ void __launch_bounds__(1024) k_rec_hist(RecPool R, unsigned n_pages, unsigned* __restrict__ hist) {
-    __shared__ unsigned h[kBins];
-    const unsigned pg = blockIdx.x;
-    for (int i = threadIdx.x; i < kBins; i += blockDim.x) h[i] = 0;
-    __syncthreads();
-    const unsigned used = R.page_used[pg];
-    const size_t g0 = (size_t)pg * kPageRecs;
-    constexpr int U = 4;
-    for (unsigned i0 = threadIdx.x; i0 < used; i0 += U * blockDim.x) {
-        unsigned bin[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const unsigned i = i0 + u * blockDim.x;
-            bin[u] = i < used ? rec_bin(rec_hash(R.lo[g0 + i], R.hi[g0 + i], R.meta[g0 + i])) : ~0u;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (bin[u] != ~0u) atomicAdd(&h[bin[u]], 1u);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kBins; i += blockDim.x) hist[(size_t)i * n_pages + pg] = h[i];
-}
+// ---- two-level partition of the records by bin (the top 12 bits of the word hash)
+// Level 1 splits the pool's pages by the top 6 bits (the per-page histogram came from k_count2),
+// level 2 splits each coarse bin's run, in tiles, by the next 6.  Both move records through an
+// LDS-sorted tile of kPartTile records, so each bin's share of a tile (~64 records) leaves as
+// one contiguous run: whole lines, not the scattered 8-byte writes of a direct per-record scatter.
+constexpr int kPartTile = 4096;
+constexpr int kL2Tile = 65536;   // records per level-2 work item
 
-// per bin: exclusive scan over the pages (in place), the bin's total
-__global__ void __launch_bounds__(1024) k_rec_binscan(unsigned* __restrict__ hist, unsigned n_pages,
-                                                      unsigned long long* __restrict__ tot) {
+// per coarse bin c: exclusive scan of its per-page counts over the pages (offsets within the bin)
+__global__ void __launch_bounds__(1024) k_rec_cscan(const unsigned* __restrict__ page_ch, unsigned n_pages,
+                                                    unsigned* __restrict__ coff, unsigned long long* __restrict__ ctot) {
     typedef hipcub::BlockScan<unsigned, 1024> Scan;
     __shared__ typename Scan::TempStorage tmp;
     __shared__ unsigned carry;
-    unsigned* row = hist + (size_t)blockIdx.x * n_pages;
+    const unsigned c = blockIdx.x;
     if (threadIdx.x == 0) carry = 0;
     __syncthreads();
     for (unsigned b0 = 0; b0 < n_pages; b0 += 1024) {
         const unsigned i = b0 + threadIdx.x;
-        const unsigned v = i < n_pages ? row[i] : 0u;
+        const unsigned v = i < n_pages ? page_ch[(size_t)i * kCoarse + c] : 0u;
         unsigned ex, agg;
         Scan(tmp).ExclusiveSum(v, ex, agg);
         const unsigned cb = carry;
-        if (i < n_pages) row[i] = cb + ex;
+        if (i < n_pages) coff[(size_t)i * kCoarse + c] = cb + ex;
         __syncthreads();
         if (threadIdx.x == 0) carry = cb + agg;
         __syncthreads();
     }
-    if (threadIdx.x == 0) tot[blockIdx.x] = carry;
+    if (threadIdx.x == 0) ctot[c] = carry;
 }
 
-// bin bases (exclusive scan of the totals; base[kBins] = all records)
-__global__ void __launch_bounds__(1024) k_rec_binbase(const unsigned long long* __restrict__ tot,
-                                                      unsigned long long* __restrict__ base) {
+// exclusive scan of n <= 4096 totals (one workgroup); base[n] = their sum
+__global__ void __launch_bounds__(1024) k_rec_base(const unsigned long long* __restrict__ tot, int n,
+                                                   unsigned long long* __restrict__ base) {
     typedef hipcub::BlockScan<unsigned long long, 1024> Scan;
     __shared__ typename Scan::TempStorage tmp;
-    constexpr int per = kBins / 1024;
+    constexpr int per = 4;
     unsigned long long v[per], ex[per], agg;
 #pragma unroll
-    for (int k = 0; k < per; ++k) v[k] = tot[threadIdx.x * per + k];
+    for (int k = 0; k < per; ++k) {
+        const int i = threadIdx.x * per + k;
+        v[k] = i < n ? tot[i] : 0ULL;
+    }
     Scan(tmp).ExclusiveSum(v, ex, agg);
 #pragma unroll
-    for (int k = 0; k < per; ++k) base[threadIdx.x * per + k] = ex[k];
-    if (threadIdx.x == 0) base[kBins] = agg;
+    for (int k = 0; k < per; ++k) {
+        const int i = threadIdx.x * per + k;
+        if (i < n) base[i] = ex[k];
+    }
+    if (threadIdx.x == 0) base[n] = agg;
 }
 
-// per page: every record to its bin's run
-__global__ void __launch_bounds__(1024) k_rec_scatter(RecPool R, unsigned n_pages, const unsigned* __restrict__ hist,
-                                                      const unsigned long long* __restrict__ base,
-                                                      uint64_t* __restrict__ olo, uint64_t* __restrict__ ohi,
-                                                      uint64_t* __restrict__ ometa) {
-    __shared__ unsigned long long cur[kBins];
-    const unsigned pg = blockIdx.x;
-    for (int i = threadIdx.x; i < kBins; i += blockDim.x) cur[i] = base[i] + hist[(size_t)i * n_pages + pg];
+// records [s0, s0 + len) of (slo, shi, sme) to dest + cur[bin] (cur: LDS, advanced), bin = the 6
+// bits of the hash at `shift`, one LDS-sorted tile at a time
+__device__ __forceinline__ void part_tiles(const uint64_t* __restrict__ slo, const uint64_t* __restrict__ shi,
+                                           const uint64_t* __restrict__ sme, size_t s0, size_t len, int shift,
+                                           unsigned long long* cur, uint64_t* __restrict__ dlo,
+                                           uint64_t* __restrict__ dhi, uint64_t* __restrict__ dme) {
+    __shared__ uint64_t st_lo[kPartTile], st_hi[kPartTile], st_me[kPartTile];
+    __shared__ uint8_t st_bin[kPartTile];
+    __shared__ unsigned t_cnt[kCoarse], t_off[kCoarse], t_cur[kCoarse];
+    const int tid = threadIdx.x;
+    constexpr int U = kPartTile / 1024;
+    if (tid < kCoarse) { t_cnt[tid] = 0; t_cur[tid] = 0; }
     __syncthreads();
-    const unsigned used = R.page_used[pg];
-    const size_t g0 = (size_t)pg * kPageRecs;
-    constexpr int U = 4;   // records per thread per step: their loads are all in flight together
-    for (unsigned i0 = threadIdx.x; i0 < used; i0 += U * blockDim.x) {
+    for (size_t t0 = 0; t0 < len; t0 += kPartTile) {
+        const unsigned nt = (unsigned)(len - t0 < (size_t)kPartTile ? len - t0 : kPartTile);
         uint64_t a[U], b[U], m[U];
+        unsigned bin[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const unsigned i = i0 + u * blockDim.x;
-            if (i < used) { a[u] = R.lo[g0 + i]; b[u] = R.hi[g0 + i]; m[u] = R.meta[g0 + i]; }
+            const unsigned q = tid + u * 1024;
+            bin[u] = kCoarse;
+            if (q < nt) {
+                const size_t i = s0 + t0 + q;
+                a[u] = slo[i]; b[u] = shi[i]; m[u] = sme[i];
+                bin[u] = (unsigned)(rec_hash(a[u], b[u], m[u]) >> shift) & (kCoarse - 1);
+                atomicAdd(&t_cnt[bin[u]], 1u);
+            }
         }
+        __syncthreads();
+        if (tid < 64) {   // one wave: the tile's bin offsets
+            const unsigned v = t_cnt[tid];
+            unsigned x = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned y = __shfl_up(x, o);
+                if (tid >= o) x += y;
+            }
+            t_off[tid] = x - v;
+        }
+        __syncthreads();
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (i0 + u * blockDim.x >= used) break;
-            const unsigned long long p = atomicAdd(&cur[rec_bin(rec_hash(a[u], b[u], m[u]))], 1ULL);
-            olo[p] = a[u];
-            ohi[p] = b[u];
-            ometa[p] = m[u];
+            if (bin[u] == kCoarse) continue;
+            const unsigned q = t_off[bin[u]] + atomicAdd(&t_cur[bin[u]], 1u);
+            st_lo[q] = a[u]; st_hi[q] = b[u]; st_me[q] = m[u]; st_bin[q] = (uint8_t)bin[u];
         }
+        __syncthreads();
+        for (unsigned q = tid; q < nt; q += 1024) {   // consecutive q of one bin: one run
+            const unsigned bb = st_bin[q];
+            const unsigned long long g = cur[bb] + (q - t_off[bb]);
+            dlo[g] = st_lo[q]; dhi[g] = st_hi[q]; dme[g] = st_me[q];
+        }
+        __syncthreads();
+        if (tid < kCoarse) { cur[tid] += t_cnt[tid]; t_cnt[tid] = 0; t_cur[tid] = 0; }
+        __syncthreads();
     }
+}
+
+// level 1: one workgroup per pool page
+__global__ void __launch_bounds__(1024) k_rec_part1(RecPool R, const unsigned* __restrict__ coff,
+                                                    const unsigned long long* __restrict__ cbase,
+                                                    uint64_t* __restrict__ dlo, uint64_t* __restrict__ dhi,
+                                                    uint64_t* __restrict__ dme) {
+    __shared__ unsigned long long cur[kCoarse];
+    const unsigned pg = blockIdx.x;
+    if (threadIdx.x < kCoarse) cur[threadIdx.x] = cbase[threadIdx.x] + coff[(size_t)pg * kCoarse + threadIdx.x];
+    part_tiles(R.lo, R.hi, R.meta, (size_t)pg * kPageRecs, R.page_used[pg], 64 - kCoarseBits, cur, dlo, dhi, dme);
+}
+
+struct L2Tile {
+    unsigned long long start;
+    unsigned len, coarse;
+};
+
+// level 2, histogram: per tile of a coarse bin's run, records per fine bin
+__global__ void __launch_bounds__(1024) k_rec_fhist(const uint64_t* __restrict__ rlo, const uint64_t* __restrict__ rhi,
+                                                    const uint64_t* __restrict__ rme, const L2Tile* __restrict__ tiles,
+                                                    unsigned* __restrict__ fhist) {
+    __shared__ unsigned h[kCoarse];
+    const L2Tile T = tiles[blockIdx.x];
+    if (threadIdx.x < kCoarse) h[threadIdx.x] = 0;
+    __syncthreads();
+    constexpr int U = 4;
+    for (unsigned q0 = threadIdx.x; q0 < T.len; q0 += U * 1024) {
+        unsigned f[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const unsigned q = q0 + u * 1024;
+            f[u] = q < T.len ? (unsigned)(rec_hash(rlo[T.start + q], rhi[T.start + q], rme[T.start + q]) >>
+                                          (64 - 2 * kCoarseBits)) & (kCoarse - 1)
+                             : kCoarse;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (f[u] != kCoarse) atomicAdd(&h[f[u]], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < kCoarse) fhist[(size_t)blockIdx.x * kCoarse + threadIdx.x] = h[threadIdx.x];
+}
+
+// level 2, offsets: per (coarse c, fine f) an exclusive scan over c's tiles; totals per final bin
+__global__ void __launch_bounds__(256) k_rec_fscan(unsigned* __restrict__ fhist, const unsigned* __restrict__ tile0,
+                                                   unsigned long long* __restrict__ ftot) {
+    typedef hipcub::BlockScan<unsigned, 256> Scan;
+    __shared__ typename Scan::TempStorage tmp;
+    __shared__ unsigned carry;
+    const unsigned c = blockIdx.x / kCoarse, f = blockIdx.x % kCoarse;
+    const unsigned a = tile0[c], e = tile0[c + 1];
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (unsigned b0 = a; b0 < e; b0 += 256) {
+        const unsigned i = b0 + threadIdx.x;
+        const unsigned v = i < e ? fhist[(size_t)i * kCoarse + f] : 0u;
+        unsigned ex, agg;
+        Scan(tmp).ExclusiveSum(v, ex, agg);
+        const unsigned cb = carry;
+        if (i < e) fhist[(size_t)i * kCoarse + f] = cb + ex;
+        __syncthreads();
+        if (threadIdx.x == 0) carry = cb + agg;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) ftot[blockIdx.x] = carry;
+}
+
+// level 2, move: one workgroup per tile, into the final bins
+__global__ void __launch_bounds__(1024) k_rec_part2(const uint64_t* __restrict__ rlo, const uint64_t* __restrict__ rhi,
+                                                    const uint64_t* __restrict__ rme, const L2Tile* __restrict__ tiles,
+                                                    const unsigned* __restrict__ foff,
+                                                    const unsigned long long* __restrict__ base,
+                                                    uint64_t* __restrict__ dlo, uint64_t* __restrict__ dhi,
+                                                    uint64_t* __restrict__ dme) {
+    __shared__ unsigned long long cur[kCoarse];
+    const L2Tile T = tiles[blockIdx.x];
+    if (threadIdx.x < kCoarse)
+        cur[threadIdx.x] = base[T.coarse * kCoarse + threadIdx.x] + foff[(size_t)blockIdx.x * kCoarse + threadIdx.x];
+    part_tiles(rlo, rhi, rme, T.start, T.len, 64 - 2 * kCoarseBits, cur, dlo, dhi, dme);
 }
 
 constexpr int kRedSlots = 4096;   // LDS table of k_rec_reduce (a bin holds ~1/4096 of the words)
@@ -530,9 +642,12 @@ void RecPoolOwner::init(size_t n_bytes, unsigned grid, hipStream_t s) {
     const size_t cap = (size_t)max_pages * kPageRecs;
     rec = scratch_take(cap);
     page_used.alloc(max_pages);
+    page_ch.alloc((size_t)max_pages * kCoarse);
     n_pages.alloc(1);
     wg_page.alloc(grid);
     wg_used.alloc(grid);
+    wg_ch.alloc((size_t)grid * kCoarse);
+    BPE_HIP(hipMemsetAsync(wg_ch.p, 0, 4ull * grid * kCoarse, s));
     n_wg = grid;
     BPE_HIP(hipMemsetAsync(n_pages.p, 0, 4, s));
     BPE_HIP(hipMemsetAsync(wg_used.p, 0, 4ull * grid, s));
@@ -551,6 +666,8 @@ RecPool RecPoolOwner::dev() const {
     R.max_pages = max_pages;
     R.wg_page = wg_page.p;
     R.wg_used = wg_used.p;
+    R.page_ch = page_ch.p;
+    R.wg_ch = wg_ch.p;
     R.on = rec != nullptr;
     return R;
 }
@@ -565,24 +682,44 @@ void RecPoolOwner::reduce(const uint8_t* text, const WordCounts& wc, unsigned lo
     np = std::min(np, max_pages);
     pages_used = np;
     if (np == 0) return;
-    DevBuf<unsigned> hist((size_t)kBins * np);
-    DevBuf<unsigned long long> tot(kBins), base(kBins + 1);
-    hipLaunchKernelGGL(k_rec_hist, dim3(np), dim3(1024), 0, s, R, np, hist.p);
-    hipLaunchKernelGGL(k_rec_binscan, dim3(kBins), dim3(1024), 0, s, hist.p, np, tot.p);
-    hipLaunchKernelGGL(k_rec_binbase, dim3(1), dim3(1024), 0, s, tot.p, base.p);
-    unsigned long long total = 0;
-    BPE_HIP(hipMemcpyAsync(&total, base.p + kBins, 8, hipMemcpyDeviceToHost, s));
+    // level 1: pages -> coarse bins (B)
+    DevBuf<unsigned> coff((size_t)kCoarse * np);
+    DevBuf<unsigned long long> ctot(kCoarse), cbase(kCoarse + 1);
+    hipLaunchKernelGGL(k_rec_cscan, dim3(kCoarse), dim3(1024), 0, s, page_ch.p, np, coff.p, ctot.p);
+    hipLaunchKernelGGL(k_rec_base, dim3(1), dim3(1024), 0, s, ctot.p, kCoarse, cbase.p);
+    std::vector<unsigned long long> hb(kCoarse + 1);
+    BPE_HIP(hipMemcpyAsync(hb.data(), cbase.p, 8 * (kCoarse + 1), hipMemcpyDeviceToHost, s));
     BPE_HIP(hipStreamSynchronize(s));
+    const unsigned long long total = hb[kCoarse];
     records = total;
     if (total == 0) return;
-    std::unique_ptr<Arrays3> out = scratch_take(total);
-    hipLaunchKernelGGL(k_rec_scatter, dim3(np), dim3(1024), 0, s, R, np, hist.p, base.p, out->a.p, out->b.p,
-                       out->c.p);
-    hipLaunchKernelGGL(k_rec_reduce, dim3(kBins), dim3(1024), 0, s, out->a.p, out->b.p, out->c.p, base.p, text,
-                       wc.kv.p, wc.pos.p, wc.cap - 1, fill, status);
+    std::unique_ptr<Arrays3> B = scratch_take(total);
+    hipLaunchKernelGGL(k_rec_part1, dim3(np), dim3(1024), 0, s, R, coff.p, cbase.p, B->a.p, B->b.p, B->c.p);
+    // level 2: each coarse bin's run, in tiles -> the final bins, back into the pool's arrays (A)
+    std::vector<L2Tile> tl;
+    std::vector<unsigned> t0(kCoarse + 1, 0);
+    for (int c = 0; c < kCoarse; ++c) {
+        t0[c] = (unsigned)tl.size();
+        for (unsigned long long a = hb[c]; a < hb[c + 1]; a += kL2Tile)
+            tl.push_back(L2Tile{a, (unsigned)std::min<unsigned long long>(kL2Tile, hb[c + 1] - a), (unsigned)c});
+    }
+    t0[kCoarse] = (unsigned)tl.size();
+    const unsigned nt = (unsigned)tl.size();
+    DevBuf<L2Tile> d_tl(nt);
+    DevBuf<unsigned> d_t0(kCoarse + 1), fhist((size_t)kCoarse * nt);
+    DevBuf<unsigned long long> ftot(kBins), base(kBins + 1);
+    BPE_HIP(hipMemcpyAsync(d_tl.p, tl.data(), nt * sizeof(L2Tile), hipMemcpyHostToDevice, s));
+    BPE_HIP(hipMemcpyAsync(d_t0.p, t0.data(), 4 * (kCoarse + 1), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_rec_fhist, dim3(nt), dim3(1024), 0, s, B->a.p, B->b.p, B->c.p, d_tl.p, fhist.p);
+    hipLaunchKernelGGL(k_rec_fscan, dim3(kBins), dim3(256), 0, s, fhist.p, d_t0.p, ftot.p);
+    hipLaunchKernelGGL(k_rec_base, dim3(1), dim3(1024), 0, s, ftot.p, kBins, base.p);
+    hipLaunchKernelGGL(k_rec_part2, dim3(nt), dim3(1024), 0, s, B->a.p, B->b.p, B->c.p, d_tl.p, fhist.p, base.p,
+                       R.lo, R.hi, R.meta);
+    hipLaunchKernelGGL(k_rec_reduce, dim3(kBins), dim3(1024), 0, s, R.lo, R.hi, R.meta, base.p, text, wc.kv.p,
+                       wc.pos.p, wc.cap - 1, fill, status);
     BPE_HIP(hipGetLastError());
     BPE_HIP(hipStreamSynchronize(s));
-    scratch_give(std::move(out));
+    scratch_give(std::move(B));
 }
 
 }  // namespace bpe
