@@ -328,17 +328,17 @@ k_enc_scan2(const uint8_t* __restrict__ s, size_t n, size_t n_chunks, const Seg*
             size_t mask, unsigned long long max_fill, unsigned long long* __restrict__ fill,
             uint32_t* __restrict__ recs, unsigned long long* __restrict__ t_start,
             uint32_t* __restrict__ t_count, unsigned* __restrict__ status, int use_cache) {
-    __shared__ uint64_t s_mask[kWords], s_spec[kWords];
+    __shared__ uint64_t s_mask[kWords];
     __shared__ unsigned long long c_key[kEncCache];
     __shared__ uint64_t c_lo[kEncCache], c_hi[kEncCache];
     __shared__ uint32_t c_slot[kEncCache];
-    __shared__ uint16_t c_hit[kEncCache], c_mark[kEncCache];
+    __shared__ uint16_t c_hit[kEncCache];   // hits this epoch (3 workgroups per CU fit the LDS)
     __shared__ Seg s_seg[kSegLds];
     __shared__ int s_seg0, s_segn;   // first segment of the chunk window and how many are in LDS (-1: too many)
     __shared__ unsigned long long s_red[4];
     __shared__ int s_stop;
     const int tid = threadIdx.x;
-    for (int i = tid; i < kEncCache; i += blockDim.x) { c_key[i] = 0; c_hit[i] = 0; c_mark[i] = 0; }
+    for (int i = tid; i < kEncCache; i += blockDim.x) { c_key[i] = 0; c_hit[i] = 0; }
     load_cls2(tid, blockDim.x);
     unsigned long long inserted = 0;
 
@@ -456,7 +456,6 @@ k_enc_scan2(const uint8_t* __restrict__ s, size_t n, size_t n_chunks, const Seg*
             }
         }
         s_mask[tid] = starts;
-        s_spec[tid] = spec;
         if (c + gridDim.x < n_chunks) fetch2<kAligned>(pre, s, n, (c + gridDim.x) * kChunk, tid);
         __syncthreads();
 
@@ -506,11 +505,9 @@ k_enc_scan2(const uint8_t* __restrict__ s, size_t n, size_t n_chunks, const Seg*
             for (int i = tid; i < kEncCache; i += blockDim.x) {
                 const unsigned long long kk = c_key[i];
                 if (kk == 0 || kk == kBusy) continue;
-                const uint16_t hh = c_hit[i];
-                if ((uint16_t)(hh - c_mark[i]) >= kEncKeep) { c_mark[i] = hh; continue; }
+                if (c_hit[i] >= kEncKeep) { c_hit[i] = 0; continue; }
                 c_key[i] = 0;
                 c_hit[i] = 0;
-                c_mark[i] = 0;
             }
         }
         const unsigned long long ins = wave_sum(inserted);
@@ -526,48 +523,51 @@ k_enc_scan2(const uint8_t* __restrict__ s, size_t n, size_t n_chunks, const Seg*
 
 // ------------------------------------------------------------------ 3. unique words
 __global__ void k_collect(const unsigned long long* __restrict__ kv, const unsigned long long* __restrict__ pos,
-                          size_t cap, uint32_t* __restrict__ slot_word, unsigned long long* __restrict__ w_off,
+                          size_t cap, uint32_t* __restrict__ w_slot, unsigned long long* __restrict__ w_off,
                           uint32_t* __restrict__ w_len, unsigned* __restrict__ n_words) {
     const size_t sidx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const unsigned long long k = sidx < cap ? kv[2 * sidx] : 0ULL;
     const unsigned w = wave_append(k != 0, n_words);
     if (!k) return;
-    slot_word[sidx] = w;
+    w_slot[w] = (uint32_t)sidx;
     const bool inl = (k >> 63) != 0;   // key format: stage.h
     w_off[w] = inl ? pos[sidx] : (k & kOff40) - 1;
     w_len[w] = inl ? (uint32_t)((k >> 56) & 0x7f) : (uint32_t)(k >> 40);
 }
 
 // ------------------------------------------------------------------ 5. ids per span, then write
-__device__ __forceinline__ uint32_t rec_nids(uint32_t rec, const uint32_t* __restrict__ slot_word,
-                                             const uint32_t* __restrict__ w_nids, size_t cap, unsigned nw,
-                                             unsigned* __restrict__ status) {
-    if (rec & kSpecialRec) return 1u;
-    const uint32_t w = rec < cap ? slot_word[rec] : 0xffffffffu;
-    if (w >= nw) { atomicOr(status, 32u); return 0u; }   // a record naming no word: a bug
-    return w_nids[w];
+// slot_info[slot] (k_encode_words): the word's ids in one 8-byte cell -- kOneId | id for a word
+// of one id, nids << 39 | offset into the id pool for more, 0 for none (a pre-token equal to a
+// special) -- so a pre-token costs one dependent load from its record
+constexpr unsigned long long kOneId = 1ULL << 63;
+
+__device__ __forceinline__ uint32_t info_nids(unsigned long long info) {
+    return (info & kOneId) ? 1u : (uint32_t)((info >> 39) & 0xffffffu);
 }
 
 __global__ void k_enc_count(const uint32_t* __restrict__ recs, const unsigned long long* __restrict__ t_start,
                             const uint32_t* __restrict__ t_count, size_t n_spans,
-                            const uint32_t* __restrict__ slot_word, const uint32_t* __restrict__ w_nids,
-                            size_t cap, unsigned nw, unsigned* __restrict__ status,
-                            unsigned long long* __restrict__ per) {
+                            const unsigned long long* __restrict__ slot_info, size_t cap,
+                            unsigned* __restrict__ status, unsigned long long* __restrict__ per) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_spans) return;
     const uint32_t* r = recs + t_start[t];
     const uint32_t m = t_count[t];
     unsigned long long ids = 0;
-    for (uint32_t i = 0; i < m; ++i) ids += rec_nids(r[i], slot_word, w_nids, cap, nw, status);
+    for (uint32_t i = 0; i < m; ++i) {
+        const uint32_t rec = r[i];
+        if (rec & kSpecialRec) { ++ids; continue; }
+        if (rec >= cap) { atomicOr(status, 32u); continue; }   // a record naming no slot: a bug
+        ids += info_nids(slot_info[rec]);
+    }
     per[t] = ids;
 }
 
 __global__ void k_enc_write(const uint32_t* __restrict__ recs, const unsigned long long* __restrict__ t_start,
                             const uint32_t* __restrict__ t_count, size_t n_spans,
-                            const uint32_t* __restrict__ slot_word, const uint32_t* __restrict__ w_nids,
-                            const unsigned long long* __restrict__ w_idoff, const uint32_t* __restrict__ ids_pool,
+                            const unsigned long long* __restrict__ slot_info, const uint32_t* __restrict__ ids_pool,
                             const int64_t* __restrict__ sp_vid, const unsigned long long* __restrict__ per_off,
-                            size_t cap, unsigned nw, uint32_t* __restrict__ out) {
+                            size_t cap, uint32_t* __restrict__ out) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n_spans) return;
     const uint32_t* r = recs + t_start[t];
@@ -579,10 +579,14 @@ __global__ void k_enc_write(const uint32_t* __restrict__ recs, const unsigned lo
             out[o++] = (uint32_t)sp_vid[rec & ~kSpecialRec];
             continue;
         }
-        const uint32_t w = rec < cap ? slot_word[rec] : 0xffffffffu;
-        if (w >= nw) continue;   // reported by k_enc_count
-        const uint32_t* src = ids_pool + w_idoff[w];
-        const uint32_t nm = w_nids[w];
+        if (rec >= cap) continue;   // reported by k_enc_count
+        const unsigned long long info = slot_info[rec];
+        if (info & kOneId) {
+            out[o++] = (uint32_t)info;
+            continue;
+        }
+        const uint32_t nm = info_nids(info);
+        const uint32_t* src = ids_pool + (info & ((1ULL << 39) - 1));
         for (uint32_t j = 0; j < nm; ++j) out[o + j] = src[j];
         o += nm;
     }
@@ -603,15 +607,16 @@ __device__ __forceinline__ uint2 rank_of(const EncTables& E, uint32_t a, uint32_
 __global__ void __launch_bounds__(256)
 k_encode_words(const uint8_t* __restrict__ s, EncTables E, const unsigned long long* __restrict__ w_off,
                const uint32_t* __restrict__ w_len, const unsigned long long* __restrict__ w_idoff,
-               unsigned n_words, uint32_t* __restrict__ pool, uint32_t* __restrict__ w_nids,
-               unsigned* __restrict__ status, size_t n) {
+               const uint32_t* __restrict__ w_slot, unsigned n_words, uint32_t* __restrict__ pool,
+               unsigned long long* __restrict__ slot_info, unsigned* __restrict__ status, size_t n) {
     const unsigned w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= n_words) return;
     const uint32_t len = w_len[w];
-    if (w_off[w] + len > n) { atomicOr(status, 64u); w_nids[w] = 0; return; }   // a bug: report
+    unsigned long long* info = slot_info + w_slot[w];
+    if (w_off[w] + len > n) { atomicOr(status, 64u); *info = 0; return; }   // a bug: report
     const uint8_t* src = s + w_off[w];
     for (int k = 0; k < E.n_sp; ++k)  // match() drops pre-tokens equal to a special (73)
-        if (E.sp_len[k] == len && bytes_eq(src, E.sp_bytes + E.sp_off[k], len)) { w_nids[w] = 0; return; }
+        if (E.sp_len[k] == len && bytes_eq(src, E.sp_bytes + E.sp_off[k], len)) { *info = 0; return; }
     uint32_t* t = pool + w_idoff[w];
     for (uint32_t i = 0; i < len; ++i) t[i] = E.byte2tok[src[i]];
     uint32_t m = len;
@@ -634,7 +639,7 @@ k_encode_words(const uint8_t* __restrict__ s, EncTables E, const unsigned long l
         if (v < 0) atomicOr(status, 4u);
         t[i] = (uint32_t)v;
     }
-    w_nids[w] = m;
+    *info = m == 1 ? (kOneId | t[0]) : (((unsigned long long)m << 39) | w_idoff[w]);
 }
 
 __global__ void k_word_len64(const uint32_t* __restrict__ w_len, unsigned n, unsigned long long* __restrict__ o) {
@@ -905,13 +910,12 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
         BPE_REQUIRE(attempt < 6, BPE_E_NOMEM, "word table overflow");
         cap *= 4;
     }
-    DevBuf<uint32_t> slot_word(cap);
-    BPE_HIP(hipMemsetAsync(slot_word.p, 0xff, slot_word.bytes(), s));
+    DevBuf<uint32_t> w_slot(cap);
     DevBuf<unsigned long long> w_off(cap);
     DevBuf<uint32_t> w_len(cap);
     DevBuf<unsigned> d_nw(1);
     BPE_HIP(hipMemsetAsync(d_nw.p, 0, 4, s));
-    hipLaunchKernelGGL(k_collect, dim3(ceil_div(cap, 256)), dim3(256), 0, s, kv.p, pos.p, cap, slot_word.p,
+    hipLaunchKernelGGL(k_collect, dim3(ceil_div(cap, 256)), dim3(256), 0, s, kv.p, pos.p, cap, w_slot.p,
                        w_off.p, w_len.p, d_nw.p);
     unsigned nw = 0;
     BPE_HIP(hipMemcpyAsync(&nw, d_nw.p, 4, hipMemcpyDeviceToHost, s));
@@ -919,7 +923,8 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
 
     // 3. encode each unique word once
     DevBuf<unsigned long long> len64(std::max(nw, 1u)), idoff(std::max(nw, 1u) + 1);
-    DevBuf<uint32_t> nids(std::max(nw, 1u));
+    DevBuf<unsigned long long> slot_info(cap);   // every slot a record names is a word's slot
+    BPE_HIP(hipMemsetAsync(slot_info.p, 0, slot_info.bytes(), s));
     unsigned long long pool_n = 0;
     if (nw) {
         hipLaunchKernelGGL(k_word_len64, dim3(ceil_div(nw, 256)), dim3(256), 0, s, w_len.p, nw, len64.p);
@@ -937,13 +942,13 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
     BPE_HIP(hipMemsetAsync(status.p, 0, 4, s));
     if (nw) {
         hipLaunchKernelGGL(k_encode_words, dim3(ceil_div(nw, 256)), dim3(256), 0, s, d_text, E, w_off.p,
-                           w_len.p, idoff.p, nw, pool.p, nids.p, status.p, n);
+                           w_len.p, idoff.p, w_slot.p, nw, pool.p, slot_info.p, status.p, n);
         BPE_HIP(hipGetLastError());
     }
     // 4. ids per span, offsets, then write: two streams over the records
     DevBuf<unsigned long long> per(n_spans), per_off(n_spans);
     hipLaunchKernelGGL(k_enc_count, dim3(ceil_div(n_spans, 256)), dim3(256), 0, s, recs, t_start.p,
-                       t_count.p, n_spans, slot_word.p, nids.p, cap, nw, status.p, per.p);
+                       t_count.p, n_spans, slot_info.p, cap, status.p, per.p);
     size_t tb = 0;
     BPE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, per.p, per_off.p, (int64_t)n_spans, s));
     DevBuf<uint8_t> tmp(tb);
@@ -960,8 +965,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
     const size_t total = last[0] + last[1];
     BPE_REQUIRE(total <= n, BPE_E_HIP, "encode produced more ids than input bytes");
     hipLaunchKernelGGL(k_enc_write, dim3(ceil_div(n_spans, 256)), dim3(256), 0, s, recs, t_start.p,
-                       t_count.p, n_spans, slot_word.p, nids.p, idoff.p, pool.p, E.sp_vid, per_off.p, cap, nw,
-                       d_out);
+                       t_count.p, n_spans, slot_info.p, pool.p, E.sp_vid, per_off.p, cap, d_out);
     BPE_HIP(hipGetLastError());
     BPE_HIP(hipStreamSynchronize(s));
     return total;
