@@ -563,33 +563,71 @@ __global__ void k_enc_count(const uint32_t* __restrict__ recs, const unsigned lo
     per[t] = ids;
 }
 
-__global__ void k_enc_write(const uint32_t* __restrict__ recs, const unsigned long long* __restrict__ t_start,
-                            const uint32_t* __restrict__ t_count, size_t n_spans,
-                            const unsigned long long* __restrict__ slot_info, const uint32_t* __restrict__ ids_pool,
-                            const int64_t* __restrict__ sp_vid, const unsigned long long* __restrict__ per_off,
-                            size_t cap, uint32_t* __restrict__ out) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_spans) return;
-    const uint32_t* r = recs + t_start[t];
-    const uint32_t m = t_count[t];
-    unsigned long long o = per_off[t];
+// One workgroup per chunk: its 256 spans' ids form one contiguous output range, so they are
+// assembled in LDS and stored with coalesced 16-byte writes (a lane writing its own span straight
+// to memory leaves partial lines behind).  A chunk whose ids do not fit writes directly.
+constexpr unsigned kWriteLds = 12288;   // ids staged per chunk (48 KB; a chunk averages ~5 K)
+
+// a span's ids, in order, through put(position, id)
+template <class Put>
+__device__ __forceinline__ void emit_span(const uint32_t* __restrict__ r, uint32_t m,
+                                          const unsigned long long* __restrict__ slot_info,
+                                          const uint32_t* __restrict__ ids_pool, const int64_t* __restrict__ sp_vid,
+                                          size_t cap, unsigned long long o, const Put& put) {
     for (uint32_t i = 0; i < m; ++i) {
         const uint32_t rec = r[i];
         if (rec & kSpecialRec) {
-            out[o++] = (uint32_t)sp_vid[rec & ~kSpecialRec];
+            put(o++, (uint32_t)sp_vid[rec & ~kSpecialRec]);
             continue;
         }
         if (rec >= cap) continue;   // reported by k_enc_count
         const unsigned long long info = slot_info[rec];
         if (info & kOneId) {
-            out[o++] = (uint32_t)info;
+            put(o++, (uint32_t)info);
             continue;
         }
         const uint32_t nm = info_nids(info);
         const uint32_t* src = ids_pool + (info & ((1ULL << 39) - 1));
-        for (uint32_t j = 0; j < nm; ++j) out[o + j] = src[j];
+        for (uint32_t j = 0; j < nm; ++j) put(o + j, src[j]);
         o += nm;
     }
+}
+
+__global__ void __launch_bounds__(256) k_enc_write(const uint32_t* __restrict__ recs,
+                                                   const unsigned long long* __restrict__ t_start,
+                                                   const uint32_t* __restrict__ t_count, size_t n_spans,
+                                                   const unsigned long long* __restrict__ slot_info,
+                                                   const uint32_t* __restrict__ ids_pool,
+                                                   const int64_t* __restrict__ sp_vid,
+                                                   const unsigned long long* __restrict__ per,
+                                                   const unsigned long long* __restrict__ per_off, size_t cap,
+                                                   uint32_t* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t buf[kWriteLds];
+    const size_t t0 = (size_t)blockIdx.x * 256, t = t0 + threadIdx.x;
+    const size_t tl = t0 + 255 < n_spans ? t0 + 255 : n_spans - 1;   // the chunk's last span
+    const unsigned long long o0 = per_off[t0], o1 = per_off[tl] + per[tl];
+    const unsigned long long total = o1 - o0;
+    if (total > kWriteLds) {   // too many ids for LDS: straight to memory
+        if (t < n_spans)
+            emit_span(recs + t_start[t], t_count[t], slot_info, ids_pool, sp_vid, cap, per_off[t],
+                      [&](unsigned long long q, uint32_t v) { out[q] = v; });
+        return;
+    }
+    if (t < n_spans)
+        emit_span(recs + t_start[t], t_count[t], slot_info, ids_pool, sp_vid, cap, per_off[t] - o0,
+                  [&](unsigned long long q, uint32_t v) { buf[q] = v; });
+    __syncthreads();
+    // out + o0 is 4-byte aligned: a scalar head up to 16-byte alignment, then uint4 stores
+    const unsigned head = (unsigned)(((16 - ((uintptr_t)(out + o0) & 15)) & 15) / 4);
+    const unsigned h = head < total ? head : (unsigned)total;
+    if (threadIdx.x < h) out[o0 + threadIdx.x] = buf[threadIdx.x];
+    const unsigned body = (unsigned)(total - h) / 4;
+    uint4* dst = reinterpret_cast<uint4*>(out + o0 + h);
+    for (unsigned i = threadIdx.x; i < body; i += 256) {
+        const unsigned q = h + 4 * i;
+        dst[i] = make_uint4(buf[q], buf[q + 1], buf[q + 2], buf[q + 3]);
+    }
+    for (unsigned q = h + 4 * body + threadIdx.x; q < total; q += 256) out[o0 + q] = buf[q];
 }
 
 __device__ __forceinline__ uint2 rank_of(const EncTables& E, uint32_t a, uint32_t b) {
@@ -965,7 +1003,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
     const size_t total = last[0] + last[1];
     BPE_REQUIRE(total <= n, BPE_E_HIP, "encode produced more ids than input bytes");
     hipLaunchKernelGGL(k_enc_write, dim3(ceil_div(n_spans, 256)), dim3(256), 0, s, recs, t_start.p,
-                       t_count.p, n_spans, slot_info.p, pool.p, E.sp_vid, per_off.p, cap, d_out);
+                       t_count.p, n_spans, slot_info.p, pool.p, E.sp_vid, per.p, per_off.p, cap, d_out);
     BPE_HIP(hipGetLastError());
     BPE_HIP(hipStreamSynchronize(s));
     return total;
