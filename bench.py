@@ -222,7 +222,9 @@ def main():
             "value": round(n / (el / args.steps) / 1e6, 2), "unit": "MB/s",
             "ms_per_step": round(el / args.steps * 1e3, 2),
             "phases_ms": {k: round(s0[k], 2) for k in ("t_prepare_ms", "t_count_ms", "t_exchange_ms",
-                                                        "t_words_ms", "t_merge_ms", "t_total_ms")}}
+                                                        "t_words_ms", "t_merge_ms", "t_total_ms")},
+            "count_aggregation": {"records": s0["n_count_records"], "batches": s0["n_count_batches"],
+                                  "ms": round(s0["count_reduce_ms"], 2)}}
 
     ms_per_step = elapsed / args.steps * 1e3
     value = n / (elapsed / args.steps) / 1e6
@@ -321,7 +323,8 @@ def main():
                                                         "t_total_ms")},
             "counters": {k: s0[k] for k in ("n_pretokens", "n_words", "n_exchanged_words",
                                             "n_pairs_final", "n_rebuilds", "n_rounds_device",
-                                            "n_rounds_host", "n_index_builds", "n_trips")},
+                                            "n_rounds_host", "n_index_builds", "n_trips",
+                                            "n_count_records", "n_count_batches")},
         }
         print(json.dumps(line), flush=True)
         if not args.keep_corpus and need_file:

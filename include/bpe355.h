@@ -149,6 +149,8 @@ typedef struct {
     int64_t n_gpus;           /* devices (ranks) that took part */
     double count_reduce_ms;   /* device time aggregating the counter's spilled records */
     int64_t n_count_records;  /* pre-tokens (or cache entries) spilled as records by the counter */
+    double count_partial_ms;  /* device time of the aggregations done while the file was loading */
+    int64_t n_count_batches;  /* aggregation batches (1 + those done during the load) */
 } bpe_train_stats;
 int bpe_result_stats(const bpe_result* r, bpe_train_stats* out);
 void bpe_result_free(bpe_result* r);

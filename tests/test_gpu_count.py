@@ -89,6 +89,24 @@ def test_file_segments_records(knob, tmp_path):
     assert got == oracle.train_raw(data, 4000, EOT)
 
 
+@pytest.mark.parametrize("every", [1, 3])
+def test_file_partial_aggregation(knob, tmp_path, every):
+    # few workgroups fill and leave pages while later segments arrive: those pages are
+    # aggregated between segment launches (BPE355_AGG_SEGS), the held ones only at the end
+    knob("BPE355_REC_POOL", "1e8")
+    knob("BPE355_SEG_MB", 2)
+    knob("BPE355_STREAM_WG", 4)
+    knob("BPE355_AGG_SEGS", every)
+    data = _synth(36, 0, 30 << 20)
+    p = tmp_path / "c.txt"
+    p.write_bytes(data)
+    got = bpe_amd.train_bpe(p, 3000, EOT)
+    st = last_train_stats()
+    assert st["n_count_records"] > 0
+    assert st["n_count_batches"] > 2
+    assert got == oracle.train_raw(data, 3000, EOT)
+
+
 @pytest.mark.parametrize("shift", [1, 3, 7])
 def test_unaligned_device_text(shift):
     import torch

@@ -42,6 +42,7 @@ class TrainStats(ctypes.Structure):
         ("t_exchange_ms", ctypes.c_double), ("n_exchanged_words", ctypes.c_int64),
         ("t_load_ms", ctypes.c_double), ("n_gpus", ctypes.c_int64),
         ("count_reduce_ms", ctypes.c_double), ("n_count_records", ctypes.c_int64),
+        ("count_partial_ms", ctypes.c_double), ("n_count_batches", ctypes.c_int64),
     ]
 
     def as_dict(self):

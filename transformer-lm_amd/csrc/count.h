@@ -43,18 +43,32 @@ struct Arrays3 {
 std::unique_ptr<Arrays3> scratch_take(size_t cap);   // exclusive until given back
 void scratch_give(std::unique_ptr<Arrays3> x);
 
+// a level-2 work item of the record aggregation: a tile of one coarse bin's run
+struct L2Tile {
+    unsigned long long start;
+    unsigned len, coarse;
+};
+
 struct RecPoolOwner {
     std::unique_ptr<Arrays3> rec;    // the pool: lo, hi, meta
     DevBuf<unsigned> page_used, n_pages, wg_used, page_ch, wg_ch;
+    DevBuf<unsigned> held, done, list, list_n;   // page selection of the incremental aggregation
+    std::unique_ptr<Arrays3> B;                   // level-1 destination
+    DevBuf<unsigned> coff, d_t0, fhist, n_tiles;
+    DevBuf<unsigned long long> ctot, cbase, ftot, fbase, d_records;
+    DevBuf<L2Tile> d_tl;
+    unsigned max_tiles = 0;
     DevBuf<int> wg_page;
     unsigned max_pages = 0, n_wg = 0, pages_used = 0;
     unsigned long long records = 0;
+    unsigned batches = 0;
     void init(size_t n_bytes, unsigned grid, hipStream_t s);
     ~RecPoolOwner();
     RecPool dev() const;
-    // aggregate every record into the word table (one global add per distinct word per bin)
-    void reduce(const uint8_t* text, const WordCounts& wc, unsigned long long* fill, unsigned* status,
-                hipStream_t s);
+    // aggregate the complete pages not aggregated yet into the word table (one global add per
+    // distinct word per bin); final: every page (the workgroups have finished appending)
+    void aggregate(bool final, const uint8_t* text, const WordCounts& wc, unsigned long long* fill, unsigned* status,
+                   hipStream_t s);
 };
 
 unsigned count2_grid(size_t n_chunks);

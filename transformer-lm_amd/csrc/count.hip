@@ -282,6 +282,29 @@ __global__ void k_rec_retire(RecPool R, unsigned n_wg) {
     for (int c = 0; c < kCoarse; ++c) R.page_ch[(size_t)pg * kCoarse + c] = R.wg_ch[(size_t)b * kCoarse + c];
 }
 
+// pages a counting workgroup still appends to (not complete yet)
+__global__ void k_rec_hold(RecPool R, unsigned n_wg, unsigned* __restrict__ held) {
+    const unsigned b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= n_wg) return;
+    const int pg = R.wg_page[b];
+    if (pg >= 0) held[pg] = 1u;
+}
+
+// complete pages not aggregated yet -> list (and marked done); held flags cleared behind
+__global__ void k_rec_pick(RecPool R, unsigned* __restrict__ held, unsigned* __restrict__ done,
+                           unsigned* __restrict__ list, unsigned* __restrict__ list_n) {
+    const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned np = *R.n_pages < R.max_pages ? *R.n_pages : R.max_pages;
+    bool take = false;
+    if (p < np) {
+        take = !held[p] && !done[p];
+        held[p] = 0u;
+        if (take) done[p] = 1u;
+    }
+    const unsigned i = wave_append(take, list_n);
+    if (take) list[i] = p;
+}
+
 // ---- two-level partition of the records by bin (the top 12 bits of the word hash)
 // Level 1 splits the pool's pages by the top 6 bits (the per-page histogram came from k_count2),
 // level 2 splits each coarse bin's run, in tiles, by the next 6.  Both move records through an
@@ -291,17 +314,20 @@ constexpr int kPartTile = 4096;
 constexpr int kL2Tile = 65536;   // records per level-2 work item
 
 // per coarse bin c: exclusive scan of its per-page counts over the pages (offsets within the bin)
-__global__ void __launch_bounds__(1024) k_rec_cscan(const unsigned* __restrict__ page_ch, unsigned n_pages,
+__global__ void __launch_bounds__(1024) k_rec_cscan(const unsigned* __restrict__ page_ch,
+                                                    const unsigned* __restrict__ list,
+                                                    const unsigned* __restrict__ list_n,
                                                     unsigned* __restrict__ coff, unsigned long long* __restrict__ ctot) {
     typedef hipcub::BlockScan<unsigned, 1024> Scan;
     __shared__ typename Scan::TempStorage tmp;
     __shared__ unsigned carry;
     const unsigned c = blockIdx.x;
+    const unsigned n_pages = *list_n;
     if (threadIdx.x == 0) carry = 0;
     __syncthreads();
     for (unsigned b0 = 0; b0 < n_pages; b0 += 1024) {
         const unsigned i = b0 + threadIdx.x;
-        const unsigned v = i < n_pages ? page_ch[(size_t)i * kCoarse + c] : 0u;
+        const unsigned v = i < n_pages ? page_ch[(size_t)list[i] * kCoarse + c] : 0u;
         unsigned ex, agg;
         Scan(tmp).ExclusiveSum(v, ex, agg);
         const unsigned cb = carry;
@@ -334,12 +360,53 @@ __global__ void __launch_bounds__(1024) k_rec_base(const unsigned long long* __r
     if (threadIdx.x == 0) base[n] = agg;
 }
 
+// position g of a run laid over pool pages (dpage: the pages in order), or of a flat array
+__device__ __forceinline__ size_t paged(unsigned long long g, const unsigned* __restrict__ dpage) {
+    static_assert(kPageRecs == 1 << 16, "page-indirect positions");
+    return dpage ? (size_t)dpage[g >> 16] * kPageRecs + (size_t)(g & (kPageRecs - 1)) : (size_t)g;
+}
+
+// one wave: the batch's coarse-bin bases (cbase[kCoarse] = its records), the level-2 tiles over
+// each bin's run (tile0[c]: bin c's first tile; n_tiles) -- built on the device, so a batch needs
+// no host round trip
+__global__ void __launch_bounds__(64) k_rec_tiles(const unsigned long long* __restrict__ ctot,
+                                                  unsigned long long* __restrict__ cbase, L2Tile* __restrict__ tiles,
+                                                  unsigned* __restrict__ tile0, unsigned* __restrict__ n_tiles,
+                                                  unsigned long long* __restrict__ records) {
+    const unsigned c = threadIdx.x;
+    const unsigned long long cnt = ctot[c];
+    const unsigned nt = (unsigned)((cnt + kL2Tile - 1) / kL2Tile);
+    unsigned long long x = cnt;
+    unsigned y = nt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long xu = __shfl_up(x, o);
+        const unsigned yu = __shfl_up(y, o);
+        if (c >= (unsigned)o) { x += xu; y += yu; }
+    }
+    const unsigned long long b = x - cnt;
+    const unsigned t = y - nt;
+    cbase[c] = b;
+    tile0[c] = t;
+    if (c == 63) {
+        cbase[kCoarse] = x;
+        tile0[kCoarse] = y;
+        *n_tiles = y;
+        *records += x;
+    }
+    for (unsigned j = 0; j < nt; ++j) {
+        const unsigned long long a = (unsigned long long)j * kL2Tile;
+        tiles[t + j] = L2Tile{b + a, (unsigned)(cnt - a < (unsigned long long)kL2Tile ? cnt - a : kL2Tile), c};
+    }
+}
+
 // records [s0, s0 + len) of (slo, shi, sme) to dest + cur[bin] (cur: LDS, advanced), bin = the 6
 // bits of the hash at `shift`, one LDS-sorted tile at a time
 __device__ __forceinline__ void part_tiles(const uint64_t* __restrict__ slo, const uint64_t* __restrict__ shi,
                                            const uint64_t* __restrict__ sme, size_t s0, size_t len, int shift,
                                            unsigned long long* cur, uint64_t* __restrict__ dlo,
-                                           uint64_t* __restrict__ dhi, uint64_t* __restrict__ dme) {
+                                           uint64_t* __restrict__ dhi, uint64_t* __restrict__ dme,
+                                           const unsigned* __restrict__ dpage = nullptr) {
     __shared__ uint64_t st_lo[kPartTile], st_hi[kPartTile], st_me[kPartTile];
     __shared__ uint8_t st_bin[kPartTile];
     __shared__ unsigned t_cnt[kCoarse], t_off[kCoarse], t_cur[kCoarse];
@@ -383,7 +450,7 @@ __device__ __forceinline__ void part_tiles(const uint64_t* __restrict__ slo, con
         __syncthreads();
         for (unsigned q = tid; q < nt; q += 1024) {   // consecutive q of one bin: one run
             const unsigned bb = st_bin[q];
-            const unsigned long long g = cur[bb] + (q - t_off[bb]);
+            const size_t g = paged(cur[bb] + (q - t_off[bb]), dpage);
             dlo[g] = st_lo[q]; dhi[g] = st_hi[q]; dme[g] = st_me[q];
         }
         __syncthreads();
@@ -392,27 +459,26 @@ __device__ __forceinline__ void part_tiles(const uint64_t* __restrict__ slo, con
     }
 }
 
-// level 1: one workgroup per pool page
-__global__ void __launch_bounds__(1024) k_rec_part1(RecPool R, const unsigned* __restrict__ coff,
+// level 1: one workgroup per listed pool page
+__global__ void __launch_bounds__(1024) k_rec_part1(RecPool R, const unsigned* __restrict__ list,
+                                                    const unsigned* __restrict__ list_n,
+                                                    const unsigned* __restrict__ coff,
                                                     const unsigned long long* __restrict__ cbase,
                                                     uint64_t* __restrict__ dlo, uint64_t* __restrict__ dhi,
                                                     uint64_t* __restrict__ dme) {
     __shared__ unsigned long long cur[kCoarse];
-    const unsigned pg = blockIdx.x;
-    if (threadIdx.x < kCoarse) cur[threadIdx.x] = cbase[threadIdx.x] + coff[(size_t)pg * kCoarse + threadIdx.x];
+    if (blockIdx.x >= *list_n) return;   // (the grid is sized for every page)
+    const unsigned pg = list[blockIdx.x];
+    if (threadIdx.x < kCoarse) cur[threadIdx.x] = cbase[threadIdx.x] + coff[(size_t)blockIdx.x * kCoarse + threadIdx.x];
     part_tiles(R.lo, R.hi, R.meta, (size_t)pg * kPageRecs, R.page_used[pg], 64 - kCoarseBits, cur, dlo, dhi, dme);
 }
-
-struct L2Tile {
-    unsigned long long start;
-    unsigned len, coarse;
-};
 
 // level 2, histogram: per tile of a coarse bin's run, records per fine bin
 __global__ void __launch_bounds__(1024) k_rec_fhist(const uint64_t* __restrict__ rlo, const uint64_t* __restrict__ rhi,
                                                     const uint64_t* __restrict__ rme, const L2Tile* __restrict__ tiles,
-                                                    unsigned* __restrict__ fhist) {
+                                                    const unsigned* __restrict__ n_tiles, unsigned* __restrict__ fhist) {
     __shared__ unsigned h[kCoarse];
+    if (blockIdx.x >= *n_tiles) return;   // (the grid is sized for the largest batch)
     const L2Tile T = tiles[blockIdx.x];
     if (threadIdx.x < kCoarse) h[threadIdx.x] = 0;
     __syncthreads();
@@ -461,15 +527,17 @@ __global__ void __launch_bounds__(256) k_rec_fscan(unsigned* __restrict__ fhist,
 // level 2, move: one workgroup per tile, into the final bins
 __global__ void __launch_bounds__(1024) k_rec_part2(const uint64_t* __restrict__ rlo, const uint64_t* __restrict__ rhi,
                                                     const uint64_t* __restrict__ rme, const L2Tile* __restrict__ tiles,
+                                                    const unsigned* __restrict__ n_tiles,
                                                     const unsigned* __restrict__ foff,
                                                     const unsigned long long* __restrict__ base,
                                                     uint64_t* __restrict__ dlo, uint64_t* __restrict__ dhi,
-                                                    uint64_t* __restrict__ dme) {
+                                                    uint64_t* __restrict__ dme, const unsigned* __restrict__ dpage) {
     __shared__ unsigned long long cur[kCoarse];
+    if (blockIdx.x >= *n_tiles) return;
     const L2Tile T = tiles[blockIdx.x];
     if (threadIdx.x < kCoarse)
         cur[threadIdx.x] = base[T.coarse * kCoarse + threadIdx.x] + foff[(size_t)blockIdx.x * kCoarse + threadIdx.x];
-    part_tiles(rlo, rhi, rme, T.start, T.len, 64 - 2 * kCoarseBits, cur, dlo, dhi, dme);
+    part_tiles(rlo, rhi, rme, T.start, T.len, 64 - 2 * kCoarseBits, cur, dlo, dhi, dme, dpage);
 }
 
 constexpr int kRedSlots = 4096;   // LDS table of k_rec_reduce (a bin holds ~1/4096 of the words)
@@ -479,6 +547,7 @@ constexpr int kRedProbe = 64;
 __global__ void __launch_bounds__(1024) k_rec_reduce(const uint64_t* __restrict__ rlo, const uint64_t* __restrict__ rhi,
                                                      const uint64_t* __restrict__ rmeta,
                                                      const unsigned long long* __restrict__ base,
+                                                     const unsigned* __restrict__ dpage,
                                                      const uint8_t* __restrict__ s, unsigned long long* __restrict__ kv,
                                                      unsigned long long* __restrict__ pos, size_t mask,
                                                      unsigned long long* __restrict__ fill, unsigned* __restrict__ status) {
@@ -495,7 +564,10 @@ __global__ void __launch_bounds__(1024) k_rec_reduce(const uint64_t* __restrict_
 #pragma unroll
       for (int u = 0; u < U; ++u) {
           const unsigned long long i = i0 + (unsigned long long)u * blockDim.x;
-          if (i < b1) { ul[u] = rlo[i]; uh[u] = rhi[i]; um[u] = rmeta[i]; }
+          if (i < b1) {
+              const size_t g = paged(i, dpage);
+              ul[u] = rlo[g]; uh[u] = rhi[g]; um[u] = rmeta[g];
+          }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -631,7 +703,10 @@ void scratch_give(std::unique_ptr<Arrays3> x) {
     scratch().free_.push_back(std::move(x));
 }
 
-RecPoolOwner::~RecPoolOwner() { scratch_give(std::move(rec)); }
+RecPoolOwner::~RecPoolOwner() {
+    scratch_give(std::move(rec));
+    scratch_give(std::move(B));
+}
 
 void RecPoolOwner::init(size_t n_bytes, unsigned grid, hipStream_t s) {
     // pool: ~1 record per 10 corpus bytes (the bench corpus spills one per 15); when it runs out,
@@ -648,6 +723,27 @@ void RecPoolOwner::init(size_t n_bytes, unsigned grid, hipStream_t s) {
     wg_used.alloc(grid);
     wg_ch.alloc((size_t)grid * kCoarse);
     BPE_HIP(hipMemsetAsync(wg_ch.p, 0, 4ull * grid * kCoarse, s));
+    held.alloc(max_pages);
+    done.alloc(max_pages);
+    // the aggregation's buffers, sized for one batch of every page (no allocation while the
+    // file path aggregates between segment copies): level 1 lands in B, level 2 back in the pages
+    B = scratch_take(cap);
+    max_tiles = max_pages + kCoarse;
+    coff.alloc((size_t)kCoarse * max_pages);
+    ctot.alloc(kCoarse);
+    cbase.alloc(kCoarse + 1);
+    d_tl.alloc(max_tiles);
+    d_t0.alloc(kCoarse + 1);
+    fhist.alloc((size_t)kCoarse * max_tiles);
+    ftot.alloc(kBins);
+    fbase.alloc(kBins + 1);
+    n_tiles.alloc(1);
+    d_records.alloc(1);
+    BPE_HIP(hipMemsetAsync(d_records.p, 0, 8, s));
+    list.alloc(max_pages);
+    list_n.alloc(1);
+    BPE_HIP(hipMemsetAsync(held.p, 0, 4ull * max_pages, s));
+    BPE_HIP(hipMemsetAsync(done.p, 0, 4ull * max_pages, s));
     n_wg = grid;
     BPE_HIP(hipMemsetAsync(n_pages.p, 0, 4, s));
     BPE_HIP(hipMemsetAsync(wg_used.p, 0, 4ull * grid, s));
@@ -672,54 +768,47 @@ RecPool RecPoolOwner::dev() const {
     return R;
 }
 
-void RecPoolOwner::reduce(const uint8_t* text, const WordCounts& wc, unsigned long long* fill, unsigned* status,
-                          hipStream_t s) {
+void RecPoolOwner::aggregate(bool final, const uint8_t* text, const WordCounts& wc, unsigned long long* fill,
+                             unsigned* status, hipStream_t s) {
     const RecPool R = dev();
-    hipLaunchKernelGGL(k_rec_retire, dim3(ceil_div(n_wg, 256)), dim3(256), 0, s, R, n_wg);
-    unsigned np = 0;
-    BPE_HIP(hipMemcpyAsync(&np, n_pages.p, 4, hipMemcpyDeviceToHost, s));
-    BPE_HIP(hipStreamSynchronize(s));
-    np = std::min(np, max_pages);
-    pages_used = np;
-    if (np == 0) return;
-    // level 1: pages -> coarse bins (B)
-    DevBuf<unsigned> coff((size_t)kCoarse * np);
-    DevBuf<unsigned long long> ctot(kCoarse), cbase(kCoarse + 1);
-    hipLaunchKernelGGL(k_rec_cscan, dim3(kCoarse), dim3(1024), 0, s, page_ch.p, np, coff.p, ctot.p);
-    hipLaunchKernelGGL(k_rec_base, dim3(1), dim3(1024), 0, s, ctot.p, kCoarse, cbase.p);
-    std::vector<unsigned long long> hb(kCoarse + 1);
-    BPE_HIP(hipMemcpyAsync(hb.data(), cbase.p, 8 * (kCoarse + 1), hipMemcpyDeviceToHost, s));
-    BPE_HIP(hipStreamSynchronize(s));
-    const unsigned long long total = hb[kCoarse];
-    records = total;
-    if (total == 0) return;
-    std::unique_ptr<Arrays3> B = scratch_take(total);
-    hipLaunchKernelGGL(k_rec_part1, dim3(np), dim3(1024), 0, s, R, coff.p, cbase.p, B->a.p, B->b.p, B->c.p);
-    // level 2: each coarse bin's run, in tiles -> the final bins, back into the pool's arrays (A)
-    std::vector<L2Tile> tl;
-    std::vector<unsigned> t0(kCoarse + 1, 0);
-    for (int c = 0; c < kCoarse; ++c) {
-        t0[c] = (unsigned)tl.size();
-        for (unsigned long long a = hb[c]; a < hb[c + 1]; a += kL2Tile)
-            tl.push_back(L2Tile{a, (unsigned)std::min<unsigned long long>(kL2Tile, hb[c + 1] - a), (unsigned)c});
+    if (final) {   // the pages the workgroups hold are complete now
+        hipLaunchKernelGGL(k_rec_retire, dim3(ceil_div(n_wg, 256)), dim3(256), 0, s, R, n_wg);
+    } else {
+        hipLaunchKernelGGL(k_rec_hold, dim3(ceil_div(n_wg, 256)), dim3(256), 0, s, R, n_wg, held.p);
     }
-    t0[kCoarse] = (unsigned)tl.size();
-    const unsigned nt = (unsigned)tl.size();
-    DevBuf<L2Tile> d_tl(nt);
-    DevBuf<unsigned> d_t0(kCoarse + 1), fhist((size_t)kCoarse * nt);
-    DevBuf<unsigned long long> ftot(kBins), base(kBins + 1);
-    BPE_HIP(hipMemcpyAsync(d_tl.p, tl.data(), nt * sizeof(L2Tile), hipMemcpyHostToDevice, s));
-    BPE_HIP(hipMemcpyAsync(d_t0.p, t0.data(), 4 * (kCoarse + 1), hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_rec_fhist, dim3(nt), dim3(1024), 0, s, B->a.p, B->b.p, B->c.p, d_tl.p, fhist.p);
+    BPE_HIP(hipMemsetAsync(list_n.p, 0, 4, s));
+    hipLaunchKernelGGL(k_rec_pick, dim3(ceil_div(max_pages, 256)), dim3(256), 0, s, R, held.p, done.p, list.p,
+                       list_n.p);
+    // Every size below stays on the device (the grids are sized for a batch of every page and the
+    // surplus workgroups leave at once): the file path enqueues a batch between segment launches
+    // without waiting for it, its host-to-device copies continuing underneath.
+    ++batches;
+    // level 1: the listed pages -> coarse bins (B)
+    hipLaunchKernelGGL(k_rec_cscan, dim3(kCoarse), dim3(1024), 0, s, page_ch.p, list.p, list_n.p, coff.p, ctot.p);
+    hipLaunchKernelGGL(k_rec_tiles, dim3(1), dim3(64), 0, s, ctot.p, cbase.p, d_tl.p, d_t0.p, n_tiles.p,
+                       d_records.p);
+    hipLaunchKernelGGL(k_rec_part1, dim3(max_pages), dim3(1024), 0, s, R, list.p, list_n.p, coff.p, cbase.p, B->a.p,
+                       B->b.p, B->c.p);
+    // level 2: each coarse bin's run, in tiles -> the final bins, laid over the listed pages
+    // (their records are all in B now)
+    hipLaunchKernelGGL(k_rec_fhist, dim3(max_tiles), dim3(1024), 0, s, B->a.p, B->b.p, B->c.p, d_tl.p, n_tiles.p,
+                       fhist.p);
     hipLaunchKernelGGL(k_rec_fscan, dim3(kBins), dim3(256), 0, s, fhist.p, d_t0.p, ftot.p);
-    hipLaunchKernelGGL(k_rec_base, dim3(1), dim3(1024), 0, s, ftot.p, kBins, base.p);
-    hipLaunchKernelGGL(k_rec_part2, dim3(nt), dim3(1024), 0, s, B->a.p, B->b.p, B->c.p, d_tl.p, fhist.p, base.p,
-                       R.lo, R.hi, R.meta);
-    hipLaunchKernelGGL(k_rec_reduce, dim3(kBins), dim3(1024), 0, s, R.lo, R.hi, R.meta, base.p, text, wc.kv.p,
-                       wc.pos.p, wc.cap - 1, fill, status);
+    hipLaunchKernelGGL(k_rec_base, dim3(1), dim3(1024), 0, s, ftot.p, kBins, fbase.p);
+    hipLaunchKernelGGL(k_rec_part2, dim3(max_tiles), dim3(1024), 0, s, B->a.p, B->b.p, B->c.p, d_tl.p, n_tiles.p,
+                       fhist.p, fbase.p, R.lo, R.hi, R.meta, list.p);
+    hipLaunchKernelGGL(k_rec_reduce, dim3(kBins), dim3(1024), 0, s, R.lo, R.hi, R.meta, fbase.p, list.p, text,
+                       wc.kv.p, wc.pos.p, wc.cap - 1, fill, status);
     BPE_HIP(hipGetLastError());
-    BPE_HIP(hipStreamSynchronize(s));
-    scratch_give(std::move(B));
+    if (final) {
+        unsigned long long tot = 0;
+        unsigned allocated = 0;
+        BPE_HIP(hipMemcpyAsync(&tot, d_records.p, 8, hipMemcpyDeviceToHost, s));
+        BPE_HIP(hipMemcpyAsync(&allocated, n_pages.p, 4, hipMemcpyDeviceToHost, s));
+        BPE_HIP(hipStreamSynchronize(s));
+        records = tot;
+        pages_used = std::min(allocated, max_pages);
+    }
 }
 
 }  // namespace bpe

@@ -365,6 +365,8 @@ bool load_and_count(const Source& src, size_t off, size_t len, uint8_t* d_dst, i
     ValidatePass vp;
     CountPass cp;
     bool ok = true;
+    const char* ae = std::getenv("BPE355_AGG_SEGS");   // segments between partial aggregations (0: off)
+    const size_t agg_every = ae ? (size_t)std::max(0, std::atoi(ae)) : 4;
     try {
         vp.begin(d_dst, len, stream);
         cp.begin(d_dst, len, CountPass::initial_cap(len), stream, timing_enabled());
@@ -376,6 +378,8 @@ bool load_and_count(const Source& src, size_t off, size_t len, uint8_t* d_dst, i
             for (; waited < need; ++waited) BPE_HIP(hipStreamWaitEvent(stream, track.ev[waited], 0));
             vp.range(cut[k], cut[k + 1]);
             cp.range(cut[k], cut[k + 1]);
+            // the GPU waits on PCIe here: aggregate the record pages completed so far
+            if (agg_every > 0 && (k + 1) % agg_every == 0 && k + 2 < cut.size()) cp.partial();
         }
     } catch (...) {
         track.fail();

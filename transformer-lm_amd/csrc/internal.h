@@ -38,7 +38,9 @@ struct WordCounts {
     size_t cap = 0;
     uint64_t n_pretokens = 0;         // multi-byte pre-tokens seen
     uint64_t n_records = 0;           // cache misses spilled as records (count.hip)
-    double reduce_ms = 0;             // device time of their aggregation (when timed)
+    double reduce_ms = 0;             // device time of their aggregation after the last launch (when timed)
+    double partial_ms = 0;            // ... and of the batches aggregated between launches (file path)
+    unsigned batches = 0;             // aggregation batches
 };
 // Pre-tokenize text[0..n) with the GPT-2 pattern and count the multi-byte words.
 // (Single-byte words carry no pairs and cannot affect training.)
@@ -62,10 +64,13 @@ struct CountPass {
     bool timed = false;
     const unsigned long long* gate = nullptr;   // device flag: skip the launches unless ~0
     double kernel_ms = 0;        // summed device time of the launches (when timed)
-    std::vector<hipEvent_t> ev;
+    std::vector<hipEvent_t> ev, pev;   // count launches, partial aggregations
     static size_t initial_cap(size_t n);
     void begin(const uint8_t* d_text, size_t n, size_t cap, hipStream_t stream, bool timing);
     void range(size_t lo, size_t hi);
+    // aggregate the records of the pages completed so far (the file path calls it between
+    // segments, while the next ones arrive); finish() does the rest
+    void partial();
     bool finish();
     CountPass();
     ~CountPass();

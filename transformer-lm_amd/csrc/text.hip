@@ -527,6 +527,22 @@ void CountPass::range(size_t lo, size_t hi) {
     BPE_HIP(hipGetLastError());
 }
 
+void CountPass::partial() {
+    if (!rec) return;
+    hipEvent_t r0 = nullptr, r1 = nullptr;
+    if (timed) {
+        BPE_HIP(hipEventCreate(&r0));
+        BPE_HIP(hipEventCreate(&r1));
+        BPE_HIP(hipEventRecord(r0, s));
+    }
+    rec->aggregate(false, text, wc, fill.p, status.p, s);   // enqueued only: the host goes on
+    if (timed) {
+        BPE_HIP(hipEventRecord(r1, s));
+        pev.push_back(r0);
+        pev.push_back(r1);
+    }
+}
+
 bool CountPass::finish() {
     if (rec) {   // aggregate the spilled records into the table
         hipEvent_t r0 = nullptr, r1 = nullptr;
@@ -535,8 +551,9 @@ bool CountPass::finish() {
             BPE_HIP(hipEventCreate(&r1));
             BPE_HIP(hipEventRecord(r0, s));
         }
-        rec->reduce(text, wc, fill.p, status.p, s);
+        rec->aggregate(true, text, wc, fill.p, status.p, s);
         wc.n_records = rec->records;
+        wc.batches = rec->batches;
         if (timed) {
             BPE_HIP(hipEventRecord(r1, s));
             BPE_HIP(hipEventSynchronize(r1));
@@ -558,11 +575,19 @@ bool CountPass::finish() {
         BPE_HIP(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
         kernel_ms += ms;
     }
+    for (size_t i = 0; i + 1 < pev.size(); i += 2) {
+        float ms = 0;
+        BPE_HIP(hipEventElapsedTime(&ms, pev[i], pev[i + 1]));
+        wc.partial_ms += ms;
+    }
     if (std::getenv("BPE355_TRACE")) {
         unsigned long long d[3];
         BPE_HIP(hipMemcpy(d, ntok.p, 24, hipMemcpyDeviceToHost));
-        std::fprintf(stderr, "[bpe355] count: cap %zu pretokens %llu cache-miss %llu long %llu launches %zu records %llu\n",
-                     wc.cap, d[0], d[1], d[2], ev.size() / 2, (unsigned long long)wc.n_records);
+        std::fprintf(stderr,
+                     "[bpe355] count: cap %zu pretokens %llu cache-miss %llu long %llu launches %zu records %llu"
+                     " (batches %u, partial %.1f ms, tail %.1f ms)\n",
+                     wc.cap, d[0], d[1], d[2], ev.size() / 2, (unsigned long long)wc.n_records, wc.batches, wc.partial_ms,
+                     wc.reduce_ms);
     }
     return !(st & 1u);
 }
@@ -571,6 +596,7 @@ CountPass::CountPass() = default;
 
 CountPass::~CountPass() {
     for (auto& e : ev) (void)hipEventDestroy(e);
+    for (auto& e : pev) (void)hipEventDestroy(e);
 }
 
 size_t CountPass::initial_cap(size_t n) { return first_cap(n); }

@@ -3056,6 +3056,8 @@ void train_on_device(const uint8_t* d_raw, size_t n, int vocab_size,
     out.stats.n_pretokens = (int64_t)wc.n_pretokens;
     out.stats.n_count_records = (int64_t)wc.n_records;
     out.stats.count_reduce_ms = wc.reduce_ms;
+    out.stats.count_partial_ms = wc.partial_ms;
+    out.stats.n_count_batches = (int64_t)wc.batches;
     if (rounds <= 0) {
         out.stats.t_total_ms = ms_since(t0);
         return;
