@@ -53,6 +53,10 @@ struct DevBuf {
         n = count;
         if (count) BPE_HIP(hipMalloc(&p, count * sizeof(T)));
     }
+    // grow-only: keep the buffer when it already holds count elements (n is then the capacity)
+    void reserve(size_t count) {
+        if (count > n || !p) alloc(count);
+    }
     void release() {
         if (p) (void)hipFree(p);
         p = nullptr;

@@ -1232,6 +1232,15 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     }
 }
 
+// end of a block of trips: the state and the trips' records -> pinned host memory (plain vector
+// stores; the block's event orders them before the host reads)
+__global__ void __launch_bounds__(256) k_snapshot(const uint32_t* __restrict__ st, unsigned n_st,
+                                                  const uint32_t* __restrict__ ti, unsigned n_ti,
+                                                  uint32_t* __restrict__ h_st, uint32_t* __restrict__ h_ti) {
+    for (unsigned i = threadIdx.x; i < n_st; i += blockDim.x) h_st[i] = st[i];
+    for (unsigned i = threadIdx.x; i < n_ti; i += blockDim.x) h_ti[i] = ti[i];
+}
+
 typedef __attribute__((address_space(3))) unsigned LdsU32;   // an LDS word (explicit address space)
 
 // the slot word of class C addressed directly, every member applied in order.  claim: the word
@@ -2093,7 +2102,9 @@ class MergeLoop {
 
    private:
     static constexpr int kBatch = 64;
-    static constexpr int kTrips = 32;   // batched mode: [k_select][k_merge_batch][k_apply_batch] per block
+    static constexpr int kTrips = 32;   // batched mode: at most this many [select][merge][apply] per block
+    int trips_ = 8;                     // trips per block (BPE355_TRIPS): a halt leaves at most ~1.5
+                                        // blocks of empty trips queued behind it
     static_assert(2 * kTrips <= kBatch, "two blocks' timing events fit the event pool");
     static constexpr int kArgBlocks = 64;
     static constexpr unsigned kCScanBlocks = 64;   // k_apply_argmax workgroups scanning C
@@ -2171,6 +2182,8 @@ class MergeLoop {
     DevBuf<int> trip_info_;      // per trip of a block: first round, members, scan mode, list entries (2 slots)
     RoundState* snap_st_ = nullptr;   // pinned: the state at the end of each in-flight block
     int* snap_ti_ = nullptr;          // pinned: each block's trip_info
+    RoundState* snap_st_dev_ = nullptr;   // (their device-side addresses)
+    int* snap_ti_dev_ = nullptr;
     hipEvent_t blk_ev_[2] = {nullptr, nullptr};
     long long slot_base_[2] = {0, 0};   // trips launched before each slot's block
     void launch_block(int slot, bool timing, std::vector<hipEvent_t>& ev);
@@ -2187,6 +2200,11 @@ class MergeLoop {
     DevBuf<RebuildStats> rs_;
     // posting index
     DevBuf<uint32_t> ilist_, ibeg_, ilen_;
+    DevBuf<uint32_t> ix_cnt_, ix_pos_, ix_keys_, ix_vals_, ix_keys2_;   // its build's scratch
+    DevBuf<uint8_t> ix_tmp_;
+    HostWords<TokT> spare_;   // the word table's other buffer set (compaction writes into it)
+    DevBuf<MoveCounts> move_counts_;
+    DevBuf<unsigned> move_blk_;
     IndexDev idev_{};
     int next_index_round_ = 256;
 };
@@ -2264,8 +2282,10 @@ template <class TokT>
 void MergeLoop<TokT>::compact() {
     HostWords<TokT>& H = words_;
     const unsigned total = H.total();
-    DevBuf<MoveCounts> mc(1);
-    DevBuf<unsigned> blk((size_t)kMoveBlocks * kMoveK);
+    DevBuf<MoveCounts>& mc = move_counts_;
+    DevBuf<unsigned>& blk = move_blk_;
+    mc.reserve(1);
+    blk.reserve((size_t)kMoveBlocks * kMoveK);
     BPE_HIP(hipMemsetAsync(mc.p, 0, sizeof(MoveCounts), s_));
     const WordsDev<TokT> src = H.dev();
     if (total) {
@@ -2275,21 +2295,24 @@ void MergeLoop<TokT>::compact() {
     MoveCounts h{};
     BPE_HIP(hipMemcpyAsync(&h, mc.p, sizeof(h), hipMemcpyDeviceToHost, s_));
     BPE_HIP(hipStreamSynchronize(s_));
-    HostWords<TokT> D;
+    // the new table goes into the previous compaction's arrays (grow-only: the table shrinks as
+    // words finish, so after the first compactions nothing is allocated or freed here)
+    HostWords<TokT> D = std::move(spare_);
     for (int c = 0; c < kNumCls; ++c) {
         D.n[c] = h.n[c];
-        D.slot[c].alloc(std::max<size_t>((size_t)h.n[c] * slot_w(c), 1));
-        D.cnt[c].alloc(std::max(h.n[c], 1u));
+        D.slot[c].reserve(std::max<size_t>((size_t)h.n[c] * slot_w(c), 1));
+        D.cnt[c].reserve(std::max(h.n[c], 1u));
     }
     D.ln = h.n[kNumCls];
-    D.ltok.alloc(std::max<unsigned long long>(h.long_tokens, 1));
-    D.lbeg.alloc(std::max(D.ln, 1u));
-    D.llen.alloc(std::max(D.ln, 1u));
-    D.lcnt.alloc(std::max(D.ln, 1u));
+    D.ltok.reserve(std::max<unsigned long long>(h.long_tokens, 1));
+    D.lbeg.reserve(std::max(D.ln, 1u));
+    D.llen.reserve(std::max(D.ln, 1u));
+    D.lcnt.reserve(std::max(D.ln, 1u));
     if (total)
         hipLaunchKernelGGL(k_move<TokT>, dim3(kMoveBlocks), dim3(256), 0, s_, src, total, D.dev(), blk.p, mc.p);
     BPE_HIP(hipGetLastError());
     BPE_HIP(hipStreamSynchronize(s_));
+    spare_ = std::move(words_);
     words_ = std::move(D);
     long_tokens_ = h.long_tokens;
     n_live_ = words_.total();
@@ -2309,12 +2332,16 @@ void MergeLoop<TokT>::build_index() {
     BPE_HIP(hipMemsetAsync(ibeg_.p, 0, ibeg_.bytes(), s_));
     BPE_HIP(hipMemsetAsync(ilen_.p, 0, ilen_.bytes(), s_));
     unsigned long long E = 0;
-    DevBuf<uint32_t> cnt(std::max(n, 1u)), pos(std::max(n, 1u));
+    // scratch kept across builds (grow-only; the first build is the largest)
+    DevBuf<uint32_t>&cnt = ix_cnt_, &pos = ix_pos_, &keys = ix_keys_, &vals = ix_vals_, &keys2 = ix_keys2_;
+    DevBuf<uint8_t>& tmp = ix_tmp_;
+    cnt.reserve(std::max(n, 1u));
+    pos.reserve(std::max(n, 1u));
     if (n) {
         hipLaunchKernelGGL(k_index_count<TokT>, dim3(ceil_div(n, 256)), dim3(256), 0, s_, wdev_, n, cnt.p);
         size_t tb = 0;
         BPE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt.p, pos.p, (int)n, s_));
-        DevBuf<uint8_t> tmp(tb);
+        tmp.reserve(tb);
         BPE_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, cnt.p, pos.p, (int)n, s_));
         uint32_t last[2];
         BPE_HIP(hipMemcpyAsync(&last[0], pos.p + n - 1, 4, hipMemcpyDeviceToHost, s_));
@@ -2322,9 +2349,10 @@ void MergeLoop<TokT>::build_index() {
         BPE_HIP(hipStreamSynchronize(s_));
         E = (unsigned long long)last[0] + last[1];
     }
-    DevBuf<uint32_t> keys(std::max<unsigned long long>(E, 1)), vals(std::max<unsigned long long>(E, 1));
-    DevBuf<uint32_t> keys2(std::max<unsigned long long>(E, 1));
-    ilist_.alloc(std::max<unsigned long long>(E, 1));
+    keys.reserve(std::max<unsigned long long>(E, 1));
+    vals.reserve(std::max<unsigned long long>(E, 1));
+    keys2.reserve(std::max<unsigned long long>(E, 1));
+    ilist_.reserve(std::max<unsigned long long>(E, 1));
     if (E) {
         hipLaunchKernelGGL(k_index_emit<TokT>, dim3(ceil_div(n, 256)), dim3(256), 0, s_, wdev_, n, pos.p,
                            keys.p, vals.p);
@@ -2333,7 +2361,7 @@ void MergeLoop<TokT>::build_index() {
         size_t tb = 0;
         BPE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys.p, keys2.p, vals.p, ilist_.p,
                                                    (int)E, 0, bits, s_));
-        DevBuf<uint8_t> tmp(tb);
+        tmp.reserve(tb);
         BPE_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, keys.p, keys2.p, vals.p, ilist_.p,
                                                    (int)E, 0, bits, s_));
         hipLaunchKernelGGL(k_index_bounds, dim3(ceil_div(E, 256)), dim3(256), 0, s_, keys2.p, E,
@@ -2517,11 +2545,15 @@ void MergeLoop<TokT>::run() {
         batch_.alloc(1);
         BPE_HIP(hipMemsetAsync(batch_.p, 0, sizeof(Batch), s_));
         trip_info_.alloc(2 * 4 * kTrips);
-        if (!snap_st_) {
-            BPE_HIP(hipHostMalloc(reinterpret_cast<void**>(&snap_st_), 2 * sizeof(RoundState)));
-            BPE_HIP(hipHostMalloc(reinterpret_cast<void**>(&snap_ti_), 2 * 4 * kTrips * sizeof(int)));
+        if (!snap_st_) {   // coherent pinned memory, written by k_snapshot
+            BPE_HIP(hipHostMalloc(reinterpret_cast<void**>(&snap_st_), 2 * sizeof(RoundState), hipHostMallocCoherent));
+            BPE_HIP(hipHostMalloc(reinterpret_cast<void**>(&snap_ti_), 2 * 4 * kTrips * sizeof(int),
+                                  hipHostMallocCoherent));
+            BPE_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&snap_st_dev_), snap_st_, 0));
+            BPE_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&snap_ti_dev_), snap_ti_, 0));
             for (auto& e : blk_ev_) BPE_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         }
+        if (const char* e = std::getenv("BPE355_TRIPS")) trips_ = std::max(1, std::min(std::atoi(e), kTrips));
         list_.alloc(kListCap);
     }
     m_a_.alloc(n_rounds_); m_b_.alloc(n_rounds_); m_new_.alloc(n_rounds_); m_mode_.alloc(n_rounds_);
@@ -2549,7 +2581,10 @@ void MergeLoop<TokT>::run() {
     }
     // test knob BPE355_PAIR_CAP_LOG2: a smaller first table (>= 2^18 holds the 65 536 byte pairs
     // at load 1/2), so moderate corpora exercise grow_pairs / k_rehash as the bench corpus does
+    // first table: ~2 slots per unique word (the bench corpus peaks at 0.8 keys per word, so the
+    // table never grows there; each growth is a rehash plus a rebuild of C)
     int pair_log2 = 22;
+    while (pair_log2 < 26 && (1ull << pair_log2) < 2ull * n_words_) ++pair_log2;
     if (const char* e = std::getenv("BPE355_PAIR_CAP_LOG2")) pair_log2 = std::max(18, std::min(30, std::atoi(e)));
     alloc_pairs(size_t(1) << pair_log2);
     const unsigned n_single_keep = hs_.n_single;
@@ -2590,13 +2625,21 @@ void MergeLoop<TokT>::run() {
 
     const bool trace = std::getenv("BPE355_TRACE") != nullptr;
     const int rank = comm_ ? comm_->rank : 0;
+    // host-side phase clock (trace): rebuilds, table growth, compaction + index, trip blocks
+    double h_ms[4] = {0, 0, 0, 0};
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto since = [](std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    };
     for (;;) {
         if (trace)
             std::fprintf(stderr, "[bpe355 r%d] round %d halt %d nC %u T %lld pairs %llu err %u\n", rank,
                          hs_.round, hs_.halt, hs_.nC, hs_.T, hs_.pair_used, hs_.err);
         if (hs_.round >= n_rounds_) break;
         if (hs_.halt == HALT_REBUILD) {
+            const auto t0 = now();
             const int r = rebuild();
+            h_ms[0] += since(t0);
             if (r == 1) { exhaustion(); break; }
             if (r == 2) break;   // no keys left: `if len(byte_pair_frequencies) == 0: break`
         }
@@ -2604,7 +2647,9 @@ void MergeLoop<TokT>::run() {
             // k_select checks the pair table, the token pool and the compaction schedule before
             // every trip and hands back to the host (HALT_HOST); here the host makes room
             if (hs_.pair_used + 4ull * (hs_.ntok + kMaxBatch) * kMaxBatch > pcap_ / kPairLoadDiv) {
+                const auto t0 = now();
                 grow_pairs();
+                h_ms[1] += since(t0);
                 hs_.halt = HALT_REBUILD;   // C holds slot indices: rebuild it
                 continue;
             }
@@ -2614,6 +2659,7 @@ void MergeLoop<TokT>::run() {
             hs_.single_limit = n_live_ / 4 + 1024;
             hs_.pair_limit = pcap_ / kPairLoadDiv;
             push_state();
+            const auto tb0 = now();
             {   // blocks back to back until one halts; the block behind a halted one is empty
                 int slot = 0;
                 launch_block(slot, timing, ev);
@@ -2625,15 +2671,18 @@ void MergeLoop<TokT>::run() {
                 }
                 finish_block(slot ^ 1, timing, ev, k1_ms, k1_bytes, k1_launches);   // drained
             }
+            h_ms[3] += since(tb0);
             BPE_REQUIRE(!(hs_.err & ERR_PAIRS_FULL), BPE_E_NOMEM, "pair table overflow");
             BPE_REQUIRE(!(hs_.err & ERR_C_FULL), BPE_E_NOMEM, "candidate list overflow");
             BPE_REQUIRE(!(hs_.err & ERR_POOL), BPE_E_NOMEM, "token pool overflow");
             if (hs_.halt == HALT_DONE) break;
             if (hs_.n_single > n_live_ / 4 + 1024 || hs_.round >= next_index_round_) {
+                const auto t0 = now();
                 compact();
                 build_index();
                 reset_tags();
                 push_state();
+                h_ms[2] += since(t0);
                 next_index_round_ = std::max(hs_.round + 512, (int)(hs_.round * 2.5));
             }
             continue;
@@ -2714,6 +2763,9 @@ void MergeLoop<TokT>::run() {
         }
     }
     for (auto& e : ev) (void)hipEventDestroy(e);
+    if (trace)
+        std::fprintf(stderr, "[bpe355] merge loop host clock: rebuild %.1f ms, grow %.1f, compact+index %.1f, trip blocks %.1f\n",
+                     h_ms[0], h_ms[1], h_ms[2], h_ms[3]);
     if (round_log && hs_.round) {   // a, b, new, list length (~0: full scan), count per round
         const int rd = hs_.round;
         std::vector<uint32_t> va(rd), vb(rd), vn(rd), vm(rd);
@@ -2832,8 +2884,8 @@ void MergeLoop<TokT>::report_probe() {
 
 template <class TokT>
 void MergeLoop<TokT>::reset_tags() {
-    tags_.alloc(std::max(idev_.n_slot_words, 1u));
-    BPE_HIP(hipMemsetAsync(tags_.p, 0, tags_.bytes(), s_));
+    tags_.reserve(std::max(idev_.n_slot_words, 1u));
+    BPE_HIP(hipMemsetAsync(tags_.p, 0, std::max(idev_.n_slot_words, 1u) * sizeof(uint32_t), s_));
 }
 
 // One block: kTrips x [k_select][k_merge_batch][k_apply_batch], then a snapshot of the state
@@ -2860,7 +2912,7 @@ void MergeLoop<TokT>::launch_block(int slot, bool timing, std::vector<hipEvent_t
     const unsigned apply_blocks = kApplyBatchBlocks;
     int* ti = trip_info_.p + (size_t)slot * 4 * kTrips;
     slot_base_[slot] = trips_launched_;
-    for (int t = 0; t < kTrips; ++t) {
+    for (int t = 0; t < trips_; ++t) {
         const bool timed = timing && (trips_launched_ + t) % kTimingStride == 0;
         hipEvent_t* e = &ev[2 * ((size_t)slot * kTrips + t)];
         hipLaunchKernelGGL(k_select, dim3(1), dim3(kSelThreads), 0, s_, st_.p, bs_.p, pairs(), toks(), idev_,
@@ -2874,12 +2926,15 @@ void MergeLoop<TokT>::launch_block(int slot, bool timing, std::vector<hipEvent_t
                            (const Batch*)batch_.p, pairs(), toks(), LR_.p, lr_member, lr_parity, ntb, part_.p,
                            list_.p, 0);
     }
+    static_assert(sizeof(RoundState) % 4 == 0, "k_snapshot copies words");
+    // the block's snapshot: one small kernel stores the state and the trip records into pinned
+    // host memory (two copy packets cost ~3x as much at every block boundary)
+    hipLaunchKernelGGL(k_snapshot, dim3(1), dim3(256), 0, s_, (const uint32_t*)st_.p,
+                       (unsigned)(sizeof(RoundState) / 4), (const uint32_t*)ti, (unsigned)(4 * trips_),
+                       (uint32_t*)(snap_st_dev_ + slot), (uint32_t*)(snap_ti_dev_ + (size_t)slot * 4 * kTrips));
     BPE_HIP(hipGetLastError());
-    BPE_HIP(hipMemcpyAsync(&snap_st_[slot], st_.p, sizeof(RoundState), hipMemcpyDeviceToHost, s_));
-    BPE_HIP(hipMemcpyAsync(snap_ti_ + (size_t)slot * 4 * kTrips, ti, 4 * kTrips * sizeof(int),
-                           hipMemcpyDeviceToHost, s_));
     BPE_HIP(hipEventRecord(blk_ev_[slot], s_));
-    trips_launched_ += kTrips;
+    trips_launched_ += trips_;
 }
 
 template <class TokT>
@@ -2888,12 +2943,12 @@ void MergeLoop<TokT>::finish_block(int slot, bool timing, std::vector<hipEvent_t
     BPE_HIP(hipEventSynchronize(blk_ev_[slot]));
     hs_ = snap_st_[slot];
     const int* ti = snap_ti_ + (size_t)slot * 4 * kTrips;
-    for (int t = 0; t < kTrips; ++t) trips_run_ += ti[4 * t + 1] > 0;
+    for (int t = 0; t < trips_; ++t) trips_run_ += ti[4 * t + 1] > 0;
     {   // size the merge grid of the blocks launched from now on by this block's largest trip:
         // the members' list entries at one per thread, twice over for growth; a full scan (or
         // a single member without a list) wants the whole layout.  Any grid is correct.
         unsigned need = kMaxBatch;
-        for (int t = 0; t < kTrips; ++t) {
+        for (int t = 0; t < trips_; ++t) {
             if (ti[4 * t + 1] <= 0) continue;
             if (ti[4 * t + 2]) { need = merge_grid_; break; }
             need = std::max(need, 2 * ceil_div((unsigned)ti[4 * t + 3], 256u));
@@ -2902,7 +2957,7 @@ void MergeLoop<TokT>::finish_block(int slot, bool timing, std::vector<hipEvent_t
     }
     if (!timing) return;
     const double slot_avg = scan_bytes_ / std::max(1u, idev_.n_slot_words + words_.ln);
-    for (int t = 0; t < kTrips; ++t) {
+    for (int t = 0; t < trips_; ++t) {
         if ((slot_base_[slot] + t) % kTimingStride || ti[4 * t + 1] <= 0) continue;
         float ms = 0;
         const hipEvent_t* e = &ev[2 * ((size_t)slot * kTrips + t)];
