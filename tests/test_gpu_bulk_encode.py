@@ -92,6 +92,32 @@ def test_encode_chunks_equals_separate_encodes(k, n_words):
     assert list(out[:n_out.value]) == want
 
 
+@pytest.mark.parametrize("k", [2, 3, 5, 11])
+def test_prefix_special_fits_when_longest_straddles_a_cut(k):
+    """Specials '<|a' and '<|a|>': where a piece cut falls inside '<|a|>', the reference's
+    re.split on that piece still matches '<|a' (tokenizer.py:63-66)."""
+    from bpe_amd import Tokenizer, _lib
+    specials = ["<|a", "<|a|>"]
+    vocab, merges = gpt2_files.load_gpt2(specials)
+    tok = Tokenizer(dict(vocab), list(merges), specials)
+    rng = random.Random(k)
+    text = "".join(rng.choice(["<|a|>", "<|a", "|>", " b", "x<|a|>y", "<|", "a|>"]) for _ in range(300))
+    pieces = _pieces(text, k)
+    want = []
+    for piece in pieces:
+        want += oracle.encode(vocab, merges, specials, piece)
+    data = text.encode("utf-8")
+    starts = [0]
+    for piece in pieces[:-1]:
+        starts.append(starts[-1] + len(piece.encode("utf-8")))
+    arr = (ctypes.c_uint64 * len(starts))(*starts)
+    out = (ctypes.c_uint32 * len(data))()
+    n_out = ctypes.c_size_t(0)
+    _lib.check(_lib.lib().bpe_tok_encode_chunks(tok._device(), data, len(data), arr, len(starts), out,
+                                                len(data), ctypes.byref(n_out)))
+    assert list(out[:n_out.value]) == want
+
+
 @pytest.mark.parametrize("fmt", ["pt", "bin"])
 def test_encode_file_matches_reference_loop(tmp_path, fmt):
     import torch

@@ -71,20 +71,21 @@ __global__ void k_find_specials(const uint8_t* __restrict__ s, size_t n, EncTabl
                                 const unsigned* __restrict__ first_mask,
                                 unsigned long long* __restrict__ pos_out, int* __restrict__ sp_out,
                                 unsigned* __restrict__ n_out, unsigned long long cap) {
+    // Every special matching at i is recorded (sorted longest first, the host takes the first
+    // that fits): when the longest one straddles a piece cut, re.split on that piece still
+    // matches a shorter special that is its prefix (tokenizer.py:63-66).
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    int hit = -1;
+    bool cand = false;
     if (i < n) {
         const unsigned b = s[i];
-        if ((first_mask[b >> 5] >> (b & 31)) & 1u) {
-            for (int k = 0; k < E.n_sp; ++k) {  // specials are sorted longest first: first hit wins
-                const unsigned l = E.sp_len[k];
-                if (i + l <= n && bytes_eq(s + i, E.sp_bytes + E.sp_off[k], l)) { hit = k; break; }
-            }
-        }
+        cand = (first_mask[b >> 5] >> (b & 31)) & 1u;
     }
-    const unsigned idx = wave_append(hit >= 0, n_out);
-    if (hit >= 0) {
-        if (idx < cap) { pos_out[idx] = i; sp_out[idx] = hit; }
+    if (!__any(cand)) return;
+    for (int k = 0; k < E.n_sp; ++k) {   // uniform trip count: wave_append needs every lane
+        const unsigned l = E.sp_len[k];
+        const bool hit = cand && i + l <= n && bytes_eq(s + i, E.sp_bytes + E.sp_off[k], l);
+        const unsigned idx = wave_append(hit, n_out);
+        if (hit && idx < cap) { pos_out[idx] = i; sp_out[idx] = k; }
     }
 }
 
@@ -879,7 +880,9 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
         }
         std::vector<size_t> order(cnt);
         for (size_t i = 0; i < cnt; ++i) order[i] = i;
-        std::sort(order.begin(), order.end(), [&](size_t x, size_t y) { return pos[x] < pos[y]; });
+        std::sort(order.begin(), order.end(), [&](size_t x, size_t y) {   // by position, longest first
+            return pos[x] < pos[y] || (pos[x] == pos[y] && spk[x] < spk[y]);
+        });
         unsigned long long cur = 0;
         size_t ci = 0;
         auto cut_until = [&](unsigned long long upto) {   // normal segments ended by cuts <= upto
@@ -893,7 +896,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
             if (p0 < cur) continue;
             const unsigned long long e = p0 + T.specials[spk[oi]].size();
             cut_until(p0);
-            if (ci < cuts.size() && cuts[ci] < e) continue;   // straddles a chunk boundary
+            if (ci < cuts.size() && cuts[ci] < e) continue;   // straddles a cut: a shorter one at p0 may fit
             if (p0 > cur) segs.push_back(Seg{cur, p0, -1, 0});
             segs.push_back(Seg{p0, e, spk[oi], 0});
             cur = e;

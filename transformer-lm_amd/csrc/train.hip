@@ -66,7 +66,7 @@ struct RoundState {
     int n_rounds;
     int ntok;
     long long T;
-    unsigned nC, capC, c_limit, pad0;
+    unsigned nC, capC, c_limit, probe_merge_done;   // probe_*_done: BPE355_PROBE workgroup counters
     unsigned nC_base;           // |C| before this round's appends (set by k_merge)
     int cur_round, cur_ntok;    // for k_apply_argmax: this round, and ntok after it (k_merge)
     unsigned cur_a, cur_b, cur_new, cur_slot;
@@ -78,7 +78,7 @@ struct RoundState {
     unsigned long long pair_used;
     unsigned long long scan_slots;
     int nparts;                 // batched: apply workgroups whose top-M lists part[] holds
-    int pad1;
+    unsigned probe_apply_done;
     unsigned long long* probe;  // BPE355_PROBE: phase stamps of sampled trips (else null)
     // batched rounds (k_select): the host's limits, checked before every trip
     int host_round;             // hand back to the host at this round (compaction schedule)
@@ -874,10 +874,22 @@ struct DeltaSinkN {
     }
 };
 
-// BPE355_PROBE: 100 MHz stamps of one trip in kProbeTrip, 16 per sampled trip (MergeLoop::report_probe)
+// BPE355_PROBE: 100 MHz stamps of one trip in kProbeTrip, kProbeSlots per sampled trip
+// (MergeLoop::report_probe): 0-13 phase stamps, 14/15 the last merge/apply workgroup done, 16 the
+// next trip's select start
 constexpr int kProbeTrip = 8;
+constexpr int kProbeSlots = 20;
 __device__ __forceinline__ void probe_stamp(const RoundState* st, int trip, int k) {
-    if (st->probe && (trip % kProbeTrip) == 0) st->probe[16 * (size_t)(trip / kProbeTrip) + k] = __builtin_amdgcn_s_memrealtime();
+    if (st->probe && (trip % kProbeTrip) == 0)
+        st->probe[kProbeSlots * (size_t)(trip / kProbeTrip) + k] = __builtin_amdgcn_s_memrealtime();
+}
+// one workgroup of a sampled trip's kernel is done (thread 0, after the workgroup's work): the
+// last of the grid stamps slot k
+__device__ __forceinline__ void probe_done(RoundState* st, unsigned* ctr, int trip, int k) {
+    if (st->probe && (trip % kProbeTrip) == 0) {
+        const unsigned o = atomicAdd(ctr, 1u);
+        if (o % gridDim.x == gridDim.x - 1) probe_stamp(st, trip, k);
+    }
 }
 
 __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int j) {
@@ -942,7 +954,11 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     __shared__ TokMetaS s_meta[kTopM];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int ptrip = bs->trip;
-    if (tid == 0) probe_stamp(st, ptrip, 0);
+    if (tid == 0) {
+        probe_stamp(st, ptrip, 0);
+        if (ptrip > 0 && st->probe && ((ptrip - 1) % kProbeTrip) == 0)
+            st->probe[kProbeSlots * (size_t)((ptrip - 1) / kProbeTrip) + 16] = __builtin_amdgcn_s_memrealtime();
+    }
     // ---- every independent load first
     Partial q{};
     if (wv < kSelListWave) q = part[tid];   // the buffer holds kApplyBatchBlocks entries
@@ -1036,6 +1052,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         if (cand_better(s_wave[w], p1, K.pool, K.off, K.len)) p1 = s_wave[w];
     // the list's head is the global best whenever the best is >= T2 and nothing overflowed; the
     // ranks are distinct, so s_list holds a prefix
+    if (lane == 0) probe_stamp(st, ptrip, 17);
     const bool list_ok = ln <= kListCap && s_list[0].cnt != LLONG_MIN && s_list[0].slot == p1.slot &&
                          s_list[0].a == p1.a && s_list[0].b == p1.b;
     int nf = 1;
@@ -1083,6 +1100,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         old = s_nw_old[i];
     }
     const bool fr = i < nf && old == ~0u;
+    if (lane == 0) probe_stamp(st, ptrip, 18);
     const unsigned long long h = m.ha * m.pb + m.hb;
     const unsigned lk = m.la + m.lb;
     // (1) tokens disjoint from, and (3) new bytes different from, every earlier candidate's
@@ -1147,6 +1165,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
             k = k_strict;
         }
     }
+    if (lane == 0) probe_stamp(st, ptrip, 19);
     const bool fr0 = __builtin_amdgcn_readlane((int)fr, 0);
     if (k == 1 && lane == 0) {
         const int why = p1.a == p1.b ? 0 : !fr0 ? 1 : nf == 1 ? 2 : k_rule == 1 ? 3 : 4;
@@ -1305,7 +1324,10 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
         if (bid >= (unsigned)k && bid < W.lblk0) {
             const bool lists = k > 1 ? !B.full_scan : B.m[0].use_list != 0;
             const unsigned total = k > 1 ? B.list_pre[k] : B.m[0].list_len;
-            if (lists && bid * blockDim.x >= total) return;
+            if (lists && bid * blockDim.x >= total) {
+                if (tid == 0) probe_done(st, &st->probe_merge_done, B.trip, 14);
+                return;
+            }
         }
     }
     if (tid < k) { s_ma[tid] = B.m[tid].a; s_mb[tid] = B.m[tid].b; s_mn[tid] = B.m[tid].nw; }
@@ -1420,6 +1442,10 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
         if (v) atomicAdd(&LRt[(size_t)(q / (2 * kLdsB)) * lr_member + q % (2 * kLdsB)], v);
     }
     if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 8);
+    if (st->probe) {
+        __syncthreads();
+        if (tid == 0) probe_done(st, &st->probe_merge_done, B.trip, 14);
+    }
 }
 
 // Apply the trip's deltas and list the next trip's candidates.  Items:
@@ -1665,6 +1691,10 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
         }
     }
     if (pw0) probe_stamp(st, B.trip, 13);
+    if (!scan_only && st->probe) {
+        __syncthreads();
+        if (tid == 0) probe_done(st, &st->probe_apply_done, B.trip, 15);
+    }
 }
 
 // ------------------------------------------------------------------ word table build
@@ -2607,7 +2637,7 @@ void MergeLoop<TokT>::run() {
     hs_.max_len = std::max(max_len_, 1u);
     hs_.max_batch = max_batch_;
     if (batched_ && std::getenv("BPE355_PROBE")) {
-        probe_.alloc(16ull * (n_rounds_ / kProbeTrip + 2));
+        probe_.alloc((size_t)kProbeSlots * (n_rounds_ / kProbeTrip + 2));
         BPE_HIP(hipMemsetAsync(probe_.p, 0, probe_.bytes(), s_));
         hs_.probe = probe_.p;
     }
@@ -2840,26 +2870,55 @@ void MergeLoop<TokT>::report_probe() {
     const int to[] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 16};
     double acc[14] = {};
     int n = 0;
-    for (size_t t = 0; t + 1 < pr.size() / 16; ++t) {
-        const unsigned long long* p = &pr[16 * t];
-        const unsigned long long* q = &pr[16 * (t + 1)];
+    // the last workgroups: merge flush (block 0) -> last merge workgroup done -> apply start;
+    // apply end (block 0) -> last apply workgroup done -> the next trip's select start
+    double tails[4] = {};
+    int nt4 = 0;
+    for (size_t t = 0; t + 1 < pr.size() / kProbeSlots; ++t) {
+        const unsigned long long* p = &pr[kProbeSlots * t];
         bool ok = true;
         for (int i = 0; i < 14; ++i) ok &= p[i] != 0;
         if (!ok) continue;
         for (int i = 0; i < 13; ++i) acc[i] += (double)(p[to[i]] - p[from[i]]) * 0.01;
-        (void)q;
         ++n;
+        if (p[14] && p[15] && p[16]) {
+            tails[0] += (double)(long long)(p[14] - p[8]) * 0.01;
+            tails[1] += (double)(long long)(p[9] - p[14]) * 0.01;
+            tails[2] += (double)(long long)(p[15] - p[13]) * 0.01;
+            tails[3] += (double)(long long)(p[16] - p[15]) * 0.01;
+            ++nt4;
+        }
     }
     std::fprintf(stderr, "[bpe355 probe] %d sampled trips, mean us:", n);
     for (int i = 0; i < 13 && n; ++i) std::fprintf(stderr, " %s %.2f |", names[i], acc[i] / n);
     std::fprintf(stderr, "\n");
+    {   // inside select's rule: p1 over the waves | list head + metadata | clash + k | strict gap / 4'
+        double r[4] = {};
+        int nr = 0;
+        for (size_t t = 0; t + 1 < pr.size() / kProbeSlots; ++t) {
+            const unsigned long long* p = &pr[kProbeSlots * t];
+            if (!(p[2] && p[17] && p[18] && p[19] && p[3])) continue;
+            r[0] += (double)(p[17] - p[2]) * 0.01; r[1] += (double)(p[18] - p[17]) * 0.01;
+            r[2] += (double)(p[19] - p[18]) * 0.01; r[3] += (double)(p[3] - p[19]) * 0.01;
+            ++nr;
+        }
+        if (nr)
+            std::fprintf(stderr, "[bpe355 probe] select rule: p1 %.2f | head+meta %.2f | clash+k+gap %.2f | record %.2f\n",
+                         r[0] / nr, r[1] / nr, r[2] / nr, r[3] / nr);
+    }
+    if (nt4)
+        std::fprintf(stderr, "[bpe355 probe] %d trips: merge last-workgroup tail %.2f | last merge wg > apply start %.2f | "
+                     "apply last-workgroup tail %.2f | last apply wg > next select %.2f\n", nt4, tails[0] / nt4,
+                     tails[1] / nt4, tails[2] / nt4, tails[3] / nt4);
     // distribution of whole trips (select start -> apply end) and of the rewrite, by trip decile
     std::vector<double> tot, rw;
     std::vector<double> dec_tot(10, 0.0), dec_rw(10, 0.0);
     std::vector<int> dec_n(10, 0);
-    const size_t nt = pr.size() / 16;
+    size_t nt = 0;   // sampled trips that ran (the buffer is sized for the worst case)
+    for (size_t t = 0; t < pr.size() / kProbeSlots; ++t)
+        if (pr[kProbeSlots * t] != 0) nt = t + 1;
     for (size_t t = 0; t < nt; ++t) {
-        const unsigned long long* p = &pr[16 * t];
+        const unsigned long long* p = &pr[kProbeSlots * t];
         bool ok = true;
         for (int i = 0; i < 14; ++i) ok &= p[i] != 0;
         if (!ok) continue;
