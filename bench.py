@@ -269,9 +269,27 @@ def main():
         torch.cuda.synchronize()
         barrier()
         te = max_over_ranks(time.perf_counter() - te)
+        # B_enc = N + 4 n_ids (corpus read once, u32 ids written once)
+        b_enc = slab + 4 * int(n_out.value)
         encode = {"value": round(n / te / 1e6, 1), "unit": "MB/s", "ids_rank0": int(n_out.value),
-                  "seconds": round(te, 4), "scope": "corpus in HBM -> ids in HBM"}
+                  "seconds": round(te, 4), "scope": "corpus in HBM -> ids in HBM",
+                  "roofline": {"bound": "hbm", "achieved": round(b_enc / te / 1e9, 2), "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": round(b_enc / te / 1e9 / HBM_PEAK_GBS, 4),
+                               "bytes": b_enc, "note": "whole encode (all its kernels) on rank 0's slab"}}
         del out
+        if not args.no_file and not multiproc and n_gpus == 1:
+            # the drop-in dataset encoder end to end: file -> np.uint16 ids in host memory
+            # (encode.py:31-37 without the torch.save), 1 M-character pieces
+            from bpe_amd.encode import encode_file
+            torch.cuda.synchronize()
+            tf0 = time.perf_counter()
+            ids16 = encode_file(tok, path)
+            tf = time.perf_counter() - tf0
+            encode["end_to_end"] = {"value": round(n / tf / 1e6, 1), "unit": "MB/s", "seconds": round(tf, 3),
+                                    "ids": int(ids16.size),
+                                    "scope": "encode_file(path): file read -> np.uint16 ids in host memory, "
+                                             "1 M-character pieces (encode.py:31-37)"}
+            del ids16
 
     # ---------------------------------------------------------------- CPU baseline (rank 0, N=1)
     cpu = None

@@ -205,6 +205,12 @@ int bpe_dec_decode_device(bpe_decoder* dec, const uint32_t* d_ids, size_t n, uin
 void bpe_dec_free(bpe_decoder* dec);
 
 /* ---------------------------------------------------------------- bulk encode plumbing */
+/* The raw bytes of a regular file -> device memory d_dst (cap bytes): pread by a pool of host
+ * threads into pinned staging buffers, each DMA'd to HBM while the next is read (the file read
+ * of encode.py:31-33 / tokenizer.py:111, without a pageable host copy).  d_dst == NULL: size
+ * query (*n_out = file size).  BPE_E_IO (errno) on a missing file, a directory, or a file that
+ * is not regular (the caller reads a pipe itself); BPE_E_ARG if cap is too small. */
+int bpe_read_file_device(const char* path, uint8_t* d_dst, size_t cap, size_t* n_out);
 /* open(path, "r", encoding="utf-8").read() on device bytes: strict UTF-8 (BPE_E_UTF8) and
  * universal newlines.  d_out holds n bytes (may be d_in); *n_out = resulting length. */
 int bpe_text_prepare_device(const uint8_t* d_in, size_t n, uint8_t* d_out, size_t* n_out, void* hip_stream);

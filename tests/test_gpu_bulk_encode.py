@@ -156,3 +156,49 @@ def test_ids_above_uint16_are_refused():
         _lib.check(_lib.lib().bpe_ids_to_u16_device(_device(ids), 3, _device(out), None))
     _lib.check(_lib.lib().bpe_ids_to_u16_device(_device(ids), 2, _device(out), None))
     assert out[:2].cpu().numpy().view(np.uint16).tolist() == [1, 65535]
+
+
+def test_read_file_device_bytes(tmp_path):
+    """the library's file reader (pinned staging, several pread threads, 16 MB chunks): exact
+    bytes at sizes around the chunk size, and the reference's exceptions for bad paths"""
+    import os
+    from bpe_amd.encode import read_file_device
+    rng = np.random.default_rng(5)
+    for size in (0, 1, (16 << 20) - 1, (16 << 20) + 1, 3 * (16 << 20) + 12345):
+        p = tmp_path / f"f{size}.bin"
+        data = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+        p.write_bytes(data)
+        raw = read_file_device(p)
+        assert raw is not None and raw.numel() == size
+        assert bytes(raw.cpu().numpy()) == data
+    with pytest.raises(FileNotFoundError):
+        read_file_device(tmp_path / "missing.txt")
+    assert read_file_device(tmp_path) is None   # not a regular file: encode_file reads it itself
+    from bpe_amd import _lib
+    n = ctypes.c_size_t(0)
+    rc = _lib.lib().bpe_read_file_device(os.fsencode(str(tmp_path)), None, 0, ctypes.byref(n))
+    assert rc != 0
+
+
+def test_encode_file_from_fifo_and_directory(tmp_path):
+    """a FIFO goes through the host read (as the reference's open().read()); a directory raises
+    IsADirectoryError like open() does"""
+    import os
+    import threading
+    from bpe_amd import Tokenizer
+    from bpe_amd.encode import encode_file
+    vocab, merges = gpt2_files.load_gpt2(["<|endoftext|>"])
+    tok = Tokenizer(dict(vocab), list(merges), ["<|endoftext|>"])
+    text = _mixed_text(4, 3000)
+    src = tmp_path / "reg.txt"
+    src.write_bytes(text.encode("utf-8"))
+    want = encode_file(tok, src, chars_per_piece=500)
+    fifo = tmp_path / "pipe"
+    os.mkfifo(fifo)
+    w = threading.Thread(target=lambda: fifo.write_bytes(text.encode("utf-8")))
+    w.start()
+    got = encode_file(tok, fifo, chars_per_piece=500)
+    w.join()
+    assert got.tolist() == want.tolist()
+    with pytest.raises(IsADirectoryError):
+        encode_file(tok, tmp_path)

@@ -12,6 +12,8 @@ timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/s
 cat $OUT/smoke.log
 timeout -k 10 400 python -u bench.py > $OUT/bench.log 2>&1 || { echo "bench failed"; tail -30 $OUT/bench.log; exit 1; }
 tail -1 $OUT/bench.log
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 -u bench.py --no-cpu-baseline --steps 2 > $OUT/bench_prof.log 2>&1 || { echo "rocprof failed"; tail -30 $OUT/bench_prof.log; exit 1; }
+# the profile of the roofline's own configuration: corpus in HBM, one k_count2 launch per step
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 -u bench.py --no-cpu-baseline --no-file --steps 2 > $OUT/bench_prof.log 2>&1 || { echo "rocprof failed"; tail -30 $OUT/bench_prof.log; exit 1; }
 tail -1 $OUT/bench_prof.log
+bash tools/gpu_pmc.sh $TAG/pmc || exit 1
 echo done

@@ -23,6 +23,8 @@ from __future__ import annotations
 
 import argparse
 import ctypes
+import os
+import stat
 
 import numpy as np
 
@@ -41,15 +43,14 @@ fname = {   # encode.py:8-15
 CHARS_PER_PIECE = 1024 * 1024   # encode.py:33 f.read(1024 * 1024)
 
 
-def encode_bytes_u16(tokenizer: Tokenizer, data: bytes, chars_per_piece: int = CHARS_PER_PIECE) -> np.ndarray:
-    """The reference's encode.py ids for a file whose raw bytes are `data`, as np.uint16."""
+def encode_device_u16(tokenizer: Tokenizer, raw, chars_per_piece: int = CHARS_PER_PIECE) -> np.ndarray:
+    """The reference's encode.py ids for the raw file bytes held in the device tensor `raw`
+    (uint8; overwritten by the text-mode read), as np.uint16 in host memory."""
     import torch
     L = _lib.lib()
-    n = len(data)
+    n = raw.numel()
     if n == 0:
         return np.zeros(0, dtype=np.uint16)
-    raw = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda")
-    torch.cuda.synchronize()
     m = ctypes.c_size_t(0)
     _lib.check(L.bpe_text_prepare_device(ctypes.c_void_p(raw.data_ptr()), n, ctypes.c_void_p(raw.data_ptr()),
                                          ctypes.byref(m), None), "read")
@@ -69,16 +70,48 @@ def encode_bytes_u16(tokenizer: Tokenizer, data: bytes, chars_per_piece: int = C
     out16 = torch.empty(max(k, 1), dtype=torch.int16, device="cuda")
     _lib.check(L.bpe_ids_to_u16_device(ctypes.c_void_p(ids.data_ptr()), k, ctypes.c_void_p(out16.data_ptr()),
                                        None), "uint16 ids")
+    del ids
     torch.cuda.synchronize()
     return out16[:k].cpu().numpy().view(np.uint16)
+
+
+def encode_bytes_u16(tokenizer: Tokenizer, data: bytes, chars_per_piece: int = CHARS_PER_PIECE) -> np.ndarray:
+    """The reference's encode.py ids for a file whose raw bytes are `data`, as np.uint16."""
+    import torch
+    if len(data) == 0:
+        return np.zeros(0, dtype=np.uint16)
+    raw = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda")
+    torch.cuda.synchronize()
+    return encode_device_u16(tokenizer, raw, chars_per_piece)
+
+
+def read_file_device(path):
+    """A regular file's raw bytes in HBM (uint8 tensor) through the library's reader: pinned
+    staging buffers filled by a pool of pread threads, each DMA'd while the next is read.  None
+    for a file that is not regular (a pipe, FIFO or device): the caller reads it itself."""
+    import torch
+    if not stat.S_ISREG(os.stat(path).st_mode):   # missing: FileNotFoundError, as open() raises
+        return None
+    L = _lib.lib()
+    n = ctypes.c_size_t(0)
+    p = os.fsencode(os.fspath(path))
+    _lib.check(L.bpe_read_file_device(p, None, 0, ctypes.byref(n)), "read")
+    raw = torch.empty(max(n.value, 1), dtype=torch.uint8, device="cuda")[:n.value]
+    if n.value:
+        _lib.check(L.bpe_read_file_device(p, ctypes.c_void_p(raw.data_ptr()), n.value, ctypes.byref(n)), "read")
+    return raw
 
 
 def encode_file(tokenizer: Tokenizer, input_path, output_path=None, fmt: str = "pt",
                 chars_per_piece: int = CHARS_PER_PIECE) -> np.ndarray:
     """Encode a text file like encode.py:main; write it if output_path is given."""
-    with open(input_path, "rb") as f:
-        data = f.read()
-    pt = encode_bytes_u16(tokenizer, data, chars_per_piece)
+    raw = read_file_device(input_path)
+    if raw is not None:
+        pt = encode_device_u16(tokenizer, raw, chars_per_piece)
+    else:
+        with open(input_path, "rb") as f:
+            data = f.read()
+        pt = encode_bytes_u16(tokenizer, data, chars_per_piece)
     if output_path is not None:
         if fmt == "pt":
             import torch

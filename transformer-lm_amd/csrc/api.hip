@@ -77,7 +77,10 @@ void put_u32(std::string& b, uint32_t v) { b.append(reinterpret_cast<const char*
 
 }  // namespace
 
-void set_error(int, const std::string& msg) { g_err = msg; }
+void set_error(int, const std::string& msg, int sys_errno) {
+    g_err = msg;
+    g_errno = sys_errno;
+}
 bool timing_enabled() { return g_timing; }
 
 }  // namespace bpe

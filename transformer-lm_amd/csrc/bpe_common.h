@@ -13,7 +13,7 @@ namespace bpe {
 
 // ------------------------------------------------------------------ error plumbing
 // Every C-ABI entry point returns a BPE_* code and leaves a message for bpe_last_error().
-void set_error(int code, const std::string& msg);
+void set_error(int code, const std::string& msg, int sys_errno = 0);
 struct Error {
     int code;
     std::string msg;

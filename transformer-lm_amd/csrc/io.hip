@@ -10,6 +10,9 @@
 
 #include <vector>
 
+#include <sys/stat.h>
+
+#include "drive.h"
 #include "internal.h"
 
 namespace bpe {
@@ -59,7 +62,7 @@ int guarded_io(F&& f) {
         set_error(0, "");
         return BPE_OK;
     } catch (const Error& e) {
-        set_error(e.code, e.msg);
+        set_error(e.code, e.msg, e.sys_errno);
         return e.code;
     } catch (const std::bad_alloc&) {
         set_error(BPE_E_NOMEM, "host allocation failed");
@@ -71,6 +74,23 @@ int guarded_io(F&& f) {
 }  // namespace bpe
 
 extern "C" {
+
+int bpe_read_file_device(const char* path, uint8_t* d_dst, size_t cap, size_t* n_out) {
+    return bpe::guarded_io([&] {
+        BPE_REQUIRE(path && n_out, BPE_E_ARG, "NULL argument");
+        *n_out = 0;
+        struct stat st;
+        if (::stat(path, &st) == 0 && !S_ISREG(st.st_mode) && !S_ISDIR(st.st_mode))
+            throw bpe::Error{BPE_E_IO, std::string("not a regular file: ") + path, EINVAL};
+        const bpe::Source src = bpe::Source::open_path(path);   // missing file / directory: errno
+        *n_out = src.size;
+        if (!d_dst) return;
+        BPE_REQUIRE(cap >= src.size, BPE_E_ARG, "device buffer smaller than the file");
+        int dev = 0;
+        BPE_HIP(hipGetDevice(&dev));
+        bpe::stage_to_device(src, 0, src.size, d_dst, dev, bpe::io_threads());
+    });
+}
 
 int bpe_text_prepare_device(const uint8_t* d_in, size_t n, uint8_t* d_out, size_t* n_out, void* hip_stream) {
     return bpe::guarded_io([&] {

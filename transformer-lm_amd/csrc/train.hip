@@ -650,6 +650,56 @@ __device__ __forceinline__ size_t pair_update(const PairsDev& P, RoundState* st,
     return s;
 }
 
+// pair_update with the home slot's key, count and flags already loaded (k0, c0, f0): the
+// caller issues several keys' home-slot loads before finishing any of them
+__device__ __forceinline__ size_t pair_update_from(const PairsDev& P, RoundState* st, unsigned p, unsigned q,
+                                                   long long delta, bool inc, unsigned long long k0, long long c0,
+                                                   unsigned f0, long long* c_out, unsigned* f_out) {
+    const unsigned long long key = pair_key(p, q);
+    size_t s = mix64(key) & P.mask;
+    long long c = c0;
+    unsigned f = f0;
+    bool ins = false;
+    if (k0 != key) {   // the probe from the home slot on, its first key already known
+        unsigned long long k = k0;
+        size_t probe = 0;
+        for (;;) {
+            if (k == key) break;
+            if (k == 0) {
+                k = atomicCAS(&P.key[s], 0ULL, key);
+                if (k == 0) {
+                    atomicAdd(&st->pair_used, 1ULL);
+                    ins = true;
+                    break;
+                }
+                if (k == key) break;
+            }
+            if (++probe > P.mask) {
+                atomicOr(&st->err, ERR_PAIRS_FULL);
+                return ~(size_t)0;
+            }
+            s = (s + 1) & P.mask;
+            k = P.key[s];
+        }
+        if (ins) {          // a slot this call claimed was empty: count and flags are 0
+            c = 0;
+            f = 0;
+        } else {
+            c = P.cnt[s];
+            f = P.flag[s];
+        }
+    }
+    c += delta;
+    P.cnt[s] = c;
+    if ((inc || ins) && !(f & kPresent)) {
+        f |= kPresent;
+        P.flag[s] = f;
+    }
+    *c_out = c;
+    *f_out = f;
+    return s;
+}
+
 constexpr unsigned kApplyThreads = 256;    // large workgroups: fewer argmax partials for k_merge
 __global__ void __launch_bounds__(kApplyThreads) k_apply_argmax(RoundState* __restrict__ st, PairsDev P, ToksDev K,
                                                       const unsigned long long* __restrict__ LR,
@@ -876,9 +926,9 @@ struct DeltaSinkN {
 
 // BPE355_PROBE: 100 MHz stamps of one trip in kProbeTrip, kProbeSlots per sampled trip
 // (MergeLoop::report_probe): 0-13 phase stamps, 14/15 the last merge/apply workgroup done, 16 the
-// next trip's select start
+// next trip's select start, 17-19 inside select's rule, 20/21 the last merge/apply workgroup's index
 constexpr int kProbeTrip = 8;
-constexpr int kProbeSlots = 20;
+constexpr int kProbeSlots = 24;
 __device__ __forceinline__ void probe_stamp(const RoundState* st, int trip, int k) {
     if (st->probe && (trip % kProbeTrip) == 0)
         st->probe[kProbeSlots * (size_t)(trip / kProbeTrip) + k] = __builtin_amdgcn_s_memrealtime();
@@ -888,7 +938,10 @@ __device__ __forceinline__ void probe_stamp(const RoundState* st, int trip, int 
 __device__ __forceinline__ void probe_done(RoundState* st, unsigned* ctr, int trip, int k) {
     if (st->probe && (trip % kProbeTrip) == 0) {
         const unsigned o = atomicAdd(ctr, 1u);
-        if (o % gridDim.x == gridDim.x - 1) probe_stamp(st, trip, k);
+        if (o % gridDim.x == gridDim.x - 1) {
+            probe_stamp(st, trip, k);
+            st->probe[kProbeSlots * (size_t)(trip / kProbeTrip) + k + 6] = blockIdx.x + 1;
+        }
     }
 }
 
@@ -1570,82 +1623,105 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     // and its steps far apart, so the dense start of each member's cells (the byte tokens, which
     // neighbour everything) spreads over many waves instead of serialising in a few
     for (unsigned base = 0; base < n_items; base += S * kBatchApplyItems) {
-        // every item's first load, then every C entry's slot state, before any processing
-        unsigned long long dv[kBatchApplyItems];
+        // three stages over the thread's items, so that their dependent loads overlap instead of
+        // chaining item after item: (1) each item's first load -- its cell, an S key's two cells, a
+        // C entry; (2) each item's key and the loads it needs -- the key's home slot and both
+        // tokens' prefixes (an update), or the slot state and the touched cells (a C entry);
+        // (3) the updates and offers
+        unsigned long long dv[kBatchApplyItems], dw[kBatchApplyItems];
         uint4 ce[kBatchApplyItems];
 #pragma unroll
         for (unsigned u = 0; u < kBatchApplyItems; ++u) {
             const unsigned v = base + u * S + g;
             dv[u] = 0;
+            dw[u] = 0;
             ce[u] = make_uint4(0, 0, 0, 0);
             if (v < n_cell) {
                 const unsigned j = v / per_member, r = v % per_member, x = r >> 2, op = r & 3;
                 dv[u] = LRc[(size_t)j * lr_member + 2 * (size_t)x + (op >> 1)];
-            } else if (v >= n_cell + n_sp && v < n_items) {
-                ce[u] = P.C[v - n_cell - n_sp];
-            }
-        }
-        long long cc[kBatchApplyItems];
-        unsigned cf[kBatchApplyItems];
-        unsigned long long ck[kBatchApplyItems][2];
-#pragma unroll
-        for (unsigned u = 0; u < kBatchApplyItems; ++u) {
-            const unsigned v = base + u * S + g;
-            cc[u] = 0; cf[u] = 0; ck[u][0] = 0; ck[u][1] = 0;
-            if (v >= n_cell + n_sp && v < n_items) {
-                cf[u] = P.flag[ce[u].x];
-                cc[u] = P.cnt[ce[u].x];
-                ck[u][0] = K.key8[ce[u].y];
-                ck[u][1] = K.key8[ce[u].z];
-            }
-        }
-#pragma unroll
-        for (unsigned u = 0; u < kBatchApplyItems; ++u) {
-            const unsigned v = base + u * S + g;
-            if (v < n_cell) {
-                const unsigned j = v / per_member, r = v % per_member, x = r >> 2, op = r & 3;
-                const long long d = (long long)dv[u];
-                if (d && !in_S(x)) {
-                    const BatchMember& M = B.m[j];
-                    const unsigned p = op <= 1 ? x : (op == 2 ? M.b : M.nw);
-                    const unsigned q = op == 0 ? M.a : (op == 1 ? M.nw : x);
-                    const bool inc = op & 1;
-                    const unsigned long long kp = K.key8[p], kq = K.key8[q];   // issued with the probe
-                    long long c;
-                    unsigned f;
-                    const size_t s = pair_update(P, st, p, q, inc ? d : -d, inc, &c, &f);
-                    updated(s, p, q, c, f, inc, kp, kq);
-                }
             } else if (v < n_cell + n_sp) {
                 const unsigned sp = v - n_cell;
                 const unsigned p = s_tok[sp / ns], q = s_tok[sp % ns];
                 const unsigned rp = s_role[sp / ns], rq = s_role[sp % ns];
                 // q's member sees p on its left (cell 2p), p's member sees q on its right (2q + 1)
-                const unsigned long long lq = (rq & 5) ? LRc[(size_t)(rq >> 3) * lr_member + 2 * (size_t)p] : 0ull;
-                const unsigned long long lp = (rp & 6) ? LRc[(size_t)(rp >> 3) * lr_member + 2 * (size_t)q + 1] : 0ull;
+                if (rq & 5) dv[u] = LRc[(size_t)(rq >> 3) * lr_member + 2 * (size_t)p];
+                if (rp & 6) dw[u] = LRc[(size_t)(rp >> 3) * lr_member + 2 * (size_t)q + 1];
+            } else if (v < n_items) {
+                ce[u] = P.C[v - n_cell - n_sp];
+            }
+        }
+        unsigned ip[kBatchApplyItems], iq[kBatchApplyItems], how[kBatchApplyItems];   // how: 1 update, 2 inc, 4 C entry
+        long long delta[kBatchApplyItems], hc[kBatchApplyItems];
+        unsigned long long hk[kBatchApplyItems], kp[kBatchApplyItems], kq[kBatchApplyItems];
+        unsigned hf[kBatchApplyItems];
+        bool touched[kBatchApplyItems];
+#pragma unroll
+        for (unsigned u = 0; u < kBatchApplyItems; ++u) {
+            const unsigned v = base + u * S + g;
+            how[u] = 0; ip[u] = 0; iq[u] = 0; delta[u] = 0; touched[u] = false;
+            hk[u] = 0; hc[u] = 0; hf[u] = 0; kp[u] = 0; kq[u] = 0;
+            if (v < n_cell) {
+                const unsigned j = v / per_member, r = v % per_member, x = r >> 2, op = r & 3;
+                const long long d = (long long)dv[u];
+                if (d && !in_S(x)) {
+                    const BatchMember& M = B.m[j];
+                    ip[u] = op <= 1 ? x : (op == 2 ? M.b : M.nw);
+                    iq[u] = op == 0 ? M.a : (op == 1 ? M.nw : x);
+                    const bool inc = op & 1;
+                    delta[u] = inc ? d : -d;
+                    how[u] = 1 | (inc ? 2 : 0);
+                }
+            } else if (v < n_cell + n_sp) {
+                const unsigned sp = v - n_cell;
+                const unsigned rp = s_role[sp / ns], rq = s_role[sp % ns];
+                const long long lq = (long long)dv[u], lp = (long long)dw[u];
                 const bool popped = (rp >> 3) == (rq >> 3) && (rp & 1) && (rq & 2);
                 long long inc = 0, dec = 0;
-                if (rq & 1) dec += (long long)lq;
-                if (rq & 4) inc += (long long)lq;
-                if (rp & 2) dec += (long long)lp;
-                if (rp & 4) inc += (long long)lp;
+                if (rq & 1) dec += lq;
+                if (rq & 4) inc += lq;
+                if (rp & 2) dec += lp;
+                if (rp & 4) inc += lp;
                 if (!popped && (inc || dec)) {
-                    const unsigned long long kp = K.key8[p], kq = K.key8[q];
-                    long long c;
-                    unsigned f;
-                    const size_t s = pair_update(P, st, p, q, inc - dec, inc != 0, &c, &f);
-                    updated(s, p, q, c, f, inc != 0, kp, kq);
+                    ip[u] = s_tok[sp / ns];
+                    iq[u] = s_tok[sp % ns];
+                    delta[u] = inc - dec;
+                    how[u] = 1 | (inc != 0 ? 2 : 0);
                 }
             } else if (v < n_items) {
                 const unsigned p = ce[u].y, q = ce[u].z;
-                bool touched = false;
-                {   // does an item of this trip update the key?
-                    const int ip = find_S(p), iq = find_S(q);
-                    const unsigned rp = ip >= 0 ? s_role[ip] : 0u, rq = iq >= 0 ? s_role[iq] : 0u;
-                    if ((rq & 5) && LRc[(size_t)(rq >> 3) * lr_member + 2 * (size_t)p] != 0) touched = true;
-                    if ((rp & 6) && LRc[(size_t)(rp >> 3) * lr_member + 2 * (size_t)q + 1] != 0) touched = true;
-                }
-                if (!touched && (cf[u] & kPresent)) offer(Cand{cc[u], ck[u][0], ck[u][1], ce[u].x, p, q});
+                ip[u] = p;
+                iq[u] = q;
+                how[u] = 4;
+                // does an item of this trip update the key?
+                const int sp_ = find_S(p), sq_ = find_S(q);
+                const unsigned rp = sp_ >= 0 ? s_role[sp_] : 0u, rq = sq_ >= 0 ? s_role[sq_] : 0u;
+                const unsigned long long t1 = (rq & 5) ? LRc[(size_t)(rq >> 3) * lr_member + 2 * (size_t)p] : 0ull;
+                const unsigned long long t2 = (rp & 6) ? LRc[(size_t)(rp >> 3) * lr_member + 2 * (size_t)q + 1] : 0ull;
+                touched[u] = (t1 | t2) != 0;
+                hf[u] = P.flag[ce[u].x];
+                hc[u] = P.cnt[ce[u].x];
+            }
+            if (how[u] & 1) {   // the key's home slot: at load <= 1/2 it usually decides
+                const size_t s0 = mix64(pair_key(ip[u], iq[u])) & P.mask;
+                hk[u] = P.key[s0];
+                hc[u] = P.cnt[s0];
+                hf[u] = P.flag[s0];
+            }
+            if (how[u]) {
+                kp[u] = K.key8[ip[u]];
+                kq[u] = K.key8[iq[u]];
+            }
+        }
+#pragma unroll
+        for (unsigned u = 0; u < kBatchApplyItems; ++u) {
+            if (how[u] & 1) {
+                long long c;
+                unsigned f;
+                const size_t s = pair_update_from(P, st, ip[u], iq[u], delta[u], (how[u] & 2) != 0, hk[u], hc[u],
+                                                  hf[u], &c, &f);
+                updated(s, ip[u], iq[u], c, f, (how[u] & 2) != 0, kp[u], kq[u]);
+            } else if (how[u] & 4) {
+                if (!touched[u] && (hf[u] & kPresent)) offer(Cand{hc[u], kp[u], kq[u], ce[u].x, ip[u], iq[u]});
             }
         }
     }
@@ -1693,6 +1769,11 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     if (pw0) probe_stamp(st, B.trip, 13);
     if (!scan_only && st->probe) {
         __syncthreads();
+        if (tid == 0 && (B.trip % kProbeTrip) == 0) {   // workgroups that reserved list / C space
+            unsigned long long* pr = st->probe + kProbeSlots * (size_t)(B.trip / kProbeTrip);
+            if (s_nl) atomicAdd(&pr[22], 1ull);
+            if (s_nc) atomicAdd(&pr[23], 1ull);
+        }
         if (tid == 0) probe_done(st, &st->probe_apply_done, B.trip, 15);
     }
 }
@@ -2905,6 +2986,29 @@ void MergeLoop<TokT>::report_probe() {
         if (nr)
             std::fprintf(stderr, "[bpe355 probe] select rule: p1 %.2f | head+meta %.2f | clash+k+gap %.2f | record %.2f\n",
                          r[0] / nr, r[1] / nr, r[2] / nr, r[3] / nr);
+    }
+    {   // which workgroup finishes last: merge blocks below k register members; apply's last block
+        int nm = 0, nm_reg = 0, na = 0, na_lastblk = 0;
+        std::vector<int> mlast, alast;
+        for (size_t t = 0; t + 1 < pr.size() / kProbeSlots; ++t) {
+            const unsigned long long* p = &pr[kProbeSlots * t];
+            if (p[20]) { ++nm; nm_reg += (p[20] - 1) < kMaxBatch; mlast.push_back((int)p[20] - 1); }
+            if (p[21]) { ++na; na_lastblk += (p[21] - 1) == kApplyGrid - 1; alast.push_back((int)p[21] - 1); }
+        }
+        if (nm && na) {
+            std::sort(alast.begin(), alast.end());
+            std::sort(mlast.begin(), mlast.end());
+            std::fprintf(stderr, "[bpe355 probe] last merge wg < %d (registers a member): %d of %d (median wg %d) | "
+                         "last apply wg = grid-1: %d of %d (median wg %d)\n", kMaxBatch, nm_reg, nm,
+                         mlast[mlast.size() / 2], na_lastblk, na, alast[alast.size() / 2]);
+            double wl = 0, wc = 0;
+            for (size_t t = 0; t + 1 < pr.size() / kProbeSlots; ++t) {
+                wl += (double)pr[kProbeSlots * t + 22];
+                wc += (double)pr[kProbeSlots * t + 23];
+            }
+            std::fprintf(stderr, "[bpe355 probe] apply workgroups per trip reserving list space %.1f, C space %.1f\n",
+                         wl / na, wc / na);
+        }
     }
     if (nt4)
         std::fprintf(stderr, "[bpe355 probe] %d trips: merge last-workgroup tail %.2f | last merge wg > apply start %.2f | "
