@@ -37,7 +37,11 @@ namespace bpe {
 
 namespace {
 
-constexpr int kCache2 = 1024;                     // LDS word-cache entries (2-way sets)
+// LDS word-cache entries (2-way sets).  512 entries keep the workgroup's LDS under 40 KB, so 4
+// workgroups fit a CU, with k_count2 held to 128 VGPRs (4 waves/SIMD): 59.0 vs 65.5 ms at
+// 11.9 GB for 5 % more records than 1024 entries at 3 waves/SIMD (tools/ab_count.sh; 256
+// entries at 5 waves: 55.9 ms but 12 % more records and the same count phase)
+constexpr int kCache2 = 512;
 constexpr int kEpoch2 = 4;                        // chunks between cache evictions
 constexpr unsigned kKeep2 = 2;                    // an entry stays if hit this often per epoch
 constexpr unsigned kCntBits = 19;                 // record count field
@@ -50,7 +54,7 @@ constexpr int kBins = 1 << kBinBits;
 __device__ __forceinline__ unsigned rec_bin(uint64_t h) { return (unsigned)(h >> (64 - kBinBits)); }
 
 template <bool kAligned>
-__global__ void __launch_bounds__(256) k_count2(const uint8_t* __restrict__ s, size_t lo, size_t n, size_t chunk0,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_count2(const uint8_t* __restrict__ s, size_t lo, size_t n, size_t chunk0,
                                                 size_t n_chunks, unsigned long long* __restrict__ kv,
                                                 unsigned long long* __restrict__ pos, size_t mask,
                                                 unsigned long long max_fill, unsigned long long* __restrict__ fill,

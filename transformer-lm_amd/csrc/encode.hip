@@ -98,7 +98,7 @@ __global__ void k_find_specials(const uint8_t* __restrict__ s, size_t n, EncTabl
 // slot, or kSpecialRec | special index -- at recs[span start + k]: a span of B bytes holds at
 // most B pre-tokens, so the records of all spans fit in an n-entry array with no prefix sum.
 constexpr uint32_t kSpecialRec = 0x80000000u;
-constexpr int kEncCache = 1024;
+constexpr int kEncCache = 512;    // with 4 workgroups per CU (k_enc_scan2): 36.0 vs 34.9 GB/s at 1024 / 3
 constexpr int kEncEpoch = 4;
 constexpr unsigned kEncKeep = 2;
 
@@ -323,7 +323,7 @@ struct ClipWin {   // one block's window with the bytes before window position l
 };
 
 template <bool kAligned>
-__global__ void __launch_bounds__(256, 3)
+__global__ void __launch_bounds__(256, 4)
 k_enc_scan2(const uint8_t* __restrict__ s, size_t n, size_t n_chunks, const Seg* __restrict__ segs,
             int nseg, unsigned long long* __restrict__ kv, unsigned long long* __restrict__ pos,
             size_t mask, unsigned long long max_fill, unsigned long long* __restrict__ fill,
