@@ -211,6 +211,9 @@ void bpe_dec_free(bpe_decoder* dec);
  * query (*n_out = file size).  BPE_E_IO (errno) on a missing file, a directory, or a file that
  * is not regular (the caller reads a pipe itself); BPE_E_ARG if cap is too small. */
 int bpe_read_file_device(const char* path, uint8_t* d_dst, size_t cap, size_t* n_out);
+/* n bytes of device memory -> pageable host memory h_dst (e.g. the np.uint16 array encode.py
+ * saves), through pinned staging buffers, several copier threads; waits for the device first. */
+int bpe_copy_to_host(const void* d_src, size_t n, void* h_dst);
 /* open(path, "r", encoding="utf-8").read() on device bytes: strict UTF-8 (BPE_E_UTF8) and
  * universal newlines.  d_out holds n bytes (may be d_in); *n_out = resulting length. */
 int bpe_text_prepare_device(const uint8_t* d_in, size_t n, uint8_t* d_out, size_t* n_out, void* hip_stream);

@@ -202,3 +202,15 @@ def test_encode_file_from_fifo_and_directory(tmp_path):
     assert got.tolist() == want.tolist()
     with pytest.raises(IsADirectoryError):
         encode_file(tok, tmp_path)
+
+
+def test_copy_to_host_bytes():
+    """device -> pageable host through the pinned copier threads, sizes around the 16 MB chunk"""
+    import torch
+    from bpe_amd import _lib
+    L = _lib.lib()
+    for size in (1, 4097, (16 << 20) + 3, 2 * (16 << 20) + 77):
+        src = torch.randint(0, 256, (size,), dtype=torch.uint8, device="cuda")
+        dst = np.zeros(size, dtype=np.uint8)
+        _lib.check(L.bpe_copy_to_host(_device(src), size, dst.ctypes.data))
+        assert np.array_equal(dst, src.cpu().numpy())

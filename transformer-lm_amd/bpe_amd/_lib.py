@@ -107,6 +107,7 @@ _SIGS = [
     ("bpe_dec_decode_device", ctypes.c_int, [_P, _P, _SZ, _P, _SZ, ctypes.POINTER(_SZ), _P]),
     ("bpe_dec_free", None, [_P]),
     ("bpe_read_file_device", ctypes.c_int, [ctypes.c_char_p, _P, _SZ, ctypes.POINTER(_SZ)]),
+    ("bpe_copy_to_host", ctypes.c_int, [_P, _SZ, _P]),
     ("bpe_text_prepare_device", ctypes.c_int, [_P, _SZ, _P, ctypes.POINTER(_SZ), _P]),
     ("bpe_utf8_chunk_starts_device", ctypes.c_int, [_P, _SZ, _SZ, _P, _SZ, ctypes.POINTER(_SZ), _P]),
     ("bpe_ids_to_u16_device", ctypes.c_int, [_P, _SZ, _P, _P]),

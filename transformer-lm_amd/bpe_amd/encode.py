@@ -71,8 +71,10 @@ def encode_device_u16(tokenizer: Tokenizer, raw, chars_per_piece: int = CHARS_PE
     _lib.check(L.bpe_ids_to_u16_device(ctypes.c_void_p(ids.data_ptr()), k, ctypes.c_void_p(out16.data_ptr()),
                                        None), "uint16 ids")
     del ids
-    torch.cuda.synchronize()
-    return out16[:k].cpu().numpy().view(np.uint16)
+    host = np.empty(k, dtype=np.uint16)
+    if k:
+        _lib.check(L.bpe_copy_to_host(ctypes.c_void_p(out16.data_ptr()), 2 * k, host.ctypes.data), "copy")
+    return host
 
 
 def encode_bytes_u16(tokenizer: Tokenizer, data: bytes, chars_per_piece: int = CHARS_PER_PIECE) -> np.ndarray:

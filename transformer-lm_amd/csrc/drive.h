@@ -35,6 +35,8 @@ int io_threads();
 std::vector<size_t> slab_cuts(const Source& src, int g);
 // src[off, off + len) -> d_dst on `device`, through pinned staging, `threads` readers
 void stage_to_device(const Source& src, size_t off, size_t len, uint8_t* d_dst, int device, int threads);
+// d_src[0, len) on `device` -> host memory h_dst (pageable), through pinned staging, `threads` copiers
+void device_to_host(const uint8_t* d_src, size_t len, uint8_t* h_dst, int device, int threads);
 // src[off, off + len) -> d_dst, validated and counted segment by segment as it arrives
 // (false: the text holds a \r, so the caller must apply universal newlines and count it whole)
 bool load_and_count(const Source& src, size_t off, size_t len, uint8_t* d_dst, int device, int threads,

@@ -259,6 +259,65 @@ void stage_to_device(const Source& src, size_t off, size_t len, uint8_t* d_dst, 
         if (e) std::rethrow_exception(e);
 }
 
+// ------------------------------------------------------------------ HBM -> host memory
+// The reverse of stage_to_device: each thread DMAs a chunk into its pinned buffer, then copies it
+// to the destination while its other buffer's DMA runs (a pageable destination is faulted in by
+// many threads at once instead of by one copy).
+void device_to_host(const uint8_t* d_src, size_t len, uint8_t* h_dst, int device, int threads) {
+    if (len == 0) return;
+    const size_t chunks = (len + kStageChunk - 1) / kStageChunk;
+    const int t_n = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads, chunks));
+    std::atomic<size_t> next{0};
+    std::vector<std::exception_ptr> errs(t_n);
+    auto work = [&](int t) {
+        hipStream_t s = nullptr;
+        void* buf[2] = {nullptr, nullptr};
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        size_t pend[2] = {~(size_t)0, ~(size_t)0};   // chunk whose DMA into buf[k] is in flight
+        auto drain = [&](int k) {
+            if (pend[k] == ~(size_t)0) return;
+            BPE_HIP(hipEventSynchronize(ev[k]));
+            const size_t lo = pend[k] * kStageChunk;
+            std::memcpy(h_dst + lo, buf[k], std::min(kStageChunk, len - lo));
+            pend[k] = ~(size_t)0;
+        };
+        try {
+            BPE_HIP(hipSetDevice(device));
+            BPE_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+            for (int k = 0; k < 2; ++k) {
+                buf[k] = pool().get();
+                BPE_HIP(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
+            }
+            for (int k = 0;; k ^= 1) {
+                drain(k);
+                const size_t i = next.fetch_add(1);
+                if (i >= chunks) break;
+                const size_t lo = i * kStageChunk, n = std::min(kStageChunk, len - lo);
+                BPE_HIP(hipMemcpyAsync(buf[k], d_src + lo, n, hipMemcpyDeviceToHost, s));
+                BPE_HIP(hipEventRecord(ev[k], s));
+                pend[k] = i;
+            }
+            drain(0);
+            drain(1);
+        } catch (...) {
+            errs[t] = std::current_exception();
+            next.store(chunks);
+            if (s) (void)hipStreamSynchronize(s);
+        }
+        for (int k = 0; k < 2; ++k) {
+            if (ev[k]) (void)hipEventDestroy(ev[k]);
+            if (buf[k]) pool().put(buf[k]);
+        }
+        if (s) (void)hipStreamDestroy(s);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < t_n; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    for (auto& e : errs)
+        if (e) std::rethrow_exception(e);
+}
+
 // ------------------------------------------------------------------ file -> HBM, counted on arrival
 // The corpus is cut into segments at safe split points; a segment is validated and counted
 // (into one word table) as soon as its chunks are in HBM: the stream waits on the chunks' copy

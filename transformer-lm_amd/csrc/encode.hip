@@ -333,7 +333,7 @@ k_enc_scan2(const uint8_t* __restrict__ s, size_t n, size_t n_chunks, const Seg*
     __shared__ unsigned long long c_key[kEncCache];
     __shared__ uint64_t c_lo[kEncCache], c_hi[kEncCache];
     __shared__ uint32_t c_slot[kEncCache];
-    __shared__ uint16_t c_hit[kEncCache];   // hits this epoch (3 workgroups per CU fit the LDS)
+    __shared__ uint16_t c_hit[kEncCache];   // hits this epoch (4 workgroups per CU fit the LDS)
     __shared__ Seg s_seg[kSegLds];
     __shared__ int s_seg0, s_segn;   // first segment of the chunk window and how many are in LDS (-1: too many)
     __shared__ unsigned long long s_red[4];

@@ -92,6 +92,17 @@ int bpe_read_file_device(const char* path, uint8_t* d_dst, size_t cap, size_t* n
     });
 }
 
+int bpe_copy_to_host(const void* d_src, size_t n, void* h_dst) {
+    return bpe::guarded_io([&] {
+        BPE_REQUIRE(n == 0 || (d_src && h_dst), BPE_E_ARG, "NULL argument");
+        int dev = 0;
+        BPE_HIP(hipGetDevice(&dev));
+        BPE_HIP(hipDeviceSynchronize());   // the caller's writes (any stream) are done
+        bpe::device_to_host(static_cast<const uint8_t*>(d_src), n, static_cast<uint8_t*>(h_dst), dev,
+                            bpe::io_threads());
+    });
+}
+
 int bpe_text_prepare_device(const uint8_t* d_in, size_t n, uint8_t* d_out, size_t* n_out, void* hip_stream) {
     return bpe::guarded_io([&] {
         BPE_REQUIRE(n_out && (n == 0 || (d_in && d_out)), BPE_E_ARG, "NULL argument");
