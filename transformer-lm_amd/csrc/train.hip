@@ -110,7 +110,7 @@ struct ToksDev {
     unsigned long long* hash;  // polynomial hash of the bytes
     unsigned long long* pw;    // P^len
     unsigned long long* key8;  // first 8 bytes, big-endian, zero padded
-    uint32_t* map;             // hash -> id + 1
+    unsigned long long* map;   // token dedupe map: (hash >> 32) << 32 | id + 1 (map_entry)
     uint32_t map_mask;
 };
 
@@ -272,6 +272,24 @@ __device__ bool equals_concat(const ToksDev& K, unsigned x, unsigned a, unsigned
     for (unsigned i = 0; i < ln; ++i)
         if (px[i] != concat_byte(K, a, la, b, i)) return false;
     return true;
+}
+
+// The token dedupe map (vocab.py:29: a merge whose bytes exist reuses that id): open addressing
+// on mix64(hash), entries tagged with the hash's high half, so a probe that meets another token
+// moves on without loading that token's hash
+__device__ __forceinline__ unsigned long long map_entry(unsigned long long h, unsigned id) {
+    return (h & 0xffffffff00000000ull) | (unsigned long long)(id + 1);
+}
+// the id of the token whose bytes are a + b (hash h, ln bytes), or ~0
+__device__ __forceinline__ unsigned map_find(const ToksDev& K, unsigned long long h, unsigned ln, unsigned a,
+                                             unsigned b) {
+    unsigned s = (unsigned)mix64(h) & K.map_mask;
+    for (unsigned long long e = K.map[s]; e != 0; s = (s + 1) & K.map_mask, e = K.map[s]) {
+        if ((e >> 32) != (h >> 32)) continue;
+        const unsigned id = (unsigned)e - 1;
+        if (K.hash[id] == h && K.len[id] == ln && equals_concat(K, id, a, b)) return id;
+    }
+    return ~0u;
 }
 
 // ------------------------------------------------------------------ word rewrite
@@ -505,16 +523,8 @@ __global__ void __launch_bounds__(256) k_merge(RoundState* __restrict__ st,
         if (tid == 0) {
             const unsigned a = sb.a, b = sb.b, ln = sb.ln, ntok = (unsigned)sb.ntok;
             const unsigned long long h = sb.hash;
-            unsigned s = (unsigned)mix64(h) & K.map_mask;
-            unsigned m = K.map[s];
-            unsigned nw = ntok;
-            for (; m != 0; s = (s + 1) & K.map_mask, m = K.map[s]) {
-                const unsigned id = m - 1;
-                if (K.hash[id] == h && K.len[id] == ln && equals_concat(K, id, a, b)) {
-                    nw = id;
-                    break;
-                }
-            }
+            const unsigned old = map_find(K, h, ln, a, b);
+            const unsigned nw = old != ~0u ? old : ntok;
             sb.nw = nw;
             sb.isnew = nw == ntok;
             if (!sb.isnew) sb.cov_len = kNoAnc;   // dedupe: uncovered until the next build
@@ -813,9 +823,10 @@ __global__ void __launch_bounds__(kApplyThreads) k_apply_argmax(RoundState* __re
             // k_merge reads these, in the next launch)
             const unsigned nw = st->cur_new;
             if (st->new_is_new) {
-                unsigned s = (unsigned)mix64(K.hash[nw]) & K.map_mask;
+                const unsigned long long h = K.hash[nw];
+                unsigned s = (unsigned)mix64(h) & K.map_mask;
                 while (K.map[s] != 0) s = (s + 1) & K.map_mask;
-                K.map[s] = nw + 1;
+                K.map[s] = map_entry(h, nw);
             }
             st->round = st->cur_round + 1;
             st->ntok = st->cur_ntok;
@@ -972,12 +983,7 @@ __device__ __forceinline__ void cand_meta(const Cand& c, const ToksDev& K, const
     m.za = X.len[a]; m.zb = X.len[b]; m.ba = X.beg[a]; m.bb = X.beg[b];
     const unsigned long long h = m.ha * m.pb + m.hb;
     const unsigned ln = m.la + m.lb;
-    unsigned s = (unsigned)mix64(h) & K.map_mask;
-    old = ~0u;
-    for (unsigned mm = K.map[s]; mm != 0; s = (s + 1) & K.map_mask, mm = K.map[s]) {
-        const unsigned id = mm - 1;
-        if (K.hash[id] == h && K.len[id] == ln && equals_concat(K, id, a, b)) { old = id; break; }
-    }
+    old = map_find(K, h, ln, a, b);
 }
 
 // One workgroup: the batch of this trip.  Waves 0-7 reduce the apply's per-workgroup partials
@@ -1754,8 +1760,9 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     if (pw0) probe_stamp(st, B.trip, 12);
     if (blockIdx.x == gridDim.x - 1 && tid < k && B.m[tid].isnew) {   // the new tokens enter the dedupe map
         const unsigned nw = B.m[tid].nw;
-        unsigned s = (unsigned)mix64(B.m[tid].hash) & K.map_mask;
-        while (atomicCAS(&K.map[s], 0u, nw + 1) != 0u) s = (s + 1) & K.map_mask;
+        const unsigned long long h = B.m[tid].hash;
+        unsigned s = (unsigned)mix64(h) & K.map_mask;
+        while (atomicCAS(&K.map[s], 0ull, map_entry(h, nw)) != 0ull) s = (s + 1) & K.map_mask;
     }
     if (blockIdx.x == 0 && tid == 0) {
         st->nparts = gridDim.x;
@@ -1876,9 +1883,9 @@ __global__ void k_init_tokens(ToksDev K) {
     __syncthreads();
     if (i == 0) {
         for (unsigned t = 0; t < 256; ++t) {
-            unsigned s = (unsigned)mix64(t) & K.map_mask;
+            unsigned s = (unsigned)mix64(t) & K.map_mask;   // a byte token's hash is its byte
             while (K.map[s] != 0) s = (s + 1) & K.map_mask;
-            K.map[s] = t + 1;
+            K.map[s] = map_entry(t, t);
         }
     }
 }
@@ -2278,7 +2285,8 @@ class MergeLoop {
     // tokens
     unsigned tok_cap_ = 0;
     DevBuf<uint8_t> pool_;
-    DevBuf<uint32_t> toff_, tlen_, tmap_;
+    DevBuf<uint32_t> toff_, tlen_;
+    DevBuf<unsigned long long> tmap_;
     DevBuf<unsigned long long> thash_, tpw_, tkey8_;
     DevBuf<unsigned long long> LR_;
     DevBuf<Partial> part_;
