@@ -662,9 +662,11 @@ __device__ __forceinline__ size_t pair_update(const PairsDev& P, RoundState* st,
 
 // pair_update with the home slot's key, count and flags already loaded (k0, c0, f0): the
 // caller issues several keys' home-slot loads before finishing any of them
+// Inserted keys are counted in *n_ins (the caller adds them to st->pair_used once per workgroup:
+// one same-address atomic per insert serialises thousands of them at the end of a trip).
 __device__ __forceinline__ size_t pair_update_from(const PairsDev& P, RoundState* st, unsigned p, unsigned q,
                                                    long long delta, bool inc, unsigned long long k0, long long c0,
-                                                   unsigned f0, long long* c_out, unsigned* f_out) {
+                                                   unsigned f0, long long* c_out, unsigned* f_out, unsigned& n_ins) {
     const unsigned long long key = pair_key(p, q);
     size_t s = mix64(key) & P.mask;
     long long c = c0;
@@ -678,7 +680,7 @@ __device__ __forceinline__ size_t pair_update_from(const PairsDev& P, RoundState
             if (k == 0) {
                 k = atomicCAS(&P.key[s], 0ULL, key);
                 if (k == 0) {
-                    atomicAdd(&st->pair_used, 1ULL);
+                    ++n_ins;
                     ins = true;
                     break;
                 }
@@ -1535,7 +1537,7 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     __shared__ Cand s_wave[kApplyBatchThreads / 64];
     __shared__ Partial s_lst[kListCap];
     __shared__ uint4 s_cadd[kApplyCLds];
-    __shared__ unsigned s_nl, s_nc, s_lbase, s_cbase;
+    __shared__ unsigned s_nl, s_nc, s_lbase, s_cbase, s_ins;
     const Batch& B = *bt;
     if (!scan_only && B.stop) return;   // halted: part[] keeps the lists the next select reads
     const int k = scan_only ? 0 : B.k;
@@ -1567,6 +1569,7 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
             s_ns = __popcll(km);
             s_nl = 0;
             s_nc = 0;
+            s_ins = 0;
         }
     }
     __syncthreads();
@@ -1597,6 +1600,7 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     auto in_S = [&](unsigned x) { return find_S(x) >= 0; };
     const long long T2 = bs->T2 < T ? T : bs->T2;
     Cand best = cand_none();   // this thread's best candidate (exact argmax)
+    unsigned n_ins = 0;        // pair-table keys this thread inserted
     // a candidate for the list (>= T2) and for this thread's best
     auto offer = [&](const Cand& c) {
         if (cand_better(c, best, K.pool, K.off, K.len)) best = c;
@@ -1724,7 +1728,7 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
                 long long c;
                 unsigned f;
                 const size_t s = pair_update_from(P, st, ip[u], iq[u], delta[u], (how[u] & 2) != 0, hk[u], hc[u],
-                                                  hf[u], &c, &f);
+                                                  hf[u], &c, &f, n_ins);
                 updated(s, ip[u], iq[u], c, f, (how[u] & 2) != 0, kp[u], kq[u]);
             } else if (how[u] & 4) {
                 if (!touched[u] && (hf[u] & kPresent)) offer(Cand{hc[u], kp[u], kq[u], ce[u].x, ip[u], iq[u]});
@@ -1736,6 +1740,8 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
         const Cand oc = shfl_xor_cand(best, o);
         if (cand_better(oc, best, K.pool, K.off, K.len)) best = oc;
     }
+    n_ins = wave_sum(n_ins);
+    if ((tid & 63) == 0 && n_ins) atomicAdd(&s_ins, n_ins);
     if ((tid & 63) == 0) s_wave[tid >> 6] = best;
     __syncthreads();
     if (tid == 0) {
@@ -1746,6 +1752,7 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
         const unsigned nl = s_nl, nc = min(s_nc, kApplyCLds);
         s_lbase = nl ? atomicAdd(&bs->list_n, nl) : 0u;
         s_cbase = nc ? atomicAdd(&st->nC, nc) : 0u;
+        if (s_ins) atomicAdd(&st->pair_used, (unsigned long long)s_ins);   // read by the next select
     }
     __syncthreads();
     {
