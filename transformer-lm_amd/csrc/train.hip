@@ -1379,6 +1379,16 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
     const Batch& B = *bt;
     if (B.stop) return;
     const int k = B.k;
+    // the previous trip's cells (the other parity, read by its apply) are cleared here, spread
+    // over the whole grid: workgroups without words do their share at once, the others after
+    // their flush, so the stores never wait in front of a rewrite's loads
+    auto clear_prev = [&]() {
+        unsigned long long* LRo = LRbase + (size_t)((B.trip + 1) & 1) * lr_parity;
+        const unsigned nprev = 2 * (unsigned)B.ntok;
+        const unsigned S = gridDim.x * blockDim.x;
+        for (unsigned q = blockIdx.x * blockDim.x + tid; q < (unsigned)B.prev_k * nprev; q += S)
+            LRo[(size_t)(q / nprev) * lr_member + q % nprev] = 0;
+    };
     {   // list mode: workgroups past the listed words (and past the members' registrations) have
         // nothing to do -- skip their LDS clear, barriers and flush
         const unsigned bid = blockIdx.x;
@@ -1386,6 +1396,7 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
             const bool lists = k > 1 ? !B.full_scan : B.m[0].use_list != 0;
             const unsigned total = k > 1 ? B.list_pre[k] : B.m[0].list_len;
             if (lists && bid * blockDim.x >= total) {
+                clear_prev();
                 if (tid == 0) probe_done(st, &st->probe_merge_done, B.trip, 14);
                 return;
             }
@@ -1503,6 +1514,7 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
         if (v) atomicAdd(&LRt[(size_t)(q / (2 * kLdsB)) * lr_member + q % (2 * kLdsB)], v);
     }
     if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 8);
+    clear_prev();
     if (st->probe) {
         __syncthreads();
         if (tid == 0) probe_done(st, &st->probe_merge_done, B.trip, 14);
@@ -1576,7 +1588,6 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     const int ns = s_ns;
     const long long T = st->T;
     const unsigned long long* LRc = LRbase + (size_t)(B.trip & 1) * lr_parity;
-    unsigned long long* LRo = LRbase + (size_t)((B.trip + 1) & 1) * lr_parity;
     if (!scan_only) ntb = min(ntb, (unsigned)B.ntok + B.n_fresh);   // token ids after this trip
     const unsigned per_member = 4 * ntb;
     const unsigned n_cell = (unsigned)k * per_member;
@@ -1585,11 +1596,7 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     const unsigned n_items = n_cell + n_sp + nC0;
     const unsigned g = blockIdx.x * blockDim.x + tid;
     const unsigned S = gridDim.x * blockDim.x;
-    if (!scan_only) {   // clear the previous trip's cells (its prev_k members; ids below this trip's start)
-        const unsigned nprev = 2 * (unsigned)B.ntok;
-        for (unsigned q = g; q < (unsigned)B.prev_k * nprev; q += S)
-            LRo[(size_t)(q / nprev) * lr_member + q % nprev] = 0;
-    }
+    // (the previous trip's cells were cleared by this trip's merge)
     if (pw0) probe_stamp(st, B.trip, 10);
     auto find_S = [&](unsigned x) -> int {   // x's entry in S, or -1
         if (!((s_filt[(x >> 5) % kSFilterWords] >> (x & 31)) & 1u)) return -1;
