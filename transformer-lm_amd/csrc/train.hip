@@ -882,7 +882,10 @@ __global__ void __launch_bounds__(256) k_argmax(RoundState* __restrict__ st, Pai
 // The rewrite applies the members in order to each word (the deltas of member j see the word
 // after members < j, as the reference's sequence of rounds does), so counts, present keys and
 // words after the trip equal the state after k rounds.
-constexpr int kMaxBatch = 16;
+#ifndef BPE355_MAX_BATCH
+#define BPE355_MAX_BATCH 16
+#endif
+constexpr int kMaxBatch = BPE355_MAX_BATCH;   // members per trip (3 * kMaxBatch tokens fit one wave)
 constexpr int kTopM = kMaxBatch + 1;
 constexpr unsigned kLdsB = 128;          // LDS-summed cells per member (ids below kLdsB)
 
