@@ -4,7 +4,7 @@
 set -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG; mkdir -p $OUT
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
   for v in "$@"; do
     BPE355_LIB=build/variants/$v/libbpe355.so timeout -k 10 200 python -u bench.py --steps 2 --warmup 1 --no-encode --no-cpu-baseline --no-timing > $OUT/$v.$rep.log 2>&1 || { echo "$v failed"; tail -5 $OUT/$v.$rep.log; exit 1; }
     python - $OUT/$v.$rep.log $v <<'PY'

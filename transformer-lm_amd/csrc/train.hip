@@ -1534,7 +1534,10 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
 // Every present key >= T among them is a candidate; each workgroup writes its exact top-kTopM
 // (sorted) to part[blockIdx.x * kTopM ...] and k_select merges the lists.  scan_only: the C
 // entries alone (after a rebuild of C).
-constexpr unsigned kBatchApplyItems = 4;
+#ifndef BPE355_APPLY_ITEMS
+#define BPE355_APPLY_ITEMS 2
+#endif
+constexpr unsigned kBatchApplyItems = BPE355_APPLY_ITEMS;   // items per thread per pass of k_apply_batch
 constexpr unsigned kApplyBatchThreads = 256;
 constexpr unsigned kApplyCLds = 256;
 constexpr unsigned kSFilterWords = 128;   // C admissions a workgroup stages in LDS (more: direct appends)
