@@ -241,6 +241,13 @@ def main():
                              if avg["merge_kernel_launches"] else None),
         "k_merge_batch_bytes_per_launch": (round(avg["merge_kernel_bytes"] / avg["merge_kernel_launches"])
                                            if avg["merge_kernel_launches"] else None),
+        # the rewrite's algorithmic bytes over its mean launch: far below HBM, the loop is
+        # latency-bound (merge-loop probe)
+        "k_merge_batch_GBps": (round(avg["merge_kernel_bytes"] / (avg["merge_kernel_ms"] * 1e6), 1)
+                               if avg["merge_kernel_launches"] and avg["merge_kernel_ms"] else None),
+        # a trip is three dependent launches; an empty kernel boundary costs 1.4-2.6 us on this part
+        # (tools/microbench/launch_floor.hip), so 3 x 1.4 us is the floor of a trip that did nothing
+        "launch_floor_us_per_trip": 4.2,
     }
     # the roofline line: k_count2 over the HBM-resident corpus (one launch per step, the launches
     # rocprofv3 --no-file profiles see); without that run, the file path's per-segment launches
