@@ -55,6 +55,12 @@ typedef struct bpe_tokenizer bpe_tokenizer;
 typedef struct bpe_comm bpe_comm;
 
 int bpe_abi_version(void);
+/* The HIP runtime this process bound the library to.  The library is compiled against the ROCm
+ * headers of the build image (HIP_VERSION, *compiled); the libamdhip64.so.7 that serves it is
+ * whichever copy of that soname the process loaded first -- inside a PyTorch-ROCm process,
+ * torch's bundled one (*runtime, hipRuntimeGetVersion; runtime_path: the file, via dladdr).
+ * The Python binding refuses a runtime of a different major version. */
+int bpe_runtime_info(int* compiled_hip_version, int* runtime_hip_version, char* runtime_path, size_t cap);
 const char* bpe_last_error(void);
 int bpe_last_errno(void);
 /* number of visible gfx950 devices (0 if none); never fails */

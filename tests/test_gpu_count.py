@@ -78,6 +78,20 @@ def test_train_records_vs_oracle(knob):
     assert got == oracle.train_raw(data, 6000, EOT)
 
 
+@pytest.mark.parametrize("how", [("BPE355_REC_POOL_FAIL", "1"), ("BPE355_REC_POOL_FIT", "1000")])
+def test_pool_does_not_fit_falls_back(knob, how):
+    """the record pool is capped by free device memory; when it cannot be had (its
+    allocation fails, or the memory left holds less than a page per counting workgroup) the
+    counter sends every miss to the global table -- same words, no records"""
+    knob("BPE355_REC_POOL", "1e8")
+    knob(*how)
+    data = _synth(37, 0, 8 << 20)
+    got = bpe_amd.train_bpe_bytes(data, 3000, EOT)
+    assert last_train_stats()["n_count_records"] == 0
+    assert got == oracle.train_raw(data, 3000, EOT)
+    assert _device_word_counts(data, EOT) == _want_words(data, EOT)
+
+
 def test_file_segments_records(knob, tmp_path):
     knob("BPE355_REC_POOL", "1e8")
     knob("BPE355_SEG_MB", 4)

@@ -60,6 +60,8 @@ _U8P = ctypes.c_char_p
 _SZ = ctypes.c_size_t
 _SIGS = [
     ("bpe_abi_version", ctypes.c_int, []),
+    ("bpe_runtime_info", ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                        ctypes.c_char_p, _SZ]),
     ("bpe_last_error", ctypes.c_char_p, []),
     ("bpe_last_errno", ctypes.c_int, []),
     ("bpe_device_count", ctypes.c_int, []),
@@ -140,8 +142,27 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        _check_runtime(L)
         _lib = L
     return _lib
+
+
+RUNTIME = {}   # the HIP runtime this process bound the library to (bpe_runtime_info)
+
+
+def _check_runtime(L):
+    """The library is compiled against the image's ROCm headers; the libamdhip64.so.7 serving it
+    is the first copy of that soname the process loaded (torch's bundled runtime when torch is
+    imported first).  HIP keeps its C ABI within a major version, so a different minor version
+    is recorded (bench line) and a different major version is refused."""
+    comp, run = ctypes.c_int(0), ctypes.c_int(0)
+    path = ctypes.create_string_buffer(4096)
+    rc = L.bpe_runtime_info(ctypes.byref(comp), ctypes.byref(run), path, len(path))
+    RUNTIME.update(compiled=comp.value, runtime=run.value if rc == BPE_OK else None,
+                   path=path.value.decode("utf-8", "replace"))
+    if rc == BPE_OK and run.value // 10_000_000 != comp.value // 10_000_000:
+        raise LibraryMissing(f"libbpe355 was compiled for HIP {comp.value} but the process bound HIP "
+                             f"runtime {run.value} ({RUNTIME['path']}): major versions differ")
 
 
 def check(rc: int, what: str = ""):

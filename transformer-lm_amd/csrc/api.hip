@@ -1,4 +1,7 @@
 // C ABI of libbpe355 (include/bpe355.h): argument checking, error codes, result objects.
+#include <dlfcn.h>
+#include <hip/hip_version.h>
+
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -160,6 +163,20 @@ int train_common(const uint8_t* d_data, size_t n, int vocab_size, const char* co
 extern "C" {
 
 int bpe_abi_version(void) { return BPE355_ABI_VERSION; }
+
+int bpe_runtime_info(int* compiled_hip_version, int* runtime_hip_version, char* runtime_path, size_t cap) {
+    if (compiled_hip_version) *compiled_hip_version = HIP_VERSION;
+    int rv = 0;
+    const hipError_t e = hipRuntimeGetVersion(&rv);
+    if (runtime_hip_version) *runtime_hip_version = e == hipSuccess ? rv : 0;
+    if (runtime_path && cap) {
+        runtime_path[0] = '\0';
+        Dl_info di{};
+        if (dladdr(reinterpret_cast<void*>(&hipRuntimeGetVersion), &di) && di.dli_fname)
+            std::snprintf(runtime_path, cap, "%s", di.dli_fname);
+    }
+    return e == hipSuccess ? BPE_OK : BPE_E_HIP;
+}
 const char* bpe_last_error(void) { return bpe::g_err.c_str(); }
 int bpe_last_errno(void) { return bpe::g_errno; }
 void bpe_set_timing(int enable) { bpe::g_timing = enable != 0; }

@@ -50,8 +50,16 @@ struct DevBuf {
     ~DevBuf() { release(); }
     void alloc(size_t count) {
         release();
+        if (!count) return;
+        const hipError_t e = hipMalloc(&p, count * sizeof(T));
+        if (e == hipErrorOutOfMemory) {
+            (void)hipGetLastError();   // clear it: a later launch check must not see this failure
+            p = nullptr;
+            throw ::bpe::Error{BPE_E_NOMEM, "device allocation of " + std::to_string(count * sizeof(T)) +
+                                                " bytes failed (out of memory)"};
+        }
+        BPE_HIP(e);
         n = count;
-        if (count) BPE_HIP(hipMalloc(&p, count * sizeof(T)));
     }
     // grow-only: keep the buffer when it already holds count elements (n is then the capacity)
     void reserve(size_t count) {

@@ -79,6 +79,8 @@ struct InProcShared {
     int arrived = 0;
     uint64_t gen = 0;
     std::vector<int64_t> acc, result;
+    std::vector<uint8_t> gather;   // all-gather: rank r's segment at r * bytes
+    int g_entered = 0, g_readers = 0;
 };
 
 struct InProcComm final : Comm {
@@ -112,6 +114,39 @@ struct InProcComm final : Comm {
         }
         BPE_HIP(hipMemcpyAsync(d_buf, h.data(), count * 8, hipMemcpyHostToDevice, stream));
         BPE_HIP(hipStreamSynchronize(stream));
+    }
+    // ncclAllGather's contract: every rank copies its segment into one shared host buffer, and
+    // after the last rank arrives each one copies the whole buffer back (no zero-padded sum)
+    void allgather_bytes(const void* d_send, size_t bytes, void* d_recv, hipStream_t stream) override {
+        if (bytes == 0) return;
+        std::unique_lock<std::mutex> lk(sh->m);
+        // a rank done with the previous gather may not reset the buffer others still read
+        sh->cv.wait(lk, [&] { return sh->g_readers == 0; });
+        const uint64_t g = sh->gen;
+        if (sh->g_entered++ == 0) sh->gather.assign((size_t)nranks * bytes, 0);
+        BPE_REQUIRE(sh->gather.size() == (size_t)nranks * bytes, BPE_E_RCCL,
+                    "in-process all-gather: ranks disagree on the size");
+        uint8_t* mine = sh->gather.data() + (size_t)rank * bytes;
+        lk.unlock();   // the copies of the ranks' own segments run concurrently
+        BPE_HIP(hipMemcpyAsync(mine, d_send, bytes, hipMemcpyDeviceToHost, stream));
+        BPE_HIP(hipStreamSynchronize(stream));
+        lk.lock();
+        if (++sh->arrived == nranks) {
+            sh->arrived = 0;
+            sh->g_entered = 0;
+            sh->g_readers = nranks;
+            ++sh->gen;
+            sh->cv.notify_all();
+        } else {
+            sh->cv.wait(lk, [&] { return sh->gen != g; });
+        }
+        const uint8_t* all = sh->gather.data();
+        lk.unlock();
+        BPE_HIP(hipMemcpyAsync(d_recv, all, (size_t)nranks * bytes, hipMemcpyHostToDevice, stream));
+        BPE_HIP(hipStreamSynchronize(stream));
+        lk.lock();
+        --sh->g_readers;
+        sh->cv.notify_all();
     }
 };
 

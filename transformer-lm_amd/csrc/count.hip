@@ -695,10 +695,40 @@ std::unique_ptr<Arrays3> scratch_take(size_t cap) {
     x = std::make_unique<Arrays3>();
     x->dev = dev;
     x->cap = cap;
-    x->a.alloc(cap);
-    x->b.alloc(cap);
-    x->c.alloc(cap);
+    try {
+        x->a.alloc(cap);
+        x->b.alloc(cap);
+        x->c.alloc(cap);
+    } catch (const Error& e) {
+        if (e.code != BPE_E_NOMEM) throw;
+        // the cache holds this device's other free sets: give them back and try once more
+        x->a.release(); x->b.release(); x->c.release();
+        scratch_release(dev);
+        x->a.alloc(cap);
+        x->b.alloc(cap);
+        x->c.alloc(cap);
+    }
     return x;
+}
+
+size_t scratch_cached_bytes(int dev) {
+    std::lock_guard<std::mutex> g(scratch().m);
+    size_t b = 0;
+    for (auto& f : scratch().free_)
+        if (f->dev == dev) b += 3 * f->cap * sizeof(uint64_t);
+    return b;
+}
+
+void scratch_release(int dev) {
+    std::vector<std::unique_ptr<Arrays3>> drop;
+    {
+        std::lock_guard<std::mutex> g(scratch().m);
+        auto& f = scratch().free_;
+        for (size_t i = 0; i < f.size();)
+            if (f[i]->dev == dev) { drop.push_back(std::move(f[i])); f.erase(f.begin() + i); }
+            else ++i;
+    }
+    drop.clear();   // hipFree outside the lock
 }
 
 void scratch_give(std::unique_ptr<Arrays3> x) {
@@ -717,8 +747,28 @@ void RecPoolOwner::init(size_t n_bytes, unsigned grid, hipStream_t s) {
     // the remaining misses go to the global table (correct, slower)
     size_t want = std::max<size_t>(n_bytes / 10, (size_t)grid * kPageRecs);
     if (const char* e = std::getenv("BPE355_REC_POOL")) want = (size_t)std::atof(e);   // test knob: records
+    // The pool and the aggregation's level-1 copy take 48 B per record (two sets of three u64
+    // arrays).  Cap them by the device memory that is free (plus the cache's free sets, which
+    // scratch_take reuses or hands back), keeping a reserve for the word table and the merge
+    // loop; a pool that cannot hold one page per counting workgroup is not worth having: the
+    // counter then sends its misses to the global table (R.on = 0: correct, slower).
+    int dev = 0;
+    BPE_HIP(hipGetDevice(&dev));
+    size_t free_b = 0, total_b = 0;
+    BPE_HIP(hipMemGetInfo(&free_b, &total_b));
+    const size_t avail = free_b + scratch_cached_bytes(dev);
+    const size_t reserve = std::max<size_t>(total_b / 16, n_bytes / 2);
+    size_t fit = avail > reserve ? (avail - reserve) / (6 * sizeof(uint64_t)) : 0;
+    if (const char* e = std::getenv("BPE355_REC_POOL_FIT")) fit = (size_t)std::atof(e);   // test knob
+    if (fit < want) {
+        if (fit < (size_t)grid * kPageRecs / 4)
+            throw Error{BPE_E_NOMEM, "record pool: " + std::to_string(avail) + " bytes of device memory free"};
+        want = fit;
+    }
     max_pages = (unsigned)std::max<size_t>(1, std::min<size_t>((want + kPageRecs - 1) / kPageRecs, 1u << 30));
     const size_t cap = (size_t)max_pages * kPageRecs;
+    if (std::getenv("BPE355_REC_POOL_FAIL"))   // test knob: the pool's allocation fails
+        throw Error{BPE_E_NOMEM, "record pool allocation failed (BPE355_REC_POOL_FAIL)"};
     rec = scratch_take(cap);
     page_used.alloc(max_pages);
     page_ch.alloc((size_t)max_pages * kCoarse);

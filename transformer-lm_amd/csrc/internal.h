@@ -55,6 +55,7 @@ struct CountPass {
     WordCounts wc;
     bool v2 = true;                       // the byte-parallel counter (count.hip); BPE355_COUNT_V1: the serial one
     std::unique_ptr<RecPoolOwner> rec;    // its record pool (large texts)
+    bool pool_fallback = false;           // the pool did not fit in device memory: misses go to the table
     unsigned grid2 = 0;
     DevBuf<unsigned> status;
     DevBuf<unsigned long long> ntok, fill;

@@ -487,13 +487,22 @@ void CountPass::begin(const uint8_t* d_text, size_t n, size_t cap, hipStream_t s
     static const bool v1 = std::getenv("BPE355_COUNT_V1") != nullptr;   // A/B knob: the serial counter
     v2 = !v1;
     rec.reset();
+    pool_fallback = false;
     if (v2) {
         grid2 = count2_grid((n + kChunk - 1) / kChunk);
         // misses spill as records (aggregated in LDS by bin afterwards) when the text is large
         // enough for the per-workgroup pages to pay off; BPE355_REC_POOL forces it (tests)
         if (n >= (size_t(256) << 20) || std::getenv("BPE355_REC_POOL")) {
             rec = std::make_unique<RecPoolOwner>();
-            rec->init(n, grid2, s);
+            try {
+                rec->init(n, grid2, s);
+            } catch (const Error& e) {
+                if (e.code != BPE_E_NOMEM) throw;
+                // no room for the pool: every miss goes to the global table instead (same counts)
+                BPE_HIP(hipStreamSynchronize(s));
+                rec.reset();
+                pool_fallback = true;
+            }
         }
     }
 }
