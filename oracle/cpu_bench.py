@@ -1,0 +1,194 @@
+"""ORACLE -- TEST INFRASTRUCTURE ONLY: the CPU baselines bench.py reports as `cpu_baseline`.
+
+Run by bench.py as a child process (it never touches the GPU and never imports torch):
+
+  python -m oracle.cpu_bench --corpus FILE --vocab 32000 --merges-json M.json --out R.json
+
+Legs, all on this host's cores:
+  c1        the reference's own test case in full: tests/fixtures corpus.en at vocab 500
+            (tests/test_train_bpe.py:28-34), oracle/cpu_ref.py (pure-Python port of
+            models/tokenizer/train.py, the reference's structure), one core.
+  train     the first 16 MB and 64 MB of the bench corpus at the bench vocab, the same port, one
+            core each (two processes): pre-tokenize + count measured in full, the merge rounds
+            measured until a wall cap, the rest extrapolated at the measured mean per round
+            (rounds_measured_frac says how much was measured).
+  encode    Tokenizer.encode port (cpu_ref.Encoder, tokenizer.py:92-138) of the first 64 MB with
+            the GPU-trained merges, in 1 M-character pieces each encoded on its own -- the
+            reference's dataset encoder (encode.py:31-36) -- over a pool of processes (cores
+            stated).  Piece 0's ids are returned for bench.py to compare with the GPU encoder.
+  exact     the C oracle (oracle/bpe_oracle.c: exact incremental trainer) on the full C2 corpus
+            (2 GB TinyStories-like, vocab 10 000; BASELINE configs[1]) with one counting thread
+            per core and its single-threaded merge loop; the result is checked against the
+            train_C2 scale golden.
+"""
+from __future__ import annotations
+
+import argparse
+import gzip
+import hashlib
+import json
+import multiprocessing as mp
+import os
+import pathlib
+import struct
+import sys
+import threading
+import time
+
+HERE = pathlib.Path(__file__).resolve().parent
+ROOT = HERE.parent
+for p in (ROOT, ROOT / "transformer-lm_amd"):
+    if str(p) not in sys.path:
+        sys.path.insert(0, str(p))
+
+EOT = "<|endoftext|>"
+BLOCK = 4096
+
+
+def _train_leg(args):
+    """one pure-Python training on `m` bytes of a file (m = None: the whole file)"""
+    path, m, vocab, cap_s = args
+    from oracle import cpu_ref
+    with open(path, "rb") as f:
+        text = (f.read(m) if m else f.read()).decode("utf-8")
+    text = text.replace("\r\n", "\n").replace("\r", "\n")   # the reference's text-mode read
+    t0 = time.perf_counter()
+    _, merges, info = cpu_ref.train(text, vocab, [EOT], round_cap_s=cap_s)
+    wall = time.perf_counter() - t0
+    nb = len(text.encode("utf-8"))
+    # the rounds' mean excludes the one-time build of the words, pair counts and index
+    per_round = (info["t_merge_s"] - info["t_build_s"]) / max(1, info["rounds_done"])
+    projected = info["t_count_s"] + info["t_build_s"] + per_round * info["rounds_total"]
+    return {"bytes": nb, "vocab": vocab, "wall_s": round(wall, 3), "t_count_s": round(info["t_count_s"], 3),
+            "t_build_s": round(info["t_build_s"], 3),
+            "rounds_done": info["rounds_done"], "rounds_total": info["rounds_total"],
+            "rounds_measured_frac": round(info["rounds_done"] / max(1, info["rounds_total"]), 4),
+            "ms_per_round": round(per_round * 1e3, 3),
+            "MBps": round(nb / projected / 1e6, 5) if projected > 0 else None,
+            "merges_per_s": round(1.0 / per_round, 2) if per_round > 0 else None,
+            "complete": info["complete"],
+            "merges_sha256": hashlib.sha256(b"".join(struct.pack("<I", len(a)) + a + struct.pack("<I", len(b)) + b
+                                                     for a, b in merges)).hexdigest()}
+
+
+_ENC = None
+
+
+def _enc_init(vocab_items, merges):
+    global _ENC
+    from oracle import cpu_ref
+    _ENC = cpu_ref.Encoder(dict(vocab_items), merges, [EOT])
+
+
+def _enc_piece(piece: str):
+    t = time.perf_counter()
+    ids = _ENC.encode(piece)
+    return len(ids), time.perf_counter() - t, ids
+
+
+def _pieces(text: str, chars: int):
+    return [text[i:i + chars] for i in range(0, len(text), chars)]
+
+
+def encode_leg(path, m, merges_json, procs, chars=1024 * 1024):
+    with open(merges_json) as f:
+        mj = json.load(f)
+    merges = [(bytes.fromhex(a), bytes.fromhex(b)) for a, b in mj["merges"]]
+    vocab = {int(i): bytes.fromhex(h) for i, h in mj["vocab"]}
+    with open(path, "rb") as f:
+        text = f.read(m).decode("utf-8")
+    pieces = _pieces(text, chars)
+    ctx = mp.get_context("fork")   # this process never initialised a GPU
+    t0 = time.perf_counter()
+    with ctx.Pool(procs, initializer=_enc_init, initargs=(list(vocab.items()), merges)) as pool:
+        res = pool.map(_enc_piece, pieces, chunksize=1)
+    wall = time.perf_counter() - t0
+    n_ids = sum(r[0] for r in res)
+    busy = sum(r[1] for r in res)
+    nb = len(text.encode("utf-8"))
+    return {"bytes": nb, "pieces": len(pieces), "chars_per_piece": chars, "procs": procs,
+            "wall_s": round(wall, 3), "MBps": round(nb / wall / 1e6, 4),
+            "MBps_per_core": round(nb / busy / 1e6, 4), "n_ids": n_ids,
+            "piece0_chars": len(pieces[0]) if pieces else 0}, (res[0][2] if res else [])
+
+
+def exact_leg(threads, piece=64 << 20):
+    """C oracle on the C2 corpus: generated into host memory first (untimed), then counted by
+    `threads` threads (safe-split pieces, one oracle counter each), summed, and trained"""
+    import numpy as np
+    from bpe_amd import _lib   # the corpus generator's host twin only (no device call)
+    from oracle import oracle
+    g = json.load(gzip.open(ROOT / "tests" / "golden" / "scale" / "train_C2.json.gz", "rt"))
+    n, seed, flavour = g["n"], g["seed"], g["flavour"]
+    L = _lib.lib()
+    buf = np.empty(n, dtype=np.uint8)
+    tg = time.perf_counter()
+    assert L.bpe_synth_corpus_host(buf.ctypes.data, n, seed, flavour, 0, threads) == 0
+    t_gen = time.perf_counter() - tg
+    pieces = [(lo, min(piece, n - lo)) for lo in range(0, n, piece)]
+    counters = [oracle.Counter([EOT]) for _ in range(threads)]
+    t0 = time.perf_counter()
+
+    def work(t):
+        for i in range(t, len(pieces), threads):
+            lo, m = pieces[i]
+            counters[t].feed(buf.ctypes.data + lo, m)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    for c in counters[1:]:
+        counters[0].absorb(c)
+        c.close()
+    t_count = time.perf_counter() - t0
+    vocab, merges = counters[0].train(g["vocab"])
+    wall = time.perf_counter() - t0
+    counters[0].close()
+    h = hashlib.sha256()
+    for i in range(len(vocab)):
+        h.update(struct.pack("<I", len(vocab[i])) + vocab[i])
+    want = [(bytes.fromhex(a), bytes.fromhex(b)) for a, b in g["merges"]]
+    return {"bytes": n, "vocab": g["vocab"], "threads": threads, "wall_s": round(wall, 3),
+            "t_count_s": round(t_count, 3), "t_merge_s": round(wall - t_count, 3), "t_generate_s": round(t_gen, 3),
+            "MBps": round(n / wall / 1e6, 2), "merges_per_s": round(len(merges) / max(1e-9, wall - t_count), 1),
+            "exact": merges == want and h.hexdigest() == g["vocab_sha256"]}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--corpus", required=True)
+    ap.add_argument("--vocab", type=int, default=32000)
+    ap.add_argument("--samples-mb", default="16,64")
+    ap.add_argument("--cap-s", type=float, default=20.0, help="wall cap of each sample's merge rounds")
+    ap.add_argument("--merges-json", default=None)
+    ap.add_argument("--encode-mb", type=float, default=64.0)
+    ap.add_argument("--procs", type=int, default=16, help="cores for the encode pool and the exact leg")
+    ap.add_argument("--no-exact", action="store_true")
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    c1 = ROOT / "tests" / "golden" / "fixtures" / "corpus.en"
+    legs = [(str(c1), None, 500, None)]
+    for s in a.samples_mb.split(","):
+        m = int(float(s) * 1e6) // BLOCK * BLOCK
+        legs.append((a.corpus, m, a.vocab, a.cap_s))
+    out = {"host_cpus": os.cpu_count()}
+    ctx = mp.get_context("fork")
+    with ctx.Pool(len(legs)) as pool:
+        async_train = pool.map_async(_train_leg, legs)
+        if a.merges_json:
+            m = int(a.encode_mb * 1e6) // BLOCK * BLOCK
+            out["encode"], piece0 = encode_leg(a.corpus, m, a.merges_json, max(1, a.procs - len(legs)))
+            out["encode_piece0_ids_sha256"] = hashlib.sha256(struct.pack(f"<{len(piece0)}I", *piece0)).hexdigest()
+        res = async_train.get()
+    out["c1"] = res[0]
+    out["train"] = res[1:]
+    if not a.no_exact:
+        out["exact"] = exact_leg(a.procs)
+    with open(a.out, "w") as f:
+        json.dump(out, f)
+
+
+if __name__ == "__main__":
+    main()

@@ -31,8 +31,10 @@ def count_pretokens(text: str, specials) -> dict:
     return counts
 
 
-def train(text: str, vocab_size: int, specials=(), deadline: float | None = None):
-    """Returns (vocab, merges, info).  info["complete"] is False if the deadline stopped it."""
+def train(text: str, vocab_size: int, specials=(), deadline: float | None = None,
+          round_cap_s: float | None = None):
+    """Returns (vocab, merges, info).  info["complete"] is False if the deadline (absolute) or the
+    cap on the merge rounds' wall time (from the end of the count) stopped it."""
     t0 = time.perf_counter()
     vocab_list: list = []
     present = set()
@@ -44,6 +46,9 @@ def train(text: str, vocab_size: int, specials=(), deadline: float | None = None
 
     counts = count_pretokens(text, specials)
     t_count = time.perf_counter() - t0
+    if round_cap_s is not None:
+        cap_at = time.perf_counter() + round_cap_s
+        deadline = cap_at if deadline is None else min(deadline, cap_at)
     words = []
     freq = []
     for piece, c in counts.items():
@@ -56,6 +61,8 @@ def train(text: str, vocab_size: int, specials=(), deadline: float | None = None
         for x, y in zip(w, w[1:]):
             pairs[(x, y)] = pairs.get((x, y), 0) + c
             where.setdefault((x, y), set()).add(wi)
+
+    t_build = time.perf_counter() - t0 - t_count   # words, pair counts and the pair -> words index
 
     def bump(p, d):
         pairs[p] = pairs.get(p, 0) + d
@@ -97,5 +104,74 @@ def train(text: str, vocab_size: int, specials=(), deadline: float | None = None
         done += 1
     info = {"complete": done == max(0, rounds) or not pairs, "rounds_done": done,
             "rounds_total": max(0, rounds), "t_count_s": t_count,
-            "t_merge_s": time.perf_counter() - t0 - t_count, "n_words": len(words)}
+            "t_merge_s": time.perf_counter() - t0 - t_count, "t_build_s": t_build, "n_words": len(words)}
     return {i: t for i, t in enumerate(vocab_list)}, merges, info
+
+
+class Encoder:
+    """Tokenizer.encode restated with the reference's structure (models/tokenizer/tokenizer.py):
+      12-38    vocab_inv = {bytes: id} (last id wins); specials deduped, longest first, joined
+               into one capture-group split pattern; a missing special gets id len(vocab)
+      63-90    segment on the specials; each non-special segment pre-tokenized on its own,
+               matches equal to a special dropped
+      92-109   merge: every non-overlapping occurrence of the pair, left to right
+      111-138  per pre-token: the adjacent pair of minimum merge rank (ties: first position)
+               until no pair is ranked; ids by vocab_inv (KeyError when missing)
+    inv_merges is rebuilt per encode() call, as the reference does (tokenizer.py:115)."""
+
+    def __init__(self, vocab: dict, merges, specials=None):
+        self.vocab = dict(vocab)
+        self.vocab_inv = {v: k for k, v in self.vocab.items()}
+        self.merges = list(merges)
+        self.special_tokens = sorted(set(specials or []), key=len, reverse=True)
+        sp = "|".join(regex.escape(t) for t in self.special_tokens)
+        self.segment_rgx = f"({sp})" if sp else None
+        for t in self.special_tokens:
+            if t.encode("utf-8") not in self.vocab_inv:
+                self.vocab[t.encode("utf-8")] = len(self.vocab)
+                self.vocab_inv[t.encode("utf-8")] = len(self.vocab) - 1
+
+    def pretokenize(self, text: str):
+        segments = regex.split(self.segment_rgx, text) if self.segment_rgx else [text]
+        out = []
+        for seg in segments:
+            if seg == "":
+                continue
+            if seg in self.special_tokens:
+                out.append(seg)
+                continue
+            for m in GPT2_SPLIT.finditer(seg, concurrent=True):
+                s = m.group(0)
+                if s not in self.special_tokens:
+                    out.append(s)
+        return out
+
+    @staticmethod
+    def merge(tokens, pair, replacement):
+        new, i = [], 0
+        while i < len(tokens):
+            if tokens[i] == pair[0] and i < len(tokens) - 1 and tokens[i + 1] == pair[1]:
+                new.append(replacement)
+                i += 2
+            else:
+                new.append(tokens[i])
+                i += 1
+        return new
+
+    def encode(self, text: str):
+        pretokens = self.pretokenize(text)
+        inv_merges = {pair: i for i, pair in enumerate(self.merges)}
+        ids = []
+        inf = float("inf")
+        for tok in pretokens:
+            if tok in self.special_tokens:
+                ids.append(self.vocab_inv[tok.encode("utf-8")])
+                continue
+            raw = [bytes([b]) for b in tok.encode("utf-8")]
+            while len(raw) > 1:
+                pair = min(zip(raw, raw[1:]), key=lambda p: inv_merges.get(p, inf))
+                if pair not in inv_merges:
+                    break
+                raw = self.merge(raw, pair, pair[0] + pair[1])
+            ids.extend(self.vocab_inv[b] for b in raw)
+        return ids

@@ -17,3 +17,12 @@ def test_cpu_ref_train_matches_reference(name):
     assert info["complete"]
     assert got_merges == merges
     assert got_vocab == vocab
+
+
+@pytest.mark.parametrize("name", G.names("encode"))
+def test_cpu_ref_encode_matches_reference(name):
+    """the encode port bench.py times (cpu_baseline.encode) against every encode golden"""
+    o = G.load("encode", name)
+    vocab, merges = G.tokenizer_inputs(o)
+    enc = cpu_ref.Encoder(vocab, merges, o["special_tokens"])
+    assert enc.encode(G.encode_text(o)) == o["ids"]
