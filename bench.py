@@ -63,8 +63,10 @@ def parse():
     ap.add_argument("--no-device-resident", action="store_true")
     ap.add_argument("--no-encode", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-mb", type=float, default=16.0)
-    ap.add_argument("--cpu-cap-s", type=float, default=20.0)
+    ap.add_argument("--cpu-samples-mb", default="16,64", help="pure-Python training samples (MB)")
+    ap.add_argument("--cpu-cap-s", type=float, default=20.0, help="wall cap of each sample's merge rounds")
+    ap.add_argument("--cpu-encode-mb", type=float, default=64.0)
+    ap.add_argument("--cpu-procs", type=int, default=16, help="host cores for the encode pool / exact leg")
     ap.add_argument("--no-timing", action="store_true", help="skip per-launch HIP event timing")
     ap.add_argument("--no-file", action="store_true",
                     help="profiling runs: skip the file path (every k_count2 launch then covers the whole "
@@ -83,6 +85,57 @@ def write_corpus(L, path: pathlib.Path, n: int, seed: int, flavour: int):
             del buf
             assert rc == 0, rc
     os.replace(tmp, path)
+
+
+def cpu_baselines(args, path, vocab, merges, L):
+    """The CPU legs (oracle/cpu_bench.py) in a child process that never touches the GPU: the
+    pure-Python port on corpus.en in full and on 16 / 64 MB samples (one core each), the
+    pure-Python encode port over 1 M-character pieces (a pool of cores), and the exact C oracle
+    on the full C2 corpus (one counting thread per core).  Returned as cpu_baseline; `value` is
+    the 64 MB training sample (one core, as the reference runs)."""
+    import hashlib
+    import struct
+    import subprocess
+    from bpe_amd import Tokenizer
+    tmp = pathlib.Path(tempfile.mkdtemp(prefix="bpe355_cpu_"))
+    mj, rj = tmp / "merges.json", tmp / "cpu.json"
+    mj.write_text(json.dumps({"merges": [(a.hex(), b.hex()) for a, b in merges],
+                              "vocab": [(i, b.hex()) for i, b in vocab.items()]}))
+    cmd = [sys.executable, "-m", "oracle.cpu_bench", "--corpus", str(path), "--vocab", str(args.vocab),
+           "--samples-mb", args.cpu_samples_mb, "--cap-s", str(args.cpu_cap_s), "--merges-json", str(mj),
+           "--encode-mb", str(args.cpu_encode_mb), "--procs", str(args.cpu_procs), "--out", str(rj)]
+    subprocess.run(cmd, cwd=ROOT, check=True, timeout=600)
+    r = json.loads(rj.read_text())
+    for f in (mj, rj):
+        f.unlink()
+    tmp.rmdir()
+    # the port's ids for piece 0 must be the GPU encoder's (a 1 M-character parity check)
+    with open(path, "rb") as f:
+        head = f.read(8 << 20).decode("utf-8", errors="ignore")
+    piece0 = head[:r["encode"]["piece0_chars"]]
+    gpu_ids = Tokenizer(vocab, merges, [EOT]).encode(piece0)
+    gpu_sha = hashlib.sha256(struct.pack(f"<{len(gpu_ids)}I", *gpu_ids)).hexdigest()
+    big = max(r["train"], key=lambda x: x["bytes"])
+    cores = os.cpu_count()
+    enc = r["encode"]
+    return {
+        "value": big["MBps"], "unit": "MB/s", "cores": 1, "kind": "port",
+        "sample": (f"first {big['bytes'] / 1e6:.1f} MB of the same corpus at vocab {args.vocab}: "
+                   f"oracle/cpu_ref.py (pure-Python port with the reference's structure) on 1 core "
+                   f"(host shows {cores}); count {big['t_count_s']:.1f}s + build {big['t_build_s']:.1f}s "
+                   f"measured, {big['rounds_done']}/{big['rounds_total']} merge rounds measured in "
+                   f"{args.cpu_cap_s:.0f}s, the rest extrapolated at {big['ms_per_round']:.1f} ms/round"),
+        "rounds_measured_frac": big["rounds_measured_frac"], "merges_per_s": big["merges_per_s"],
+        "samples": r["train"],
+        "c1": dict(r["c1"], note="tests/fixtures corpus.en at vocab 500 (reference test_train_bpe.py:28), "
+                                 "in full, 1 core"),
+        "encode": dict(enc, kind="port", cores=enc["procs"], matches_gpu_piece0=gpu_sha == r["encode_piece0_ids_sha256"],
+                       note="cpu_ref.Encoder (tokenizer.py:92-138) over 1 M-character pieces encoded on their "
+                            "own (encode.py:31-36), a pool of processes"),
+        "exact_cpu": dict(r.get("exact") or {}, kind="port (C oracle)",
+                          note="oracle/bpe_oracle.c on the full C2 corpus (BASELINE configs[1]): one counting "
+                               "thread per core, single-threaded exact merge loop; checked against train_C2"),
+    }
 
 
 def main():
@@ -302,23 +355,7 @@ def main():
     # ---------------------------------------------------------------- CPU baseline (rank 0, N=1)
     cpu = None
     if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
-        from oracle import cpu_ref
-        m = min(n, int(args.cpu_sample_mb * 1e6) // BLOCK * BLOCK)
-        with open(path, "rb") as f:
-            text = f.read(m).decode("utf-8")
-        t0c = time.perf_counter()
-        _, cmerges, info = cpu_ref.train(text, args.vocab, [EOT], deadline=t0c + args.cpu_cap_s)
-        per_round = info["t_merge_s"] / max(1, info["rounds_done"])
-        projected = info["t_count_s"] + per_round * info["rounds_total"]
-        cpu = {"value": round(m / projected / 1e6, 5), "unit": "MB/s", "cores": 1, "kind": "port",
-               "sample": (f"first {m / 1e6:.1f} MB of the same corpus, vocab {args.vocab}, "
-                          f"oracle/cpu_ref.py (pure Python, reference structure) on 1 core of "
-                          f"{os.cpu_count()}: pre-tokenize+count {info['t_count_s']:.2f}s measured, "
-                          f"{info['rounds_done']}/{info['rounds_total']} merge rounds in "
-                          f"{info['t_merge_s']:.1f}s measured, rest extrapolated at "
-                          f"{per_round * 1e3:.1f} ms/round"),
-               "rounds_measured_frac": round(info["rounds_done"] / max(1, info["rounds_total"]), 4),
-               "merges_per_s": round(1.0 / per_round, 2) if per_round > 0 else None}
+        cpu = cpu_baselines(args, path, vocab, merges, L)
 
     if rank == 0:
         s0 = stats[-1]

@@ -50,8 +50,8 @@ def main():
     out["_raw"] = raw
     with open(sys.argv[3], "w") as f:
         json.dump(out, f, indent=1)
-    for k in ("k_merge", "k_apply", "k_argmax", "k_count_words", "k_count2", "k_rec_scatter", "k_rec_reduce",
-              "k_rec_hist"):
+    for k in ("k_count2", "k_rec_reduce", "k_select", "k_merge_batch", "k_apply_batch", "k_enc_scan2",
+              "k_enc_count", "k_enc_write"):
         if k in raw:
             print(k, out[k], raw[k])
 

@@ -19,7 +19,6 @@
 //                 distinct words), then one global table_add per distinct word.
 // The global table is the same {key, count} table as before, so everything downstream (word
 // collection, the multi-GPU exchange) is unchanged.
-#include <hipcub/hipcub.hpp>
 #include <hip/hip_ext.h>
 
 #include <algorithm>
@@ -29,6 +28,7 @@
 
 #include "count.h"
 #include "pretok.h"
+#include "prims.h"
 #include "stage.h"
 #include "stage2.h"
 #include "tokstart.h"
@@ -322,8 +322,8 @@ __global__ void __launch_bounds__(1024) k_rec_cscan(const unsigned* __restrict__
                                                     const unsigned* __restrict__ list,
                                                     const unsigned* __restrict__ list_n,
                                                     unsigned* __restrict__ coff, unsigned long long* __restrict__ ctot) {
-    typedef hipcub::BlockScan<unsigned, 1024> Scan;
-    __shared__ typename Scan::TempStorage tmp;
+    typedef rocprim::block_scan<unsigned, 1024> Scan;
+    __shared__ typename Scan::storage_type tmp;
     __shared__ unsigned carry;
     const unsigned c = blockIdx.x;
     const unsigned n_pages = *list_n;
@@ -333,7 +333,7 @@ __global__ void __launch_bounds__(1024) k_rec_cscan(const unsigned* __restrict__
         const unsigned i = b0 + threadIdx.x;
         const unsigned v = i < n_pages ? page_ch[(size_t)list[i] * kCoarse + c] : 0u;
         unsigned ex, agg;
-        Scan(tmp).ExclusiveSum(v, ex, agg);
+        Scan().exclusive_scan(v, ex, 0u, agg, tmp);
         const unsigned cb = carry;
         if (i < n_pages) coff[(size_t)i * kCoarse + c] = cb + ex;
         __syncthreads();
@@ -346,8 +346,8 @@ __global__ void __launch_bounds__(1024) k_rec_cscan(const unsigned* __restrict__
 // exclusive scan of n <= 4096 totals (one workgroup); base[n] = their sum
 __global__ void __launch_bounds__(1024) k_rec_base(const unsigned long long* __restrict__ tot, int n,
                                                    unsigned long long* __restrict__ base) {
-    typedef hipcub::BlockScan<unsigned long long, 1024> Scan;
-    __shared__ typename Scan::TempStorage tmp;
+    typedef rocprim::block_scan<unsigned long long, 1024> Scan;
+    __shared__ typename Scan::storage_type tmp;
     constexpr int per = 4;
     unsigned long long v[per], ex[per], agg;
 #pragma unroll
@@ -355,7 +355,7 @@ __global__ void __launch_bounds__(1024) k_rec_base(const unsigned long long* __r
         const int i = threadIdx.x * per + k;
         v[k] = i < n ? tot[i] : 0ULL;
     }
-    Scan(tmp).ExclusiveSum(v, ex, agg);
+    Scan().exclusive_scan(v, ex, 0ULL, agg, tmp);
 #pragma unroll
     for (int k = 0; k < per; ++k) {
         const int i = threadIdx.x * per + k;
@@ -507,8 +507,8 @@ __global__ void __launch_bounds__(1024) k_rec_fhist(const uint64_t* __restrict__
 // level 2, offsets: per (coarse c, fine f) an exclusive scan over c's tiles; totals per final bin
 __global__ void __launch_bounds__(256) k_rec_fscan(unsigned* __restrict__ fhist, const unsigned* __restrict__ tile0,
                                                    unsigned long long* __restrict__ ftot) {
-    typedef hipcub::BlockScan<unsigned, 256> Scan;
-    __shared__ typename Scan::TempStorage tmp;
+    typedef rocprim::block_scan<unsigned, 256> Scan;
+    __shared__ typename Scan::storage_type tmp;
     __shared__ unsigned carry;
     const unsigned c = blockIdx.x / kCoarse, f = blockIdx.x % kCoarse;
     const unsigned a = tile0[c], e = tile0[c + 1];
@@ -518,7 +518,7 @@ __global__ void __launch_bounds__(256) k_rec_fscan(unsigned* __restrict__ fhist,
         const unsigned i = b0 + threadIdx.x;
         const unsigned v = i < e ? fhist[(size_t)i * kCoarse + f] : 0u;
         unsigned ex, agg;
-        Scan(tmp).ExclusiveSum(v, ex, agg);
+        Scan().exclusive_scan(v, ex, 0u, agg, tmp);
         const unsigned cb = carry;
         if (i < e) fhist[(size_t)i * kCoarse + f] = cb + ex;
         __syncthreads();

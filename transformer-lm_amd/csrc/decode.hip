@@ -7,7 +7,6 @@
 //
 // Layout: a dense (offset, length) table over ids 0..max_id (length ~0 = no such id) and one
 // byte pool.  Decoding: length lookup -> exclusive scan -> one thread per id copies its bytes.
-#include <hipcub/hipcub.hpp>
 
 #include <cstring>
 #include <memory>
@@ -15,6 +14,7 @@
 #include <vector>
 
 #include "internal.h"
+#include "prims.h"
 
 struct bpe_decoder {
     bpe::DevBuf<unsigned long long> off;
@@ -85,10 +85,7 @@ size_t decode_device(bpe_decoder& D, const uint32_t* d_ids, size_t n, uint8_t* d
     BPE_HIP(hipMemcpyAsync(bad.p, &none, 8, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_dec_len, dim3(ceil_div(n, 256)), dim3(256), 0, s, d_ids, n, D.len.p, D.n_ids, lens.p,
                        bad.p);
-    size_t tb = 0;
-    BPE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, lens.p, offs.p, (int64_t)n, s));
-    DevBuf<uint8_t> tmp(tb);
-    BPE_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, lens.p, offs.p, (int64_t)n, s));
+    exclusive_sum(lens.p, offs.p, n, s);
     unsigned long long h[3];
     BPE_HIP(hipMemcpyAsync(&h[0], offs.p + n - 1, 8, hipMemcpyDeviceToHost, s));
     BPE_HIP(hipMemcpyAsync(&h[1], lens.p + n - 1, 8, hipMemcpyDeviceToHost, s));

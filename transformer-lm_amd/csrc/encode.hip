@@ -17,7 +17,6 @@
 //      device hash map (pair -> rank, product) and writes its vocab ids once (word cache).
 //   4. k_scan<COUNT> + exclusive scan + k_scan<WRITE>: re-walk the pre-tokens and emit each
 //      occurrence's cached ids at its output offset, specials as their ids.
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdlib>
@@ -32,6 +31,7 @@
 
 #include "drive.h"
 #include "internal.h"
+#include "prims.h"
 #include "pretok.h"
 #include "stage.h"
 #include "stage2.h"
@@ -969,10 +969,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
     unsigned long long pool_n = 0;
     if (nw) {
         hipLaunchKernelGGL(k_word_len64, dim3(ceil_div(nw, 256)), dim3(256), 0, s, w_len.p, nw, len64.p);
-        size_t tb = 0;
-        BPE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, len64.p, idoff.p, (int)nw + 0, s));
-        DevBuf<uint8_t> tmp(tb);
-        BPE_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, len64.p, idoff.p, (int)nw, s));
+        exclusive_sum(len64.p, idoff.p, nw, s);
         unsigned long long last[2];
         BPE_HIP(hipMemcpyAsync(&last[0], idoff.p + nw - 1, 8, hipMemcpyDeviceToHost, s));
         BPE_HIP(hipMemcpyAsync(&last[1], len64.p + nw - 1, 8, hipMemcpyDeviceToHost, s));
@@ -990,10 +987,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
     DevBuf<unsigned long long> per(n_spans), per_off(n_spans);
     hipLaunchKernelGGL(k_enc_count, dim3(ceil_div(n_spans, 256)), dim3(256), 0, s, recs, t_start.p,
                        t_count.p, n_spans, slot_info.p, cap, status.p, per.p);
-    size_t tb = 0;
-    BPE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, per.p, per_off.p, (int64_t)n_spans, s));
-    DevBuf<uint8_t> tmp(tb);
-    BPE_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, per.p, per_off.p, (int64_t)n_spans, s));
+    exclusive_sum(per.p, per_off.p, n_spans, s);
     unsigned long long last[2];
     unsigned st = 0;
     BPE_HIP(hipMemcpyAsync(&last[0], per_off.p + n_spans - 1, 8, hipMemcpyDeviceToHost, s));

@@ -15,7 +15,6 @@
 // Segment a rank contributes to the all-gather (all ranks pad to the largest):
 //   u64 cnt[maxw] | u64 len_off[maxw] (len << 32 | byte offset in this segment's byte area) |
 //   bytes[maxb]
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -23,6 +22,7 @@
 #include <vector>
 
 #include "internal.h"
+#include "prims.h"
 #include "stage.h"
 
 namespace bpe {
@@ -125,10 +125,7 @@ void union_word_tables(const uint8_t* text, WordCounts& wc, Comm* comm, hipStrea
     unsigned long long nbytes = 0;
     if (n) {
         hipLaunchKernelGGL(k_len_to_u64, dim3(ceil_div(n, 256)), dim3(256), 0, stream, w_len.p, n, len64.p);
-        size_t tb = 0;
-        BPE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, len64.p, b_off.p, (int)n, stream));
-        DevBuf<uint8_t> tmp(tb);
-        BPE_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, len64.p, b_off.p, (int)n, stream));
+        exclusive_sum(len64.p, b_off.p, n, stream);
         unsigned long long last[2];
         BPE_HIP(hipMemcpyAsync(&last[0], b_off.p + n - 1, 8, hipMemcpyDeviceToHost, stream));
         BPE_HIP(hipMemcpyAsync(&last[1], len64.p + n - 1, 8, hipMemcpyDeviceToHost, stream));

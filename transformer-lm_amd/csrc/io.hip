@@ -6,7 +6,6 @@
 //                                f.read(K) returns one after another
 //   bpe_ids_to_u16_device        np.array(token_ids, dtype=np.uint16), refusing ids > 65535
 //                                instead of wrapping them
-#include <hipcub/hipcub.hpp>
 
 #include <vector>
 
@@ -14,6 +13,7 @@
 
 #include "drive.h"
 #include "internal.h"
+#include "prims.h"
 
 namespace bpe {
 namespace {
@@ -128,10 +128,7 @@ int bpe_utf8_chunk_starts_device(const uint8_t* d_text, size_t n, size_t chars_p
         const size_t threads = (n + bpe::kCharSpan - 1) / bpe::kCharSpan;
         bpe::DevBuf<unsigned long long> cnt(threads), first(threads);
         hipLaunchKernelGGL(bpe::k_char_count, dim3(bpe::ceil_div(threads, 256)), dim3(256), 0, s, d_text, n, cnt.p);
-        size_t tb = 0;
-        BPE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt.p, first.p, (int64_t)threads, s));
-        bpe::DevBuf<uint8_t> tmp(tb);
-        BPE_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, cnt.p, first.p, (int64_t)threads, s));
+        bpe::exclusive_sum(cnt.p, first.p, threads, s);
         unsigned long long last[2];
         BPE_HIP(hipMemcpyAsync(&last[0], first.p + threads - 1, 8, hipMemcpyDeviceToHost, s));
         BPE_HIP(hipMemcpyAsync(&last[1], cnt.p + threads - 1, 8, hipMemcpyDeviceToHost, s));

@@ -10,7 +10,6 @@
 // the offset of the first occurrence that claimed the slot IS the word's identity, so a
 // single 64-bit CAS publishes a slot completely and a later thread verifies a match by
 // comparing bytes against the corpus itself -- exact counting with no spin-waits.
-#include <hipcub/hipcub.hpp>
 
 #include <cstdio>
 #include <cstdlib>
@@ -19,6 +18,7 @@
 
 #include "count.h"
 #include "internal.h"
+#include "prims.h"
 #include "pretok.h"
 #include "stage.h"
 
@@ -197,12 +197,7 @@ const uint8_t* prepare_text(const uint8_t* d_in, size_t n, DevBuf<uint8_t>& scra
     hipLaunchKernelGGL(k_newline_map, dim3(ceil_div(n, 256)), dim3(256), 0, stream, d_in, n,
                        mapped.p, keep.p);
     DevBuf<unsigned long long> d_nsel(1);
-    size_t tmp_bytes = 0;
-    BPE_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmp_bytes, mapped.p, keep.p, scratch.p,
-                                          d_nsel.p, (int64_t)n, stream));
-    DevBuf<uint8_t> tmp(tmp_bytes);
-    BPE_HIP(hipcub::DeviceSelect::Flagged(tmp.p, tmp_bytes, mapped.p, keep.p, scratch.p, d_nsel.p,
-                                          (int64_t)n, stream));
+    select_flagged(mapped.p, keep.p, scratch.p, d_nsel.p, n, stream);
     unsigned long long nsel = 0;
     BPE_HIP(hipMemcpyAsync(&nsel, d_nsel.p, 8, hipMemcpyDeviceToHost, stream));
     BPE_HIP(hipStreamSynchronize(stream));

@@ -36,7 +36,6 @@
 // (every word is one token) the reference pops them in descending byte order, which the host
 // reproduces.
 #include <hip/hip_ext.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -48,6 +47,7 @@
 #include <unordered_map>
 
 #include "internal.h"
+#include "prims.h"
 
 namespace bpe {
 
@@ -2388,10 +2388,7 @@ void MergeLoop<TokT>::build_words(const WordCounts& wc, const std::vector<std::s
     if (n) {
         DevBuf<unsigned long long> len64(n);
         hipLaunchKernelGGL(k_len_u64, dim3(ceil_div(n, 256)), dim3(256), 0, s_, w_len.p, n, len64.p);
-        size_t tb = 0;
-        BPE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, len64.p, H.lbeg.p, (int)n, s_));
-        DevBuf<uint8_t> tmp(tb);
-        BPE_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, len64.p, H.lbeg.p, (int)n, s_));
+        exclusive_sum(len64.p, H.lbeg.p, n, s_);
         unsigned long long last[2];
         BPE_HIP(hipMemcpyAsync(&last[0], H.lbeg.p + n - 1, 8, hipMemcpyDeviceToHost, s_));
         BPE_HIP(hipMemcpyAsync(&last[1], len64.p + n - 1, 8, hipMemcpyDeviceToHost, s_));
@@ -2478,10 +2475,7 @@ void MergeLoop<TokT>::build_index() {
     pos.reserve(std::max(n, 1u));
     if (n) {
         hipLaunchKernelGGL(k_index_count<TokT>, dim3(ceil_div(n, 256)), dim3(256), 0, s_, wdev_, n, cnt.p);
-        size_t tb = 0;
-        BPE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt.p, pos.p, (int)n, s_));
-        tmp.reserve(tb);
-        BPE_HIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, cnt.p, pos.p, (int)n, s_));
+        exclusive_sum(cnt.p, pos.p, n, s_, &tmp);
         uint32_t last[2];
         BPE_HIP(hipMemcpyAsync(&last[0], pos.p + n - 1, 4, hipMemcpyDeviceToHost, s_));
         BPE_HIP(hipMemcpyAsync(&last[1], cnt.p + n - 1, 4, hipMemcpyDeviceToHost, s_));
@@ -2497,12 +2491,7 @@ void MergeLoop<TokT>::build_index() {
                            keys.p, vals.p);
         int bits = 1;
         while ((1u << bits) < tcap) ++bits;
-        size_t tb = 0;
-        BPE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys.p, keys2.p, vals.p, ilist_.p,
-                                                   (int)E, 0, bits, s_));
-        tmp.reserve(tb);
-        BPE_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, keys.p, keys2.p, vals.p, ilist_.p,
-                                                   (int)E, 0, bits, s_));
+        radix_sort_pairs(keys.p, keys2.p, vals.p, ilist_.p, E, (unsigned)bits, s_, &tmp);
         hipLaunchKernelGGL(k_index_bounds, dim3(ceil_div(E, 256)), dim3(256), 0, s_, keys2.p, E,
                            ibeg_.p, ilen_.p);
         hipLaunchKernelGGL(k_index_lens, dim3(ceil_div(tcap, 256)), dim3(256), 0, s_, ibeg_.p, ilen_.p, tcap);
