@@ -1342,7 +1342,6 @@ __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigne
 #pragma unroll
     for (int v = 0; v < V; ++v) r[v] = reinterpret_cast<const uint4*>(s)[v];
     const unsigned long long c = S.cnt[i];   // issued with the slot
-    if (tags && atomicMax(&tags[f], B.batch_id) >= B.batch_id) return;
     TokT e[W];
     __builtin_memcpy(e, r, sizeof(e));
     // the members this word holds: members' tokens are disjoint and their new tokens fresh, so a
@@ -1355,6 +1354,10 @@ __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigne
         for (int q = 1; q + 1 < W; ++q) hit |= (e[q] == ta) & (e[q + 1] == tb);
         hits |= (unsigned)hit << j;
     }
+    // claimed only on a hit (most list entries miss: no atomic for them).  A word rewritten under
+    // another thread's claim was loaded after that claim, so its copy here, torn or not, ends in a
+    // failed claim or in no hit: only the claimant ever writes it.
+    if (!hits || (tags && atomicMax(&tags[f], B.batch_id) >= B.batch_id)) return;
     bool first = true;
     while (hits) {
         const int j = __builtin_ctz(hits);
