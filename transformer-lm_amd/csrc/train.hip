@@ -1381,6 +1381,7 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
                                                      size_t lr_parity, uint32_t* __restrict__ tags) {
     __shared__ unsigned long long l_lr[2 * kLdsB * kMaxBatch];
     __shared__ unsigned s_ma[kMaxBatch], s_mb[kMaxBatch], s_mn[kMaxBatch];   // the members' tokens
+    __shared__ unsigned s_pre[kMaxBatch + 1], s_lbeg[kMaxBatch];   // list prefix sums, list starts
     const int tid = threadIdx.x;
     const Batch& B = *bt;
     if (B.stop) return;
@@ -1408,7 +1409,11 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
             }
         }
     }
-    if (tid < k) { s_ma[tid] = B.m[tid].a; s_mb[tid] = B.m[tid].b; s_mn[tid] = B.m[tid].nw; }
+    if (tid < k) {
+        s_ma[tid] = B.m[tid].a; s_mb[tid] = B.m[tid].b; s_mn[tid] = B.m[tid].nw;
+        s_lbeg[tid] = B.m[tid].list_beg;
+    }
+    if (tid <= k) s_pre[tid] = B.list_pre[tid];
     if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 5);
     for (unsigned q = tid; q < 2 * kLdsB * (unsigned)k; q += blockDim.x) l_lr[q] = 0;
     unsigned long long* LRt = LRbase + (size_t)(B.trip & 1) * lr_parity;   // member j at + j * lr_member
@@ -1484,8 +1489,10 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
             const unsigned total = B.list_pre[k];
             for (unsigned i = bid * blockDim.x + tid; i < total; i += nb * blockDim.x) {
                 int j = 0;
-                while (j + 1 < k && i >= B.list_pre[j + 1]) ++j;
-                const unsigned f = X.list[B.m[j].list_beg + (i - B.list_pre[j])];
+                // the member whose list holds entry i: binary search of the LDS prefix sums
+                for (int step = kMaxBatch / 2; step > 0; step >>= 1)
+                    if (j + step < k && i >= s_pre[j + step]) j += step;
+                const unsigned f = X.list[s_lbeg[j] + (i - s_pre[j])];
                 // a word on several members' lists is rewritten by the first thread to claim it
                 if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f,  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles, tags, f);
                 else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles, tags, f);
