@@ -212,18 +212,38 @@ def main():
         elapsed = max_over_ranks(time.perf_counter() - t0)
         L.bpe_set_timing(0)
 
+    def traffic_of(kernel):
+        """HBM bytes per launch from the committed PMC passes (tools/gpu_pmc_all.sh)"""
+        tf = ROOT / "profiles" / "r03" / "traffic.json"
+        return json.loads(tf.read_text()).get(kernel) if tf.exists() else None
+
+    def merge_roofline(st, note):
+        """the dominant kernel by device time, k_merge_batch (the merge-apply rewrite of a trip):
+        algorithmic bytes per launch (the members' posting-list entries, 4 B each, and the slot
+        words they name at the table's mean slot size; every slot on a full scan; the long words)
+        over its mean launch duration, both from the launches HIP events time on the library's
+        stream (stamped by the kernel's own dispatch packet; one trip in 8)"""
+        a = {k: sum(x[k] for x in st) / len(st) for k in st[0]}
+        if a["merge_kernel_launches"] <= 0:
+            return None
+        us = a["merge_kernel_ms"] * 1e3 / a["merge_kernel_launches"]
+        bpl = a["merge_kernel_bytes"] / a["merge_kernel_launches"]
+        achieved = bpl / (us * 1e-6) / 1e9
+        return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_of("k_merge_batch"),
+                "kernel": "k_merge_batch", "launches_per_step": int(a["n_trips"]),
+                "timed_launches": int(sum(x["merge_kernel_launches"] for x in st)),
+                "avg_launch_us": round(us, 3), "bytes_per_launch": round(bpl), "note": note}
+
     def roofline_of(st, per_step_launches, note):
-        """dominant kernel k_count2: algorithmic bytes (the corpus, read once) / its device time,
-        event-timed on the library's stream by the launches' own dispatch packets"""
+        """k_count2 (pre-tokenize + count): algorithmic bytes (the corpus, read once) / its device
+        time, event-timed on the library's stream by the launches' own dispatch packets"""
         a = {k: sum(x[k] for x in st) / len(st) for k in st[0]}
         if a["count_kernel_ms"] <= 0:
             return None
         kms, kb = a["count_kernel_ms"], a["count_kernel_bytes"]
         achieved = kb / (kms / 1e3) / 1e9
-        traffic = None
-        tf = ROOT / "profiles" / "traffic.json"
-        if tf.exists():
-            traffic = json.loads(tf.read_text()).get("k_count2")
+        traffic = traffic_of("k_count2")
         return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": "k_count2", "launches_per_step": per_step_launches,
@@ -305,10 +325,12 @@ def main():
     # the roofline line: k_count2 over the HBM-resident corpus (one launch per step, the launches
     # rocprofv3 --no-file profiles see); without that run, the file path's per-segment launches
     if dstats:
-        roofline = roofline_of(dstats, 1, ("corpus in HBM, one launch per step" +
-                                           ("; rank 0's slab" if n_gpus > 1 else "")))
+        roofline_count = roofline_of(dstats, 1, ("corpus in HBM, one launch per step" +
+                                                 ("; rank 0's slab" if n_gpus > 1 else "")))
+        roofline = merge_roofline(dstats, "corpus in HBM; sampled launches of the timed steps")
     else:
-        roofline = roofline_of(stats, None, "file path: summed over its per-segment launches")
+        roofline_count = roofline_of(stats, None, "file path: summed over its per-segment launches")
+        roofline = merge_roofline(stats, "file path; sampled launches of the timed steps")
 
     # ---------------------------------------------------------------- encode MB/s (device)
     encode = None
@@ -380,6 +402,7 @@ def main():
             "merge_loop": merge_loop,
             "encode": encode,
             "roofline": roofline,
+            "roofline_count": roofline_count,
             "cpu_baseline": cpu,
             # mean over the K timed steps (the load varies step to step with the host's page
             # cache and PCIe); the library's own clock, so ms_per_step - t_total_ms is the call's

@@ -925,6 +925,11 @@ struct BatchState {
 constexpr unsigned kListCap = 256;   // the candidate list k_select ranks (one thread per entry)
 constexpr unsigned kApplyGrid = 512;   // k_apply_batch workgroups (k_select reads one partial each)
 
+struct SelKey {   // a listed candidate as k_select's ranking reads it
+    long long cnt;
+    unsigned long long ka, kb, ab;   // key8 of a and of b; b << 32 | a
+};
+
 struct TokMetaS {
     unsigned long long ha, pb, hb, pa;   // hash(a), P^len(b), hash(b), P^len(a)
     unsigned la, lb, za, zb, ba, bb;     // lengths; posting lists of a and b (len, begin)
@@ -944,7 +949,7 @@ struct DeltaSinkN {
 // (MergeLoop::report_probe): 0-13 phase stamps, 14/15 the last merge/apply workgroup done, 16 the
 // next trip's select start, 17-19 inside select's rule, 20/21 the last merge/apply workgroup's index
 constexpr int kProbeTrip = 8;
-constexpr int kProbeSlots = 24;
+constexpr int kProbeSlots = 32;   // 24-28: inside k_select's first phase
 __device__ __forceinline__ void probe_stamp(const RoundState* st, int trip, int k) {
     if (st->probe && (trip % kProbeTrip) == 0)
         st->probe[kProbeSlots * (size_t)(trip / kProbeTrip) + k] = __builtin_amdgcn_s_memrealtime();
@@ -1011,6 +1016,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     static_assert(kApplyGrid <= 64 * kSelListWave, "one partial per thread of the partial waves");
     __shared__ Cand s_wave[kSelListWave];
     __shared__ Cand s_all[kListCap];
+    __shared__ SelKey s_key[kListCap];   // the same entries packed for the ranking loop
     __shared__ Cand s_list[kTopM];
     __shared__ long long s_cnt[kListCap];
     __shared__ long long s_cnt_target, s_cnt_last;   // counts at sorted positions kListTarget - 1, ln - 1
@@ -1073,20 +1079,39 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         if (li < kTopM) s_list[li] = cand_none();
         if (li == 0) { s_cnt_target = LLONG_MAX; s_cnt_last = LLONG_MAX; }
         s_all[li] = x;
+        s_key[li] = SelKey{x.cnt, x.ka, x.kb, (unsigned long long)x.b << 32 | x.a};
         s_cnt[li] = x.cnt;
+        if (li == 0 && lq.slot != 0xfffffffeu) probe_stamp(st, ptrip, 24);   // the list entry arrived
         if (have && kSelMetaAll) cand_meta(x, K, X, lm, lold);   // overlaps the partials' reduction
+        if (li == 0 && lold != 0xfffffffeu && lm.la != 0xfffffffeu) probe_stamp(st, ptrip, 25);   // metadata + dedupe
     }
+    if (tid == 0) probe_stamp(st, ptrip, 26);   // wave 0's partials reduced
+    if (tid == 0 && st->probe && (ptrip % kProbeTrip) == 0) st->probe[kProbeSlots * (size_t)(ptrip / kProbeTrip) + 30] = ln + 1;
     __syncthreads();
+    if (li == 0) probe_stamp(st, ptrip, 27);
     long long tgt = LLONG_MAX, last = LLONG_MAX;
     if (have) {
-        // rank by count first (cheap); the full order only among equal counts near the top
-        int rc = 0;
+        // rank among the entries: (count, a's 8-byte prefix, b's) branch-free, loads independent of
+        // each other so they pipeline; only equal prefixes of different tokens need the bytes (rare:
+        // then the full comparison, as cand_better)
+        int rc = 0, rank = 0;
+        bool tail = false;
 #pragma unroll 8
-        for (int j = 0; j < nl; ++j) rc += s_cnt[j] > x.cnt ? 1 : 0;
-        int rank = rc;
-        if (rc < kTopM)
+        for (int j = 0; j < nl; ++j) {
+            const SelKey y = s_key[j];
+            const unsigned ya = (unsigned)y.ab, yb = (unsigned)(y.ab >> 32);
+            const bool gt = y.cnt > x.cnt, eq = y.cnt == x.cnt && j != li;
+            const bool ad = ya != x.a, bd = yb != x.b;
+            rc += gt;
+            rank += gt | (eq & ad & (y.ka > x.ka)) | (eq & !ad & bd & (y.kb > x.kb));
+            tail |= eq & ((ad & (y.ka == x.ka)) | (!ad & bd & (y.kb == x.kb)));
+        }
+        if (li == 0 && rank != -7) probe_stamp(st, ptrip, 29);   // ranking loop done
+        if (tail) {
+            rank = rc;
             for (int j = 0; j < nl; ++j)
                 rank += (s_cnt[j] == x.cnt && j != li && cand_better(s_all[j], x, K.pool, K.off, K.len)) ? 1 : 0;
+        }
         if (rank < kTopM) {
             if (!kSelMetaAll) cand_meta(x, K, X, lm, lold);
             s_list[rank] = x;
@@ -1096,6 +1121,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         // the count at sorted position t is the least count whose first position is <= t
         tgt = rc <= (int)kListTarget - 1 ? x.cnt : LLONG_MAX;
         last = x.cnt;
+        if (li == 0 && rank != -7) probe_stamp(st, ptrip, 28);   // ranked
     }
     if (li >= 0) {   // wave minima, then one LDS atomic per wave
         for (int o = 32; o > 0; o >>= 1) {
@@ -3013,6 +3039,32 @@ void MergeLoop<TokT>::report_probe() {
         if (nr)
             std::fprintf(stderr, "[bpe355 probe] select rule: p1 %.2f | head+meta %.2f | clash+k+gap %.2f | record %.2f\n",
                          r[0] / nr, r[1] / nr, r[2] / nr, r[3] / nr);
+        double q[6] = {};
+        int nq = 0;
+        for (size_t t = 0; t + 1 < pr.size() / kProbeSlots; ++t) {
+            const unsigned long long* p = &pr[kProbeSlots * t];
+            if (!p[1] || !p[24] || !p[25] || !p[26] || !p[27] || !p[28] || !p[2]) continue;
+            q[0] += (double)((long long)p[24] - (long long)p[1]) * 0.01; q[1] += (double)((long long)p[25] - (long long)p[24]) * 0.01;
+            q[2] += (double)((long long)p[26] - (long long)p[1]) * 0.01; q[3] += (double)((long long)p[27] - (long long)p[25]) * 0.01;
+            q[4] += (double)((long long)p[28] - (long long)p[27]) * 0.01; q[5] += (double)((long long)p[2] - (long long)p[28]) * 0.01;
+            ++nq;
+        }
+        if (nq)
+            std::fprintf(stderr, "[bpe355 probe] select phase 1 (list thread 0): list entry %.2f | metadata+dedupe %.2f | "
+                                 "(wave 0 partials %.2f) | barrier %.2f | rank %.2f | minima+barrier %.2f (%d trips)\n",
+                         q[0] / nq, q[1] / nq, q[2] / nq, q[3] / nq, q[4] / nq, q[5] / nq, nq);
+        std::vector<double> nls, rl;
+        for (size_t t = 0; t + 1 < pr.size() / kProbeSlots; ++t) {
+            const unsigned long long* p = &pr[kProbeSlots * t];
+            if (p[30]) nls.push_back((double)p[30] - 1);
+            if (p[27] && p[29]) rl.push_back(((long long)p[29] - (long long)p[27]) * 0.01);
+        }
+        std::sort(nls.begin(), nls.end());
+        std::sort(rl.begin(), rl.end());
+        if (!nls.empty() && !rl.empty())
+            std::fprintf(stderr, "[bpe355 probe] select list entries p10 %.0f p50 %.0f p90 %.0f max %.0f | ranking loop us p50 %.2f p90 %.2f\n",
+                         nls[nls.size() / 10], nls[nls.size() / 2], nls[nls.size() * 9 / 10], nls.back(),
+                         rl[rl.size() / 2], rl[rl.size() * 9 / 10]);
     }
     {   // which workgroup finishes last: merge blocks below k register members; apply's last block
         int nm = 0, nm_reg = 0, na = 0, na_lastblk = 0;
