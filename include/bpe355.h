@@ -189,6 +189,15 @@ int bpe_tok_encode_chunks(bpe_tokenizer* tok, const uint8_t* utf8, size_t n, con
                           size_t n_starts, uint32_t* ids_out, size_t cap, size_t* n_out);
 int bpe_tok_encode_chunks_device(bpe_tokenizer* tok, const uint8_t* d_utf8, size_t n, const uint64_t* starts,
                                  size_t n_starts, uint32_t* d_out, size_t* n_out, void* hip_stream);
+/* The reference's dataset encoder (encode.py:18-38) on one file: the file is read by the library's
+ * pinned multi-threaded reader into HBM, decoded as open(path, "r", encoding="utf-8") reads it
+ * (strict UTF-8, universal newlines), cut into chars_per_piece-character pieces (f.read(1024*1024)),
+ * each piece encoded on its own, and the ids written as np.uint16 (encode.py:37; an id past
+ * 65535 fails with BPE_E_LIMIT instead of wrapping) into ids_out (host memory, cap ids; the
+ * file's byte count always suffices).  The device buffers are kept by the tokenizer across
+ * calls.  phase_ms (NULL or 4 doubles): read, decode + piece starts, encode, copy to host. */
+int bpe_tok_encode_file_u16(bpe_tokenizer* tok, const char* path, size_t chars_per_piece, uint16_t* ids_out,
+                            size_t cap, size_t* n_out, double* phase_ms);
 /* encode(text) on n_gpus devices of this process (<= 0: every visible one; SURVEY.md 8b's n_gpus):
  * the text is cut at safe split points that no special token spans, each device encodes its
  * piece, the ids are concatenated -- identical to bpe_tok_encode (tokenizer.py:111-138). */

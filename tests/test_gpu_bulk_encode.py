@@ -214,3 +214,19 @@ def test_copy_to_host_bytes():
         dst = np.zeros(size, dtype=np.uint8)
         _lib.check(L.bpe_copy_to_host(_device(src), size, dst.ctypes.data))
         assert np.array_equal(dst, src.cpu().numpy())
+
+
+def test_encode_file_refuses_ids_above_uint16(tmp_path):
+    """the native bulk path writes np.uint16 on the device: an id past 65535 (here a special
+    token's) fails loudly instead of wrapping (encode.py:37 would wrap it silently)"""
+    from bpe_amd import Tokenizer
+    from bpe_amd.encode import encode_file
+    vocab = {i: bytes([i]) for i in range(256)}
+    vocab[70000] = b"<|big|>"
+    tok = Tokenizer(vocab, [], ["<|big|>"])
+    src = tmp_path / "s.txt"
+    src.write_bytes(b"ab <|big|> cd")
+    with pytest.raises(RuntimeError, match="uint16"):
+        encode_file(tok, src)
+    src.write_bytes(b"ab cd ef")   # the same handle again, with every id in range
+    assert encode_file(tok, src).tolist() == [97, 98, 32, 99, 100, 32, 101, 102]

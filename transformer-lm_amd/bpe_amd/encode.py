@@ -104,12 +104,30 @@ def read_file_device(path):
     return raw
 
 
+last_phases_ms = {}   # the last encode_file's read / decode / encode / copy times (library clock)
+
+
+def encode_file_native(tokenizer: Tokenizer, path, chars_per_piece: int = CHARS_PER_PIECE) -> np.ndarray:
+    """A regular file through bpe_tok_encode_file_u16: read into HBM by the library's reader,
+    decoded, pieces, encoded straight to uint16 in a device buffer the tokenizer keeps, and copied
+    into host memory by copier threads -- no intermediate uint32 ids, no per-call device arrays."""
+    L = _lib.lib()
+    n = os.stat(path).st_size
+    host = np.empty(max(n, 1), dtype=np.uint16)   # ids <= bytes; pages are touched only as written
+    k = ctypes.c_size_t(0)
+    ph = (ctypes.c_double * 4)()
+    _lib.check(L.bpe_tok_encode_file_u16(tokenizer._device(), os.fsencode(os.fspath(path)), chars_per_piece,
+                                         host.ctypes.data, host.size, ctypes.byref(k), ph), "encode file")
+    last_phases_ms.clear()
+    last_phases_ms.update(read=ph[0], decode=ph[1], encode=ph[2], copy=ph[3])
+    return host[:k.value]
+
+
 def encode_file(tokenizer: Tokenizer, input_path, output_path=None, fmt: str = "pt",
                 chars_per_piece: int = CHARS_PER_PIECE) -> np.ndarray:
     """Encode a text file like encode.py:main; write it if output_path is given."""
-    raw = read_file_device(input_path)
-    if raw is not None:
-        pt = encode_device_u16(tokenizer, raw, chars_per_piece)
+    if stat.S_ISREG(os.stat(input_path).st_mode):   # missing: FileNotFoundError, as open() raises
+        pt = encode_file_native(tokenizer, input_path, chars_per_piece)
     else:
         with open(input_path, "rb") as f:
             data = f.read()

@@ -19,6 +19,7 @@
 //      occurrence's cached ids at its output offset, specials as their ids.
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -594,6 +595,9 @@ __device__ __forceinline__ void emit_span(const uint32_t* __restrict__ r, uint32
     }
 }
 
+// OutT uint32_t: the ids; uint16_t: np.uint16 as encode.py saves them (encode.py:37), an id past
+// 65535 reported in status (bit 128) instead of wrapped
+template <class OutT>
 __global__ void __launch_bounds__(256) k_enc_write(const uint32_t* __restrict__ recs,
                                                    const unsigned long long* __restrict__ t_start,
                                                    const uint32_t* __restrict__ t_count, size_t n_spans,
@@ -602,33 +606,59 @@ __global__ void __launch_bounds__(256) k_enc_write(const uint32_t* __restrict__ 
                                                    const int64_t* __restrict__ sp_vid,
                                                    const unsigned long long* __restrict__ per,
                                                    const unsigned long long* __restrict__ per_off, size_t cap,
-                                                   uint32_t* __restrict__ out) {
+                                                   OutT* __restrict__ out, unsigned* __restrict__ status) {
     __shared__ __attribute__((aligned(16))) uint32_t buf[kWriteLds];
+    __shared__ unsigned s_wide;
     const size_t t0 = (size_t)blockIdx.x * 256, t = t0 + threadIdx.x;
     const size_t tl = t0 + 255 < n_spans ? t0 + 255 : n_spans - 1;   // the chunk's last span
     const unsigned long long o0 = per_off[t0], o1 = per_off[tl] + per[tl];
     const unsigned long long total = o1 - o0;
+    constexpr bool kNarrow = sizeof(OutT) == 2;
     if (total > kWriteLds) {   // too many ids for LDS: straight to memory
+        bool wide = false;
         if (t < n_spans)
             emit_span(recs + t_start[t], t_count[t], slot_info, ids_pool, sp_vid, cap, per_off[t],
-                      [&](unsigned long long q, uint32_t v) { out[q] = v; });
+                      [&](unsigned long long q, uint32_t v) { out[q] = (OutT)v; wide |= kNarrow && v > 0xffffu; });
+        if (wide) atomicOr(status, 128u);
         return;
     }
+    if (threadIdx.x == 0) s_wide = 0;
     if (t < n_spans)
         emit_span(recs + t_start[t], t_count[t], slot_info, ids_pool, sp_vid, cap, per_off[t] - o0,
                   [&](unsigned long long q, uint32_t v) { buf[q] = v; });
     __syncthreads();
-    // out + o0 is 4-byte aligned: a scalar head up to 16-byte alignment, then uint4 stores
-    const unsigned head = (unsigned)(((16 - ((uintptr_t)(out + o0) & 15)) & 15) / 4);
+    // out + o0 is OutT-aligned: a scalar head up to 16-byte alignment, then 16-byte stores
+    constexpr unsigned kPer = 16 / sizeof(OutT);   // ids per 16-byte store
+    const unsigned head = (unsigned)(((16 - ((uintptr_t)(out + o0) & 15)) & 15) / sizeof(OutT));
     const unsigned h = head < total ? head : (unsigned)total;
-    if (threadIdx.x < h) out[o0 + threadIdx.x] = buf[threadIdx.x];
-    const unsigned body = (unsigned)(total - h) / 4;
+    bool wide = false;
+    if (threadIdx.x < h) { out[o0 + threadIdx.x] = (OutT)buf[threadIdx.x]; wide |= buf[threadIdx.x] > 0xffffu; }
+    const unsigned body = (unsigned)(total - h) / kPer;
     uint4* dst = reinterpret_cast<uint4*>(out + o0 + h);
     for (unsigned i = threadIdx.x; i < body; i += 256) {
-        const unsigned q = h + 4 * i;
-        dst[i] = make_uint4(buf[q], buf[q + 1], buf[q + 2], buf[q + 3]);
+        const unsigned q = h + kPer * i;
+        if (kNarrow) {
+            uint32_t w[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t lo = buf[q + 2 * k], hi = buf[q + 2 * k + 1];
+                wide |= (lo | hi) > 0xffffu;
+                w[k] = (lo & 0xffffu) | (hi << 16);
+            }
+            dst[i] = make_uint4(w[0], w[1], w[2], w[3]);
+        } else {
+            dst[i] = make_uint4(buf[q], buf[q + 1], buf[q + 2], buf[q + 3]);
+        }
     }
-    for (unsigned q = h + 4 * body + threadIdx.x; q < total; q += 256) out[o0 + q] = buf[q];
+    for (unsigned q = h + kPer * body + threadIdx.x; q < total; q += 256) {
+        out[o0 + q] = (OutT)buf[q];
+        wide |= buf[q] > 0xffffu;
+    }
+    if (kNarrow && wide) s_wide = 1;
+    if (kNarrow) {
+        __syncthreads();
+        if (threadIdx.x == 0 && s_wide) atomicOr(status, 128u);
+    }
 }
 
 __device__ __forceinline__ uint2 rank_of(const EncTables& E, uint32_t a, uint32_t b) {
@@ -707,6 +737,17 @@ struct bpe_tokenizer {
     // re-allocating tens of GB per call costs up to seconds in the driver (measured 0.5 -> 2.8 s
     // for an 11.9 GB encode).  Calls on one handle are serialized on its stream.
     bpe::DevBuf<uint32_t> recs_cache;
+    // the other per-call device arrays, kept the same way (grow-only): per 64-byte span, per
+    // word-table slot, per unique word, the id pool, the u16 output of the bulk encoder
+    struct Scratch {
+        bpe::DevBuf<uint32_t> t_count, w_slot, w_len, pool;
+        bpe::DevBuf<unsigned long long> t_start, fill, kv, pos, w_off, len64, idoff, slot_info, per, per_off;
+        bpe::DevBuf<unsigned> status, d_nw;
+        bpe::DevBuf<bpe::Seg> segs;
+        bpe::DevBuf<uint8_t> tmp;
+        bpe::DevBuf<uint16_t> ids16;
+        bpe::DevBuf<uint8_t> text, text2;   // the bulk encoder's file bytes (and its newline-translated copy)
+    } sc;
     // construction inputs, to build the same tables for the other ranks of a multi-device encode
     // (bpe_tok_encode_gpus); those copies own their stream and record buffer
     std::string vblob, mblob;
@@ -839,7 +880,8 @@ void build_tokenizer(bpe_tokenizer& T, const uint8_t* vb, size_t vn, const uint8
 // result that of separate encode() calls on the pieces between them, concatenated: a cut ends
 // every segment, and a special token may not straddle one (encode.py's 1 M-character chunks,
 // encode_iterable's 2 MiB batches).
-size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t* d_out,
+template <class OutT>
+size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_out,
                      hipStream_t s, const std::vector<unsigned long long>& cuts_in = {}) {
     if (n == 0) return 0;
     std::vector<unsigned long long> cuts;
@@ -905,7 +947,9 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
         if (cur < n) segs.push_back(Seg{cur, n, -1, 0});
     }
     const int nseg = (int)segs.size();
-    DevBuf<Seg> d_segs(nseg);
+    auto& S = T.sc;
+    DevBuf<Seg>& d_segs = S.segs;
+    d_segs.reserve(std::max(nseg, 1));
     BPE_HIP(hipMemcpyAsync(d_segs.p, segs.data(), nseg * sizeof(Seg), hipMemcpyHostToDevice, s));
 
     // 2. one staged pass: unique pre-tokens into the word table, one record per pre-token
@@ -925,16 +969,20 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
         sgrid = std::max(1u, std::min(sgrid, (unsigned)std::atoi(e)));
     // first guess: small texts have many more unique words per byte than large corpora
     size_t cap = next_pow2(std::max<size_t>(1 << 16, n < (1u << 26) ? n / 16 : n / 1024));
-    DevBuf<unsigned long long> kv, pos;
+    DevBuf<unsigned long long>&kv = S.kv, &pos = S.pos;
     if (T.recs_cache.n < std::max<size_t>(n, 1)) T.recs_cache.alloc(std::max<size_t>(n, 1));
     uint32_t* const recs = T.recs_cache.p;
-    DevBuf<uint32_t> t_count(n_spans);
-    DevBuf<unsigned long long> t_start(n_spans), fill(1);
-    DevBuf<unsigned> status(1);
+    DevBuf<uint32_t>& t_count = S.t_count;
+    DevBuf<unsigned long long>&t_start = S.t_start, &fill = S.fill;
+    DevBuf<unsigned>& status = S.status;
+    t_count.reserve(n_spans);
+    t_start.reserve(n_spans);
+    fill.reserve(1);
+    status.reserve(1);
     for (int attempt = 0;; ++attempt) {
-        kv.alloc(2 * cap);
-        pos.alloc(cap);
-        BPE_HIP(hipMemsetAsync(kv.p, 0, kv.bytes(), s));
+        kv.reserve(2 * cap);
+        pos.reserve(cap);
+        BPE_HIP(hipMemsetAsync(kv.p, 0, 2 * cap * sizeof(unsigned long long), s));
         BPE_HIP(hipMemsetAsync(status.p, 0, 4, s));
         BPE_HIP(hipMemsetAsync(fill.p, 0, 8, s));
         hipLaunchKernelGGL(kern, dim3(sgrid), dim3(256), lds, s, d_text, n, n_chunks, d_segs.p, nseg,
@@ -951,10 +999,13 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
         BPE_REQUIRE(attempt < 6, BPE_E_NOMEM, "word table overflow");
         cap *= 4;
     }
-    DevBuf<uint32_t> w_slot(cap);
-    DevBuf<unsigned long long> w_off(cap);
-    DevBuf<uint32_t> w_len(cap);
-    DevBuf<unsigned> d_nw(1);
+    DevBuf<uint32_t>&w_slot = S.w_slot, &w_len = S.w_len;
+    DevBuf<unsigned long long>& w_off = S.w_off;
+    DevBuf<unsigned>& d_nw = S.d_nw;
+    w_slot.reserve(cap);
+    w_off.reserve(cap);
+    w_len.reserve(cap);
+    d_nw.reserve(1);
     BPE_HIP(hipMemsetAsync(d_nw.p, 0, 4, s));
     hipLaunchKernelGGL(k_collect, dim3(ceil_div(cap, 256)), dim3(256), 0, s, kv.p, pos.p, cap, w_slot.p,
                        w_off.p, w_len.p, d_nw.p);
@@ -963,20 +1014,24 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
     BPE_HIP(hipStreamSynchronize(s));
 
     // 3. encode each unique word once
-    DevBuf<unsigned long long> len64(std::max(nw, 1u)), idoff(std::max(nw, 1u) + 1);
-    DevBuf<unsigned long long> slot_info(cap);   // every slot a record names is a word's slot
-    BPE_HIP(hipMemsetAsync(slot_info.p, 0, slot_info.bytes(), s));
+    DevBuf<unsigned long long>&len64 = S.len64, &idoff = S.idoff;
+    len64.reserve(std::max(nw, 1u));
+    idoff.reserve(std::max(nw, 1u) + 1);
+    DevBuf<unsigned long long>& slot_info = S.slot_info;   // every slot a record names is a word's slot
+    slot_info.reserve(cap);
+    BPE_HIP(hipMemsetAsync(slot_info.p, 0, cap * sizeof(unsigned long long), s));
     unsigned long long pool_n = 0;
     if (nw) {
         hipLaunchKernelGGL(k_word_len64, dim3(ceil_div(nw, 256)), dim3(256), 0, s, w_len.p, nw, len64.p);
-        exclusive_sum(len64.p, idoff.p, nw, s);
+        exclusive_sum(len64.p, idoff.p, nw, s, &S.tmp);
         unsigned long long last[2];
         BPE_HIP(hipMemcpyAsync(&last[0], idoff.p + nw - 1, 8, hipMemcpyDeviceToHost, s));
         BPE_HIP(hipMemcpyAsync(&last[1], len64.p + nw - 1, 8, hipMemcpyDeviceToHost, s));
         BPE_HIP(hipStreamSynchronize(s));
         pool_n = last[0] + last[1];
     }
-    DevBuf<uint32_t> pool(std::max<unsigned long long>(pool_n, 1));
+    DevBuf<uint32_t>& pool = S.pool;
+    pool.reserve(std::max<unsigned long long>(pool_n, 1));
     BPE_HIP(hipMemsetAsync(status.p, 0, 4, s));
     if (nw) {
         hipLaunchKernelGGL(k_encode_words, dim3(ceil_div(nw, 256)), dim3(256), 0, s, d_text, E, w_off.p,
@@ -984,10 +1039,12 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
         BPE_HIP(hipGetLastError());
     }
     // 4. ids per span, offsets, then write: two streams over the records
-    DevBuf<unsigned long long> per(n_spans), per_off(n_spans);
+    DevBuf<unsigned long long>&per = S.per, &per_off = S.per_off;
+    per.reserve(n_spans);
+    per_off.reserve(n_spans);
     hipLaunchKernelGGL(k_enc_count, dim3(ceil_div(n_spans, 256)), dim3(256), 0, s, recs, t_start.p,
                        t_count.p, n_spans, slot_info.p, cap, status.p, per.p);
-    exclusive_sum(per.p, per_off.p, n_spans, s);
+    exclusive_sum(per.p, per_off.p, n_spans, s, &S.tmp);
     unsigned long long last[2];
     unsigned st = 0;
     BPE_HIP(hipMemcpyAsync(&last[0], per_off.p + n_spans - 1, 8, hipMemcpyDeviceToHost, s));
@@ -999,9 +1056,15 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, uint32_t
                                            std::to_string(st) + ")");
     const size_t total = last[0] + last[1];
     BPE_REQUIRE(total <= n, BPE_E_HIP, "encode produced more ids than input bytes");
-    hipLaunchKernelGGL(k_enc_write, dim3(ceil_div(n_spans, 256)), dim3(256), 0, s, recs, t_start.p,
-                       t_count.p, n_spans, slot_info.p, pool.p, E.sp_vid, per.p, per_off.p, cap, d_out);
+    if (sizeof(OutT) == 2) BPE_HIP(hipMemsetAsync(status.p, 0, 4, s));
+    hipLaunchKernelGGL(k_enc_write<OutT>, dim3(ceil_div(n_spans, 256)), dim3(256), 0, s, recs, t_start.p,
+                       t_count.p, n_spans, slot_info.p, pool.p, E.sp_vid, per.p, per_off.p, cap, d_out, status.p);
     BPE_HIP(hipGetLastError());
+    if (sizeof(OutT) == 2) {
+        BPE_HIP(hipMemcpyAsync(&st, status.p, 4, hipMemcpyDeviceToHost, s));
+        BPE_HIP(hipStreamSynchronize(s));
+        BPE_REQUIRE(!(st & 128u), BPE_E_LIMIT, "a token id does not fit np.uint16 (vocab larger than 65536)");
+    }
     BPE_HIP(hipStreamSynchronize(s));
     return total;
 }
@@ -1092,6 +1155,11 @@ size_t encode_gpus(bpe_tokenizer& T, const uint8_t* utf8, size_t n, uint32_t* id
     return m;
 }
 
+// a C-ABI call of this library, inside another: its failure as an Error (message kept)
+void check_rc(int rc) {
+    if (rc != BPE_OK) throw Error{rc, bpe_last_error(), bpe_last_errno()};
+}
+
 template <class F>
 int guarded_enc(F&& f) {
     try {
@@ -1176,6 +1244,52 @@ int bpe_tok_encode_chunks_device(bpe_tokenizer* tok, const uint8_t* d_utf8, size
             BPE_REQUIRE(cuts[i] >= cuts[i - 1], BPE_E_ARG, "chunk starts must be sorted");
         hipStream_t s = hip_stream ? (hipStream_t)hip_stream : tok->stream;
         *n_out = bpe::encode_device(*tok, d_utf8, n, d_out, s, cuts);
+    });
+}
+
+int bpe_tok_encode_file_u16(bpe_tokenizer* tok, const char* path, size_t chars_per_piece, uint16_t* ids_out,
+                            size_t cap, size_t* n_out, double* phase_ms) {
+    return bpe::guarded_enc([&] {
+        BPE_REQUIRE(tok && path && n_out && chars_per_piece > 0, BPE_E_ARG, "NULL argument");
+        *n_out = 0;
+        using clk = std::chrono::steady_clock;
+        auto ms = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+        double ph[4] = {0, 0, 0, 0};
+        auto t0 = clk::now();
+        const bpe::Source src = bpe::Source::open_path(path);   // FileNotFoundError etc. before the GPU
+        int dev = 0;
+        BPE_HIP(hipGetDevice(&dev));
+        auto& S = tok->sc;
+        const hipStream_t s = tok->stream;
+        const size_t n = src.size;
+        S.text.reserve(std::max<size_t>(n, 1));
+        bpe::stage_to_device(src, 0, n, S.text.p, dev, bpe::io_threads());
+        ph[0] = ms(t0);
+        auto t1 = clk::now();
+        size_t m = 0;
+        const uint8_t* text = n ? bpe::prepare_text(S.text.p, n, S.text2, &m, s) : S.text.p;
+        // where each chars_per_piece-character piece starts (encode.py:31-33 f.read(K))
+        size_t ns = 0;
+        std::vector<uint64_t> starts;
+        if (m) {
+            bpe::check_rc(bpe_utf8_chunk_starts_device(text, m, chars_per_piece, nullptr, 0, &ns, s));
+            starts.resize(ns);
+            bpe::check_rc(bpe_utf8_chunk_starts_device(text, m, chars_per_piece, starts.data(), ns, &ns, s));
+        }
+        ph[1] = ms(t1);
+        auto t2 = clk::now();
+        S.ids16.reserve(std::max<size_t>(m, 1));
+        const std::vector<unsigned long long> cuts(starts.begin(), starts.end());
+        const size_t k = m ? bpe::encode_device(*tok, text, m, S.ids16.p, s, cuts) : 0;
+        ph[2] = ms(t2);
+        *n_out = k;
+        BPE_REQUIRE(k <= cap, BPE_E_ARG, "ids_out holds " + std::to_string(cap) + " ids, the file encodes to " +
+                                             std::to_string(k));
+        auto t3 = clk::now();
+        if (k) bpe::device_to_host(reinterpret_cast<const uint8_t*>(S.ids16.p), 2 * k,
+                                   reinterpret_cast<uint8_t*>(ids_out), dev, bpe::io_threads());
+        ph[3] = ms(t3);
+        if (phase_ms) std::memcpy(phase_ms, ph, sizeof(ph));
     });
 }
 
