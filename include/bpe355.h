@@ -195,7 +195,10 @@ int bpe_tok_encode_chunks_device(bpe_tokenizer* tok, const uint8_t* d_utf8, size
  * each piece encoded on its own, and the ids written as np.uint16 (encode.py:37; an id past
  * 65535 fails with BPE_E_LIMIT instead of wrapping) into ids_out (host memory, cap ids; the
  * file's byte count always suffices).  The device buffers are kept by the tokenizer across
- * calls.  phase_ms (NULL or 4 doubles): read, decode + piece starts, encode, copy to host. */
+ * calls.  The stages overlap: the file streams in by 1 GiB slabs while the pieces already read
+ * are validated, encoded and copied out (a text with a carriage return is redone in one pass
+ * once read).  phase_ms (NULL or 4 doubles): busy milliseconds of the reader, of validation +
+ * piece starts, of the encodes and of the copy to host. */
 int bpe_tok_encode_file_u16(bpe_tokenizer* tok, const char* path, size_t chars_per_piece, uint16_t* ids_out,
                             size_t cap, size_t* n_out, double* phase_ms);
 /* encode(text) on n_gpus devices of this process (<= 0: every visible one; SURVEY.md 8b's n_gpus):

@@ -230,3 +230,76 @@ def test_encode_file_refuses_ids_above_uint16(tmp_path):
         encode_file(tok, src)
     src.write_bytes(b"ab cd ef")   # the same handle again, with every id in range
     assert encode_file(tok, src).tolist() == [97, 98, 32, 99, 100, 32, 101, 102]
+
+
+def _piece_starts(text: str, k: int):
+    starts, off = [], 0
+    for piece in _pieces(text, k):
+        starts.append(off)
+        off += len(piece.encode("utf-8"))
+    return starts
+
+
+def _encode_chunks(tok, data: bytes, starts):
+    from bpe_amd import _lib
+    arr = (ctypes.c_uint64 * max(len(starts), 1))(*starts)
+    out = (ctypes.c_uint32 * max(len(data), 1))()
+    n_out = ctypes.c_size_t(0)
+    _lib.check(_lib.lib().bpe_tok_encode_chunks(tok._device(), data, len(data), arr, len(starts), out,
+                                                len(data), ctypes.byref(n_out)))
+    return list(out[:n_out.value])
+
+
+@pytest.mark.parametrize("slab,region,k", [(65536, 100_000, 997), (65536, 1, 4096), (131072, 10 ** 9, 7),
+                                           (65536, 50_000, 10 ** 7)])
+def test_encode_file_overlapped_regions(tmp_path, monkeypatch, slab, region, k):
+    """the overlapped bulk path (file streamed in slabs, pieces validated, counted, encoded and
+    copied region by region) against one encode of the whole text cut at the same piece starts
+    (bpe_tok_encode_chunks, itself checked against the oracle above): small slabs and regions
+    put many region ends, slab ends and piece starts next to each other; a piece longer than a
+    region (k = 10^7) is encoded whole"""
+    from bpe_amd import Tokenizer
+    from bpe_amd.encode import encode_file, last_phases_ms
+    vocab, merges = gpt2_files.load_gpt2(["<|endoftext|>"])
+    tok = Tokenizer(dict(vocab), list(merges), ["<|endoftext|>"])
+    text = _mixed_text(11, 60000).replace("\r", "")
+    data = text.encode("utf-8")
+    assert len(data) > 2 * slab
+    src = tmp_path / "t.txt"
+    src.write_bytes(data)
+    want = _encode_chunks(tok, data, _piece_starts(text, k))
+    monkeypatch.setenv("BPE355_READ_SLAB", str(slab))
+    monkeypatch.setenv("BPE355_ENC_REGION", str(region))
+    got = encode_file(tok, src, chars_per_piece=k)
+    assert got.dtype == np.uint16 and got.tolist() == want
+    assert set(last_phases_ms) == {"read", "decode", "encode", "copy"}
+
+
+def test_encode_file_late_carriage_return_and_bad_utf8(tmp_path, monkeypatch):
+    """a carriage return first seen after regions were already encoded: the whole text is redone
+    with universal newlines; an ill-formed byte late in the file raises UnicodeDecodeError at its
+    position, as decoding the whole file does"""
+    from bpe_amd import Tokenizer
+    from bpe_amd.encode import encode_file
+    vocab, merges = gpt2_files.load_gpt2(["<|endoftext|>"])
+    tok = Tokenizer(dict(vocab), list(merges), ["<|endoftext|>"])
+    monkeypatch.setenv("BPE355_READ_SLAB", "65536")
+    monkeypatch.setenv("BPE355_ENC_REGION", "30000")
+    head = _mixed_text(12, 40000).replace("\r", "")
+    raw = (head + "tail\r\nmore\rend é").encode("utf-8")
+    src = tmp_path / "cr.txt"
+    src.write_bytes(raw)
+    with open(src, "r", encoding="utf-8") as f:
+        text = f.read()
+    k = 1500
+    want = _encode_chunks(tok, text.encode("utf-8"), _piece_starts(text, k))
+    assert encode_file(tok, src, chars_per_piece=k).tolist() == want
+    bad = bytearray(head.encode("utf-8"))
+    pos = len(bad) - 1000
+    while bad[pos] >= 0x80:   # an ASCII byte, replaced by a lone continuation byte
+        pos += 1
+    bad[pos] = 0x80
+    src.write_bytes(bytes(bad))
+    with pytest.raises(UnicodeDecodeError) as e:
+        encode_file(tok, src, chars_per_piece=k)
+    assert e.value.start == pos

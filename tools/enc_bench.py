@@ -1,7 +1,9 @@
 """Encode timing on the bench corpus in HBM (train 32k once, then Tokenizer.encode device to
 device 3 times): for A/B of encoder variants (BPE355_LIB)."""
 import ctypes, sys, time
-sys.path[:0] = ["transformer-lm_amd", "."]
+import os as _os
+_ROOT = _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))
+sys.path[:0] = [_os.path.join(_ROOT, "transformer-lm_amd"), _ROOT]
 import torch
 from bpe_amd import _lib, train_bpe_device, Tokenizer
 n = int(float(sys.argv[1])) if len(sys.argv) > 1 else 11_899_998_208

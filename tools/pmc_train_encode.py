@@ -2,7 +2,9 @@
 HBM (count, word table, merge loop: every kernel of a train step) and one encode of it with the
 result (the encoder's kernels), nothing else.  usage: python tools/pmc_train_encode.py [bytes]"""
 import ctypes, sys
-sys.path[:0] = ["transformer-lm_amd", "."]
+import os as _os
+_ROOT = _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))
+sys.path[:0] = [_os.path.join(_ROOT, "transformer-lm_amd"), _ROOT]
 import torch
 from bpe_amd import _lib, train_bpe_device, Tokenizer
 n = int(float(sys.argv[1])) // 4096 * 4096 if len(sys.argv) > 1 else 11_899_998_208

@@ -116,6 +116,14 @@ __device__ __forceinline__ T wave_max(T v) {
 }
 
 inline unsigned ceil_div(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
+// Workgroups for a grid-stride kernel over `items`: a dispatch's grid is at most 2^32 work-items
+// (the AQL packet's 32-bit grid size, which a larger launch silently wraps), so a kernel over
+// bytes or ids of a multi-GB text strides instead of launching one thread per item.
+constexpr size_t kMaxGridBlocks = 1u << 20;
+inline unsigned grid_for(size_t items, unsigned block) {
+    const size_t b = (items + block - 1) / block;
+    return (unsigned)(b < kMaxGridBlocks ? (b ? b : 1) : kMaxGridBlocks);
+}
 inline size_t next_pow2(size_t x) {
     size_t p = 1;
     while (p < x) p <<= 1;

@@ -36,28 +36,28 @@ constexpr uint64_t kMaxDecodeIds = 1ull << 28;   // dense table bound (vocab ids
 __global__ void k_dec_len(const uint32_t* __restrict__ ids, size_t n, const uint32_t* __restrict__ len,
                           uint64_t n_tab, unsigned long long* __restrict__ out_len,
                           unsigned long long* __restrict__ first_bad) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t id = ids[i];
-    const uint32_t l = id < n_tab ? len[id] : kNoId;
-    if (l == kNoId) {
-        atomicMin(first_bad, (unsigned long long)i);
-        out_len[i] = 0;
-        return;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t id = ids[i];
+        const uint32_t l = id < n_tab ? len[id] : kNoId;
+        if (l == kNoId) {
+            atomicMin(first_bad, (unsigned long long)i);
+            out_len[i] = 0;
+            continue;
+        }
+        out_len[i] = l;
     }
-    out_len[i] = l;
 }
 
 __global__ void k_dec_gather(const uint32_t* __restrict__ ids, size_t n, const unsigned long long* __restrict__ off,
                              const uint32_t* __restrict__ len, const uint8_t* __restrict__ pool,
                              const unsigned long long* __restrict__ out_off, uint8_t* __restrict__ out) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t id = ids[i];
-    const uint32_t l = len[id];
-    const uint8_t* src = pool + off[id];
-    uint8_t* dst = out + out_off[i];
-    for (uint32_t k = 0; k < l; ++k) dst[k] = src[k];
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t id = ids[i];
+        const uint32_t l = len[id];
+        const uint8_t* src = pool + off[id];
+        uint8_t* dst = out + out_off[i];
+        for (uint32_t k = 0; k < l; ++k) dst[k] = src[k];
+    }
 }
 
 template <class F>
@@ -83,7 +83,7 @@ size_t decode_device(bpe_decoder& D, const uint32_t* d_ids, size_t n, uint8_t* d
     DevBuf<unsigned long long> lens(n), offs(n), bad(1);
     const unsigned long long none = ~0ULL;
     BPE_HIP(hipMemcpyAsync(bad.p, &none, 8, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_dec_len, dim3(ceil_div(n, 256)), dim3(256), 0, s, d_ids, n, D.len.p, D.n_ids, lens.p,
+    hipLaunchKernelGGL(k_dec_len, dim3(grid_for(n, 256)), dim3(256), 0, s, d_ids, n, D.len.p, D.n_ids, lens.p,
                        bad.p);
     exclusive_sum(lens.p, offs.p, n, s);
     unsigned long long h[3];
@@ -99,7 +99,7 @@ size_t decode_device(bpe_decoder& D, const uint32_t* d_ids, size_t n, uint8_t* d
     const size_t total = (size_t)(h[0] + h[1]);
     *needed = total;
     BPE_REQUIRE(cap >= total, BPE_E_ARG, "decode output capacity too small");
-    hipLaunchKernelGGL(k_dec_gather, dim3(ceil_div(n, 256)), dim3(256), 0, s, d_ids, n, D.off.p, D.len.p,
+    hipLaunchKernelGGL(k_dec_gather, dim3(grid_for(n, 256)), dim3(256), 0, s, d_ids, n, D.off.p, D.len.p,
                        D.pool.p, offs.p, d_out);
     BPE_HIP(hipGetLastError());
     BPE_HIP(hipStreamSynchronize(s));

@@ -19,7 +19,10 @@
 //      occurrence's cached ids at its output offset, specials as their ids.
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -68,25 +71,97 @@ __device__ __forceinline__ bool bytes_eq(const uint8_t* x, const uint8_t* y, siz
 }
 
 // ------------------------------------------------------------------ 1. special candidates
+// Matches are appended as position << 16 | special index (sorted on the device afterwards).
+constexpr int kSpShift = 16;
+
 __global__ void k_find_specials(const uint8_t* __restrict__ s, size_t n, EncTables E,
                                 const unsigned* __restrict__ first_mask,
-                                unsigned long long* __restrict__ pos_out, int* __restrict__ sp_out,
+                                unsigned long long* __restrict__ key_out,
                                 unsigned* __restrict__ n_out, unsigned long long cap) {
     // Every special matching at i is recorded (sorted longest first, the host takes the first
     // that fits): when the longest one straddles a piece cut, re.split on that piece still
     // matches a shorter special that is its prefix (tokenizer.py:63-66).
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool cand = false;
-    if (i < n) {
-        const unsigned b = s[i];
-        cand = (first_mask[b >> 5] >> (b & 31)) & 1u;
+    // grid-stride over the text, the trip count uniform over the workgroup (wave_append needs
+    // every lane of the wave)
+    for (size_t b0 = (size_t)blockIdx.x * blockDim.x; b0 < n; b0 += (size_t)gridDim.x * blockDim.x) {
+        const size_t i = b0 + threadIdx.x;
+        bool cand = false;
+        if (i < n) {
+            const unsigned b = s[i];
+            cand = (first_mask[b >> 5] >> (b & 31)) & 1u;
+        }
+        if (!__any(cand)) continue;
+        for (int k = 0; k < E.n_sp; ++k) {
+            const unsigned l = E.sp_len[k];
+            const bool hit = cand && i + l <= n && bytes_eq(s + i, E.sp_bytes + E.sp_off[k], l);
+            const unsigned idx = wave_append(hit, n_out);
+            if (hit && idx < cap) key_out[idx] = ((unsigned long long)i << kSpShift) | (unsigned)k;
+        }
     }
-    if (!__any(cand)) return;
-    for (int k = 0; k < E.n_sp; ++k) {   // uniform trip count: wave_append needs every lane
-        const unsigned l = E.sp_len[k];
-        const bool hit = cand && i + l <= n && bytes_eq(s + i, E.sp_bytes + E.sp_off[k], l);
-        const unsigned idx = wave_append(hit, n_out);
-        if (hit && idx < cap) { pos_out[idx] = i; sp_out[idx] = k; }
+}
+
+// ------------------------------------------------------------------ 1'. segments on the device
+// The sorted matches (position << 16 | index) become the segment table without a host pass when
+// the matches that no piece cut splits (a cut strictly inside a match: re.split on the piece
+// cannot see it) do not overlap one another -- then re.split keeps every one of them.  Between
+// two kept specials (and before the first, after the last) the cuts split the normal text.
+// Overlapping matches (a special that overlaps itself or another) go to the host's
+// leftmost-longest resolution instead.
+__device__ __forceinline__ size_t cuts_le(const unsigned long long* __restrict__ cuts, size_t nc,
+                                          unsigned long long p) {   // how many cuts are <= p
+    size_t lo = 0, hi = nc;
+    while (lo < hi) {
+        const size_t mid = (lo + hi) >> 1;
+        if (cuts[mid] <= p) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void k_sp_eligible(const unsigned long long* __restrict__ keys, size_t m, const uint32_t* __restrict__ sp_len,
+                              const unsigned long long* __restrict__ cuts, size_t nc, uint8_t* __restrict__ elig) {
+    for (size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += (size_t)gridDim.x * blockDim.x) {
+        const unsigned long long p = keys[j] >> kSpShift, e = p + sp_len[keys[j] & 0xffffu];
+        const size_t i = cuts_le(cuts, nc, p);   // the first cut > p
+        elig[j] = (i == nc || cuts[i] >= e) ? 1 : 0;
+    }
+}
+
+// entry j <= me: the segments ending with special j (j == me: the tail after the last one)
+__global__ void k_sp_count(const unsigned long long* __restrict__ keys, size_t me, const uint32_t* __restrict__ sp_len,
+                           const unsigned long long* __restrict__ cuts, size_t nc, unsigned long long n,
+                           unsigned long long* __restrict__ cnt, unsigned* __restrict__ conflict) {
+    for (size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x; j <= me; j += (size_t)gridDim.x * blockDim.x) {
+        unsigned long long prev = 0;
+        if (j > 0) prev = (keys[j - 1] >> kSpShift) + sp_len[keys[j - 1] & 0xffffu];
+        const unsigned long long p = j < me ? keys[j] >> kSpShift : n;
+        if (p < prev) atomicOr(conflict, 1u);
+        unsigned long long c = j < me ? 1 : 0;
+        if (prev < p) c += 1 + (cuts_le(cuts, nc, p - 1) - cuts_le(cuts, nc, prev));   // cuts in (prev, p)
+        cnt[j] = c;
+    }
+}
+
+__global__ void k_sp_emit(const unsigned long long* __restrict__ keys, size_t me, const uint32_t* __restrict__ sp_len,
+                          const unsigned long long* __restrict__ cuts, size_t nc, unsigned long long n,
+                          const unsigned long long* __restrict__ off, Seg* __restrict__ segs) {
+    for (size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x; j <= me; j += (size_t)gridDim.x * blockDim.x) {
+        unsigned long long prev = 0;
+        if (j > 0) prev = (keys[j - 1] >> kSpShift) + sp_len[keys[j - 1] & 0xffffu];
+        const unsigned long long p = j < me ? keys[j] >> kSpShift : n;
+        unsigned long long o = off[j];
+        if (prev < p) {
+            unsigned long long start = prev;
+            for (size_t i = cuts_le(cuts, nc, prev); i < nc && cuts[i] < p; ++i) {
+                segs[o++] = Seg{start, cuts[i], -1, 0};
+                start = cuts[i];
+            }
+            segs[o++] = Seg{start, p, -1, 0};
+        }
+        if (j < me) {
+            const unsigned k = (unsigned)(keys[j] & 0xffffu);
+            segs[o] = Seg{p, p + sp_len[k], (int)k, 0};
+        }
     }
 }
 
@@ -744,6 +819,9 @@ struct bpe_tokenizer {
         bpe::DevBuf<unsigned long long> t_start, fill, kv, pos, w_off, len64, idoff, slot_info, per, per_off;
         bpe::DevBuf<unsigned> status, d_nw;
         bpe::DevBuf<bpe::Seg> segs;
+        bpe::DevBuf<unsigned long long> sp_key, sp_sorted;   // special matches, (position << 16 | index)
+        bpe::DevBuf<unsigned long long> sp_cnt, sp_off, cuts;   // the device segment builder's arrays
+        bpe::DevBuf<uint8_t> sp_flag;
         bpe::DevBuf<uint8_t> tmp;
         bpe::DevBuf<uint16_t> ids16;
         bpe::DevBuf<uint8_t> text, text2;   // the bulk encoder's file bytes (and its newline-translated copy)
@@ -888,43 +966,75 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
     for (unsigned long long c : cuts_in)
         if (c > 0 && c < n && (cuts.empty() || c > cuts.back())) cuts.push_back(c);
     EncTables E = T.tables();
-    // 1. segments
-    std::vector<Seg> segs;
-    {
-        unsigned long long cnt = 0;
-        std::vector<unsigned long long> pos;
-        std::vector<int> spk;
-        if (!T.specials.empty()) {
-            unsigned long long cap = std::max<unsigned long long>(1024, n / 64);
-            for (;;) {
-                DevBuf<unsigned long long> d_pos(cap);
-                DevBuf<unsigned> d_n(1);
-                DevBuf<int> d_sp(cap);
-                BPE_HIP(hipMemsetAsync(d_n.p, 0, 4, s));
-                hipLaunchKernelGGL(k_find_specials, dim3(ceil_div(n, 256)), dim3(256), 0, s, d_text, n, E,
-                                   T.first_mask.p, d_pos.p, d_sp.p, d_n.p, cap);
+    // 1. segments: every special match (k_find_specials), sorted on the device by (position,
+    // index) -- by position, longest first (T.specials is longest first) -- then built into the
+    // segment table on the device (k_sp_*), or left to right here when matches overlap
+    auto& S = T.sc;
+    DevBuf<Seg>& d_segs = S.segs;
+    int nseg = 0;
+    bool on_device = false;
+    std::vector<unsigned long long> keys;
+    if (!T.specials.empty()) {
+        BPE_REQUIRE(T.specials.size() < (1u << kSpShift) && (n >> (64 - kSpShift)) == 0, BPE_E_LIMIT,
+                    "too many special tokens or too long a text");
+        unsigned long long cap = std::max<unsigned long long>(1024, n / 64);
+        S.status.reserve(1);
+        unsigned cnt32 = 0;
+        for (;;) {
+            S.sp_key.reserve(cap);
+            BPE_HIP(hipMemsetAsync(S.status.p, 0, 4, s));
+            hipLaunchKernelGGL(k_find_specials, dim3(grid_for(n, 256)), dim3(256), 0, s, d_text, n, E,
+                               T.first_mask.p, S.sp_key.p, S.status.p, cap);
+            BPE_HIP(hipGetLastError());
+            to_host(&cnt32, S.status.p, 4, s);
+            if (cnt32 <= cap) break;
+            cap = cnt32;
+        }
+        if (cnt32) {
+            S.sp_sorted.reserve(cnt32);
+            unsigned bits = kSpShift;
+            while (bits < 64 && (n >> (bits - kSpShift)) != 0) ++bits;
+            radix_sort_keys(S.sp_key.p, S.sp_sorted.p, cnt32, bits, s, &S.tmp);
+            const size_t nc = cuts.size();
+            S.cuts.reserve(std::max<size_t>(nc, 1));
+            if (nc) to_device(S.cuts.p, cuts.data(), nc * 8, s);
+            // the matches no cut splits, in order (into sp_key)
+            S.sp_flag.reserve(cnt32);
+            S.sp_off.reserve(2);
+            hipLaunchKernelGGL(k_sp_eligible, dim3(grid_for(cnt32, 256)), dim3(256), 0, s, S.sp_sorted.p,
+                               (size_t)cnt32, E.sp_len, S.cuts.p, nc, S.sp_flag.p);
+            select_flagged(S.sp_sorted.p, S.sp_flag.p, S.sp_key.p, S.sp_off.p, cnt32, s);
+            unsigned long long me = 0;
+            to_host(&me, S.sp_off.p, 8, s);
+            // segments per kept special (and the tail), their offsets, overlap check
+            S.sp_cnt.reserve(me + 1);
+            S.sp_off.reserve(me + 1);
+            BPE_HIP(hipMemsetAsync(S.status.p, 0, 4, s));
+            hipLaunchKernelGGL(k_sp_count, dim3(grid_for(me + 1, 256)), dim3(256), 0, s, S.sp_key.p, (size_t)me,
+                               E.sp_len, S.cuts.p, nc, (unsigned long long)n, S.sp_cnt.p, S.status.p);
+            exclusive_sum(S.sp_cnt.p, S.sp_off.p, (size_t)me + 1, s, &S.tmp);
+            unsigned conflict = 0;
+            unsigned long long last[2];
+            to_host(&conflict, S.status.p, 4, s);
+            to_host(&last[0], S.sp_off.p + me, 8, s);
+            to_host(&last[1], S.sp_cnt.p + me, 8, s);
+            if (!conflict) {
+                const unsigned long long total = last[0] + last[1];
+                BPE_REQUIRE(total < (1ull << 31), BPE_E_LIMIT, "too many segments (special tokens and pieces)");
+                nseg = (int)total;
+                d_segs.reserve(std::max(nseg, 1));
+                hipLaunchKernelGGL(k_sp_emit, dim3(grid_for(me + 1, 256)), dim3(256), 0, s, S.sp_key.p, (size_t)me,
+                                   E.sp_len, S.cuts.p, nc, (unsigned long long)n, S.sp_off.p, d_segs.p);
                 BPE_HIP(hipGetLastError());
-                unsigned cnt32 = 0;
-                BPE_HIP(hipMemcpyAsync(&cnt32, d_n.p, 4, hipMemcpyDeviceToHost, s));
-                BPE_HIP(hipStreamSynchronize(s));
-                cnt = cnt32;
-                BPE_HIP(hipStreamSynchronize(s));
-                if (cnt > cap) { cap = cnt; continue; }
-                pos.resize(cnt);
-                spk.resize(cnt);
-                if (cnt) {
-                    BPE_HIP(hipMemcpyAsync(pos.data(), d_pos.p, cnt * 8, hipMemcpyDeviceToHost, s));
-                    BPE_HIP(hipMemcpyAsync(spk.data(), d_sp.p, cnt * 4, hipMemcpyDeviceToHost, s));
-                    BPE_HIP(hipStreamSynchronize(s));
-                }
-                break;
+                on_device = true;
+            } else {
+                keys.resize(cnt32);
+                to_host(keys.data(), S.sp_sorted.p, (size_t)cnt32 * 8, s);
             }
         }
-        std::vector<size_t> order(cnt);
-        for (size_t i = 0; i < cnt; ++i) order[i] = i;
-        std::sort(order.begin(), order.end(), [&](size_t x, size_t y) {   // by position, longest first
-            return pos[x] < pos[y] || (pos[x] == pos[y] && spk[x] < spk[y]);
-        });
+    }
+    if (!on_device) {   // leftmost, non-overlapping (re.split), cut by the pieces
+        std::vector<Seg> segs;
         unsigned long long cur = 0;
         size_t ci = 0;
         auto cut_until = [&](unsigned long long upto) {   // normal segments ended by cuts <= upto
@@ -933,24 +1043,24 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
                 cur = std::max(cur, cuts[ci]);
             }
         };
-        for (size_t oi : order) {  // leftmost, non-overlapping (re.split)
-            const unsigned long long p0 = pos[oi];
+        for (const unsigned long long key : keys) {
+            const unsigned long long p0 = key >> kSpShift;
+            const int sk = (int)(key & ((1u << kSpShift) - 1));
             if (p0 < cur) continue;
-            const unsigned long long e = p0 + T.specials[spk[oi]].size();
+            const unsigned long long e = p0 + T.specials[sk].size();
             cut_until(p0);
             if (ci < cuts.size() && cuts[ci] < e) continue;   // straddles a cut: a shorter one at p0 may fit
             if (p0 > cur) segs.push_back(Seg{cur, p0, -1, 0});
-            segs.push_back(Seg{p0, e, spk[oi], 0});
+            segs.push_back(Seg{p0, e, sk, 0});
             cur = e;
         }
         cut_until(n);
         if (cur < n) segs.push_back(Seg{cur, n, -1, 0});
+        BPE_REQUIRE(segs.size() < (1ull << 31), BPE_E_LIMIT, "too many segments (special tokens and pieces)");
+        nseg = (int)segs.size();
+        d_segs.reserve(std::max(nseg, 1));
+        to_device(d_segs.p, segs.data(), nseg * sizeof(Seg), s);
     }
-    const int nseg = (int)segs.size();
-    auto& S = T.sc;
-    DevBuf<Seg>& d_segs = S.segs;
-    d_segs.reserve(std::max(nseg, 1));
-    BPE_HIP(hipMemcpyAsync(d_segs.p, segs.data(), nseg * sizeof(Seg), hipMemcpyHostToDevice, s));
 
     // 2. one staged pass: unique pre-tokens into the word table, one record per pre-token
     const size_t n_chunks = (n + kChunk - 1) / kChunk;
@@ -991,8 +1101,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
                            std::getenv("BPE355_NOCACHE") ? 0 : 1);   // test knob: global table only
         BPE_HIP(hipGetLastError());
         unsigned st = 0;
-        BPE_HIP(hipMemcpyAsync(&st, status.p, 4, hipMemcpyDeviceToHost, s));
-        BPE_HIP(hipStreamSynchronize(s));
+        to_host(&st, status.p, 4, s);
         if (st & 2u) throw Error{BPE_E_LIMIT, "a pre-token is longer than 16 MiB"};
         BPE_REQUIRE(!(st & 16u), BPE_E_HIP, "internal error: encode scan overran a span");
         if (!(st & 1u)) break;
@@ -1010,8 +1119,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
     hipLaunchKernelGGL(k_collect, dim3(ceil_div(cap, 256)), dim3(256), 0, s, kv.p, pos.p, cap, w_slot.p,
                        w_off.p, w_len.p, d_nw.p);
     unsigned nw = 0;
-    BPE_HIP(hipMemcpyAsync(&nw, d_nw.p, 4, hipMemcpyDeviceToHost, s));
-    BPE_HIP(hipStreamSynchronize(s));
+    to_host(&nw, d_nw.p, 4, s);
 
     // 3. encode each unique word once
     DevBuf<unsigned long long>&len64 = S.len64, &idoff = S.idoff;
@@ -1025,9 +1133,8 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
         hipLaunchKernelGGL(k_word_len64, dim3(ceil_div(nw, 256)), dim3(256), 0, s, w_len.p, nw, len64.p);
         exclusive_sum(len64.p, idoff.p, nw, s, &S.tmp);
         unsigned long long last[2];
-        BPE_HIP(hipMemcpyAsync(&last[0], idoff.p + nw - 1, 8, hipMemcpyDeviceToHost, s));
-        BPE_HIP(hipMemcpyAsync(&last[1], len64.p + nw - 1, 8, hipMemcpyDeviceToHost, s));
-        BPE_HIP(hipStreamSynchronize(s));
+        to_host(&last[0], idoff.p + nw - 1, 8, s);
+        to_host(&last[1], len64.p + nw - 1, 8, s);
         pool_n = last[0] + last[1];
     }
     DevBuf<uint32_t>& pool = S.pool;
@@ -1047,10 +1154,9 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
     exclusive_sum(per.p, per_off.p, n_spans, s, &S.tmp);
     unsigned long long last[2];
     unsigned st = 0;
-    BPE_HIP(hipMemcpyAsync(&last[0], per_off.p + n_spans - 1, 8, hipMemcpyDeviceToHost, s));
-    BPE_HIP(hipMemcpyAsync(&last[1], per.p + n_spans - 1, 8, hipMemcpyDeviceToHost, s));
-    BPE_HIP(hipMemcpyAsync(&st, status.p, 4, hipMemcpyDeviceToHost, s));
-    BPE_HIP(hipStreamSynchronize(s));
+    to_host(&last[0], per_off.p + n_spans - 1, 8, s);
+    to_host(&last[1], per.p + n_spans - 1, 8, s);
+    to_host(&st, status.p, 4, s);
     if (st & 4u) throw Error{BPE_E_KEY, "a merged token is not in the vocab"};
     BPE_REQUIRE(!(st & 112u), BPE_E_HIP, "internal error: encode records inconsistent (status " +
                                            std::to_string(st) + ")");
@@ -1061,8 +1167,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
                        t_count.p, n_spans, slot_info.p, pool.p, E.sp_vid, per.p, per_off.p, cap, d_out, status.p);
     BPE_HIP(hipGetLastError());
     if (sizeof(OutT) == 2) {
-        BPE_HIP(hipMemcpyAsync(&st, status.p, 4, hipMemcpyDeviceToHost, s));
-        BPE_HIP(hipStreamSynchronize(s));
+        to_host(&st, status.p, 4, s);
         BPE_REQUIRE(!(st & 128u), BPE_E_LIMIT, "a token id does not fit np.uint16 (vocab larger than 65536)");
     }
     BPE_HIP(hipStreamSynchronize(s));
@@ -1155,11 +1260,6 @@ size_t encode_gpus(bpe_tokenizer& T, const uint8_t* utf8, size_t n, uint32_t* id
     return m;
 }
 
-// a C-ABI call of this library, inside another: its failure as an Error (message kept)
-void check_rc(int rc) {
-    if (rc != BPE_OK) throw Error{rc, bpe_last_error(), bpe_last_errno()};
-}
-
 template <class F>
 int guarded_enc(F&& f) {
     try {
@@ -1173,6 +1273,204 @@ int guarded_enc(F&& f) {
         set_error(BPE_E_NOMEM, "host allocation failed");
         return BPE_E_NOMEM;
     }
+}
+
+// ------------------------------------------------------------------ file -> uint16 ids, overlapped
+// encode.py:31-37 for a regular file.  A reader thread streams the file into HBM in kReadSlab
+// slabs; as they land, the main thread validates the loaded prefix (strict UTF-8, exactly as one
+// pass over the whole text), counts its characters to place the piece starts (every
+// chars_per_piece-th character, f.read(K)), encodes the pieces that are complete and validated
+// straight to uint16 in the tokenizer's kept buffer, and hands their ids to a copier thread that
+// moves them into ids_out while the next region is read and encoded.  A text with a carriage
+// return (universal newlines move every later piece start) is redone in one serial pass once
+// it has been read.  phase_ms: busy time of the reader, of validation + counting, of the encodes
+// and of the copier (they overlap).
+constexpr size_t kReadSlab = 1ull << 30;        // a multiple of the counting block (64 KiB)
+constexpr size_t kMaxRegion = 3ull << 30;       // bytes one encode takes at most (the copy tail)
+
+size_t env_size(const char* name, size_t dflt) {   // test knobs: small slabs and regions
+    const char* e = std::getenv(name);
+    const long long v = e ? std::atoll(e) : 0;
+    return v > 0 ? (size_t)v : dflt;
+}
+
+size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint16_t* ids_out, size_t cap, int dev,
+                             double* ph) {
+    using clk = std::chrono::steady_clock;
+    auto since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+    auto& S = T.sc;
+    const hipStream_t s = T.stream;
+    const size_t n = src.size;
+    if (n == 0) return 0;
+    const size_t read_slab = std::max<size_t>(1, env_size("BPE355_READ_SLAB", kReadSlab) >> 16) << 16;
+    const size_t max_region = env_size("BPE355_ENC_REGION", kMaxRegion);
+    // per-region lines (range, ids, pieces, ms) appended to the file BPE355_ENC_TRACE names
+    const char* trace_path = std::getenv("BPE355_ENC_TRACE");
+    FILE* const trace = trace_path ? std::fopen(trace_path, "a") : nullptr;
+    struct Closer { FILE* f; ~Closer() { if (f) std::fclose(f); } } trace_closer{trace};
+    S.text.reserve(n);
+    S.ids16.reserve(n);   // ids <= bytes
+    uint8_t* const text = S.text.p;
+
+    // reader
+    std::mutex m;
+    std::condition_variable cv;
+    size_t loaded = 0;
+    bool read_done = false;
+    std::atomic<bool> stop{false};   // an error downstream: read no further
+    std::exception_ptr read_err;
+    // reader and copier threads: fewer than the trainer's loader uses, so the encode's host side
+    // (segment table, launches, read-backs) keeps a core (measured at 11.9 GB: 4 threads each
+    // 593-648 ms per call, 8: 713-749, 16: 810-858)
+    const int io_n = (int)env_size("BPE355_ENC_IO_THREADS", 4);
+    // experiment knob: BPE355_ENC_OVERLAP=0 reads the whole file before the first encode
+    const char* ov = std::getenv("BPE355_ENC_OVERLAP");
+    const bool overlap_read = !(ov && ov[0] == '0');
+    std::thread reader([&] {
+        const auto t0 = clk::now();
+        try {
+            for (size_t off = 0; off < n && !stop.load(); off += read_slab) {
+                const size_t len = std::min(read_slab, n - off);
+                stage_to_device(src, off, len, text + off, dev, io_n);
+                std::lock_guard<std::mutex> g(m);
+                loaded = off + len;
+                cv.notify_all();
+            }
+        } catch (...) {
+            std::lock_guard<std::mutex> g(m);
+            read_err = std::current_exception();
+        }
+        std::lock_guard<std::mutex> g(m);
+        read_done = true;
+        ph[0] = since(t0);
+        cv.notify_all();
+    });
+    // copier: one region at a time
+    std::thread copier;
+    std::exception_ptr copy_err;
+    auto copy_wait = [&] {
+        if (copier.joinable()) copier.join();
+        if (copy_err) std::rethrow_exception(copy_err);
+    };
+    auto copy_start = [&](size_t at, size_t cnt) {
+        copy_wait();
+        copier = std::thread([&, at, cnt] {
+            const auto t0 = clk::now();
+            try {
+                device_to_host(reinterpret_cast<const uint8_t*>(S.ids16.p + at), 2 * cnt,
+                               reinterpret_cast<uint8_t*>(ids_out + at), dev, io_n);
+            } catch (...) {
+                copy_err = std::current_exception();
+            }
+            ph[3] += since(t0);
+        });
+    };
+    auto finish_threads = [&] {
+        stop.store(true);
+        {
+            std::unique_lock<std::mutex> g(m);
+            cv.wait(g, [&] { return read_done; });
+        }
+        if (reader.joinable()) reader.join();
+        if (copier.joinable()) copier.join();
+    };
+
+    size_t k_done = 0;
+    bool serial = false;   // a carriage return: redo in one pass
+    try {
+        ValidatePass V;
+        V.begin(text, n, s);
+        std::vector<uint64_t> starts;      // piece starts found so far (global offsets)
+        size_t counted = 0, enc_done = 0, next_piece = 1;   // starts[0] == 0
+        uint64_t chars = 0;
+        size_t seen = 0;
+        while (enc_done < n) {
+            size_t L;
+            {
+                std::unique_lock<std::mutex> g(m);
+                cv.wait(g, [&] { return (overlap_read && loaded > seen) || read_done; });
+                if (read_err) std::rethrow_exception(read_err);
+                L = loaded;
+            }
+            seen = L;
+            const auto t1 = clk::now();
+            const size_t vend = V.prefix(L);
+            const size_t cend = L == n ? n : L / 65536 * 65536;
+            if (cend > counted) {
+                chars += piece_starts_range(text + counted, cend - counted, K, chars, counted, s, starts);
+                counted = cend;
+            }
+            unsigned long long err = 0;
+            bool cr = false;
+            V.finish(&err, &cr);
+            ph[1] += since(t1);
+            if (err != ~0ULL)
+                throw Error{BPE_E_UTF8, "'utf-8' codec can't decode byte at position " + std::to_string(err)};
+            if (cr) { serial = true; break; }
+            // encode the complete pieces inside the validated and counted prefix, at most
+            // kMaxRegion at a time, each region ending at a piece start (or the end)
+            const size_t ready = std::min(vend, counted);
+            auto region_end = [&](size_t from) -> size_t {
+                if (ready == n && n - from <= max_region) return n;
+                size_t lim = from;
+                for (size_t i = next_piece; i < starts.size() && starts[i] <= std::min(ready, from + max_region); ++i)
+                    lim = starts[i];
+                if (lim == from && ready == n)   // a piece longer than kMaxRegion: whole
+                    lim = next_piece < starts.size() ? starts[next_piece] : n;
+                return lim;
+            };
+            for (size_t e_end = region_end(enc_done); e_end > enc_done; e_end = region_end(enc_done)) {
+                std::vector<unsigned long long> cuts;
+                for (; next_piece < starts.size() && starts[next_piece] < e_end; ++next_piece)
+                    cuts.push_back(starts[next_piece] - enc_done);
+                if (next_piece < starts.size() && starts[next_piece] == e_end) ++next_piece;
+                const auto t2 = clk::now();
+                const size_t kk = encode_device(T, text + enc_done, e_end - enc_done, S.ids16.p + k_done, s, cuts);
+                const double ems = since(t2);
+                ph[2] += ems;
+                if (trace) {
+                    std::fprintf(trace, "region %zu %zu ids %zu pieces %zu ms %.1f loaded %zu\n", enc_done, e_end, kk,
+                                 cuts.size() + 1, ems, seen);
+                    std::fflush(trace);
+                }
+                BPE_REQUIRE(k_done + kk <= cap, BPE_E_ARG, "ids_out holds " + std::to_string(cap) +
+                                                              " ids, the file encodes to more");
+                copy_start(k_done, kk);
+                k_done += kk;
+                enc_done = e_end;
+            }
+        }
+        copy_wait();
+    } catch (...) {
+        finish_threads();
+        throw;
+    }
+    if (serial) {   // the rest of the file first
+        std::unique_lock<std::mutex> g(m);
+        cv.wait(g, [&] { return read_done; });
+        if (read_err) std::rethrow_exception(read_err);
+    }
+    finish_threads();
+    if (copy_err) std::rethrow_exception(copy_err);
+    if (!serial) return k_done;
+
+    // universal newlines: one pass over the whole text, as read
+    const auto t1 = clk::now();
+    size_t mlen = 0;
+    const uint8_t* t2 = prepare_text(text, n, S.text2, &mlen, s);
+    const std::vector<uint64_t> starts = utf8_piece_starts(t2, mlen, K, s);
+    ph[1] += since(t1);
+    const auto te = clk::now();
+    const std::vector<unsigned long long> cuts(starts.begin(), starts.end());
+    const size_t kk = mlen ? encode_device(T, t2, mlen, S.ids16.p, s, cuts) : 0;
+    ph[2] += since(te);
+    BPE_REQUIRE(kk <= cap, BPE_E_ARG, "ids_out holds " + std::to_string(cap) + " ids, the file encodes to " +
+                                         std::to_string(kk));
+    const auto tc = clk::now();
+    if (kk) device_to_host(reinterpret_cast<const uint8_t*>(S.ids16.p), 2 * kk, reinterpret_cast<uint8_t*>(ids_out),
+                           dev, io_threads());
+    ph[3] += since(tc);
+    return kk;
 }
 
 }  // namespace
@@ -1252,43 +1550,12 @@ int bpe_tok_encode_file_u16(bpe_tokenizer* tok, const char* path, size_t chars_p
     return bpe::guarded_enc([&] {
         BPE_REQUIRE(tok && path && n_out && chars_per_piece > 0, BPE_E_ARG, "NULL argument");
         *n_out = 0;
-        using clk = std::chrono::steady_clock;
-        auto ms = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
         double ph[4] = {0, 0, 0, 0};
-        auto t0 = clk::now();
         const bpe::Source src = bpe::Source::open_path(path);   // FileNotFoundError etc. before the GPU
         int dev = 0;
         BPE_HIP(hipGetDevice(&dev));
-        auto& S = tok->sc;
-        const hipStream_t s = tok->stream;
-        const size_t n = src.size;
-        S.text.reserve(std::max<size_t>(n, 1));
-        bpe::stage_to_device(src, 0, n, S.text.p, dev, bpe::io_threads());
-        ph[0] = ms(t0);
-        auto t1 = clk::now();
-        size_t m = 0;
-        const uint8_t* text = n ? bpe::prepare_text(S.text.p, n, S.text2, &m, s) : S.text.p;
-        // where each chars_per_piece-character piece starts (encode.py:31-33 f.read(K))
-        size_t ns = 0;
-        std::vector<uint64_t> starts;
-        if (m) {
-            bpe::check_rc(bpe_utf8_chunk_starts_device(text, m, chars_per_piece, nullptr, 0, &ns, s));
-            starts.resize(ns);
-            bpe::check_rc(bpe_utf8_chunk_starts_device(text, m, chars_per_piece, starts.data(), ns, &ns, s));
-        }
-        ph[1] = ms(t1);
-        auto t2 = clk::now();
-        S.ids16.reserve(std::max<size_t>(m, 1));
-        const std::vector<unsigned long long> cuts(starts.begin(), starts.end());
-        const size_t k = m ? bpe::encode_device(*tok, text, m, S.ids16.p, s, cuts) : 0;
-        ph[2] = ms(t2);
+        const size_t k = bpe::encode_file_pipelined(*tok, src, chars_per_piece, ids_out, cap, dev, ph);
         *n_out = k;
-        BPE_REQUIRE(k <= cap, BPE_E_ARG, "ids_out holds " + std::to_string(cap) + " ids, the file encodes to " +
-                                             std::to_string(k));
-        auto t3 = clk::now();
-        if (k) bpe::device_to_host(reinterpret_cast<const uint8_t*>(S.ids16.p), 2 * k,
-                                   reinterpret_cast<uint8_t*>(ids_out), dev, bpe::io_threads());
-        ph[3] = ms(t3);
         if (phase_ms) std::memcpy(phase_ms, ph, sizeof(ph));
     });
 }

@@ -24,12 +24,26 @@ struct Comm {
     virtual void allgather_bytes(const void* d_send, size_t bytes, void* d_recv, hipStream_t stream);
 };
 
+// ---------------------------------------------------------------- small transfers (hostio.hip)
+// host <- device and device <- host through a pinned device-mapped buffer moved by a kernel (no
+// copy-engine queue, so they do not wait behind bulk DMA); return once the bytes have arrived
+void to_host(void* dst, const void* d_src, size_t bytes, hipStream_t stream);
+void to_device(void* d_dst, const void* src, size_t bytes, hipStream_t stream);
+
 // ---------------------------------------------------------------- text preparation
 // Validates strict UTF-8 and applies universal newlines (reference train.py:22 text-mode
 // read).  Returns the device pointer to use (d_in itself when no \r is present, else
 // `scratch`) and the resulting length.  Throws Error{BPE_E_UTF8} on bad input.
 const uint8_t* prepare_text(const uint8_t* d_in, size_t n, DevBuf<uint8_t>& scratch,
                             size_t* n_out, hipStream_t stream);
+
+// Byte offsets of characters 0, k, 2k, ... of the UTF-8 text d_text[0, n) (io.hip): where the
+// pieces f.read(k) returns begin (reference encode.py:31-33).
+std::vector<uint64_t> utf8_piece_starts(const uint8_t* d_text, size_t n, size_t k, hipStream_t stream);
+// The same over a range of a longer text whose first character is character c_base: appends the
+// starts found (plus `offset`) to out, returns the range's character count.
+uint64_t piece_starts_range(const uint8_t* d_text, size_t n, size_t k, uint64_t c_base, uint64_t offset,
+                            hipStream_t stream, std::vector<uint64_t>& out);
 
 // ---------------------------------------------------------------- unique-word count
 struct WordCounts {
@@ -85,6 +99,10 @@ struct ValidatePass {
     hipStream_t s = nullptr;
     void begin(const uint8_t* d_text, size_t n, hipStream_t stream);
     void range(size_t lo, size_t hi);
+    // the units not yet validated whose windows lie inside the loaded prefix [0, loaded) of a
+    // text that ends at `total` (all of them once loaded == total); returns the validated end
+    size_t prefix(size_t loaded);
+    size_t done_units = 0;
     void finish(unsigned long long* err_pos, bool* has_cr);   // err_pos ~0: none
 };
 

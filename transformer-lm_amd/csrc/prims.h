@@ -40,6 +40,18 @@ void radix_sort_pairs(const K* kin, K* kout, const V* vin, V* vout, size_t n, un
     BPE_HIP(rocprim::radix_sort_pairs(tmp.p, tb, kin, kout, vin, vout, n, 0u, end_bit, s));
 }
 
+// keys sorted by the bits [0, end_bit)
+template <class K>
+void radix_sort_keys(const K* kin, K* kout, size_t n, unsigned end_bit, hipStream_t s, DevBuf<uint8_t>* keep = nullptr) {
+    if (n == 0) return;
+    DevBuf<uint8_t> local;
+    DevBuf<uint8_t>& tmp = keep ? *keep : local;
+    size_t tb = 0;
+    BPE_HIP(rocprim::radix_sort_keys(nullptr, tb, kin, kout, n, 0u, end_bit, s));
+    tmp.reserve(std::max<size_t>(tb, 1));
+    BPE_HIP(rocprim::radix_sort_keys(tmp.p, tb, kin, kout, n, 0u, end_bit, s));
+}
+
 // out = the in[i] with flags[i] != 0, in order; *d_count = how many (device)
 template <class T, class F, class C>
 void select_flagged(const T* in, const F* flags, T* out, C* d_count, size_t n, hipStream_t s) {

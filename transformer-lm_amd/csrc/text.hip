@@ -69,9 +69,8 @@ constexpr int kValidateBytes = 16;
 // text taken to end at n.  A segment of a corpus that is still arriving validates its units
 // with n = the segment's end, a safe split point: its last byte is ASCII, so no well-formed
 // sequence crosses it and an ill-formed one is ill-formed whatever follows.
-__global__ void k_validate(const uint8_t* __restrict__ s, size_t n, size_t u0, size_t u1,
-                           unsigned long long* __restrict__ err_pos, unsigned* __restrict__ has_cr) {
-    const size_t t = u0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void validate_unit(const uint8_t* __restrict__ s, size_t n, size_t t, size_t u1,
+                                              unsigned long long* __restrict__ err_pos, unsigned* __restrict__ has_cr) {
     const size_t lo = t * kValidateBytes;
     if (t >= u1 || lo >= n) return;
     bool cr = false;
@@ -92,7 +91,8 @@ __global__ void k_validate(const uint8_t* __restrict__ s, size_t n, size_t u0, s
         uint32_t prev = __shfl_up(w[3], 1), next = __shfl_down(w[0], 1);
         if (!hi_bits) return;                                       // all ASCII: done
         if (lane == 0) prev = lo >= 4 ? *reinterpret_cast<const uint32_t*>(s + lo - 4) : 0u;
-        if (lane == 63 || lo + 2 * kValidateBytes > n) {   // the next unit is not a full one in a lane
+        // the next unit is not a full one in a lane (past the text, the wave or the launch's range)
+        if (lane == 63 || t + 1 >= u1 || lo + 2 * kValidateBytes > n) {
             next = 0;
             for (int k = 0; k < 4 && lo + kValidateBytes + k < n; ++k) next |= (uint32_t)s[lo + kValidateBytes + k] << (8 * k);
         }
@@ -164,14 +164,22 @@ __global__ void k_validate(const uint8_t* __restrict__ s, size_t n, size_t u0, s
     if (cr) atomicOr(has_cr, 1u);
 }
 
+// grid-stride over the units, whole workgroups per step (the unit body exchanges neighbours
+// between lanes)
+__global__ void k_validate(const uint8_t* __restrict__ s, size_t n, size_t u0, size_t u1,
+                           unsigned long long* __restrict__ err_pos, unsigned* __restrict__ has_cr) {
+    for (size_t b0 = u0 + (size_t)blockIdx.x * blockDim.x; b0 < u1; b0 += (size_t)gridDim.x * blockDim.x)
+        validate_unit(s, n, b0 + threadIdx.x, u1, err_pos, has_cr);
+}
+
 // universal newlines: "\r\n" -> "\n", lone "\r" -> "\n"
 __global__ void k_newline_map(const uint8_t* __restrict__ s, size_t n, uint8_t* __restrict__ out,
                               uint8_t* __restrict__ keep) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint8_t b = s[i];
-    out[i] = (b == 0x0D) ? 0x0A : b;
-    keep[i] = !(b == 0x0D && i + 1 < n && s[i + 1] == 0x0A);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const uint8_t b = s[i];
+        out[i] = (b == 0x0D) ? 0x0A : b;
+        keep[i] = !(b == 0x0D && i + 1 < n && s[i + 1] == 0x0A);
+    }
 }
 
 const uint8_t* prepare_text(const uint8_t* d_in, size_t n, DevBuf<uint8_t>& scratch,
@@ -179,28 +187,26 @@ const uint8_t* prepare_text(const uint8_t* d_in, size_t n, DevBuf<uint8_t>& scra
     *n_out = n;
     if (n == 0) return d_in;
     DevBuf<unsigned long long> flags(2);
-    unsigned long long h_init[2] = {~0ULL, 0ULL};
-    BPE_HIP(hipMemcpyAsync(flags.p, h_init, sizeof(h_init), hipMemcpyHostToDevice, stream));
+    const unsigned long long h_init[2] = {~0ULL, 0ULL};
+    to_device(flags.p, h_init, sizeof(h_init), stream);
     const size_t threads = (n + kValidateBytes - 1) / kValidateBytes;
-    hipLaunchKernelGGL(k_validate, dim3(ceil_div(threads, 256)), dim3(256), 0, stream, d_in, n,
+    hipLaunchKernelGGL(k_validate, dim3(grid_for(threads, 256)), dim3(256), 0, stream, d_in, n,
                        (size_t)0, threads, flags.p, reinterpret_cast<unsigned*>(flags.p + 1));
     BPE_HIP(hipGetLastError());
     unsigned long long h[2];
-    BPE_HIP(hipMemcpyAsync(h, flags.p, sizeof(h), hipMemcpyDeviceToHost, stream));
-    BPE_HIP(hipStreamSynchronize(stream));
+    to_host(h, flags.p, sizeof(h), stream);
     if (h[0] != ~0ULL)
         throw Error{BPE_E_UTF8, "'utf-8' codec can't decode byte at position " + std::to_string(h[0])};
     if ((unsigned)h[1] == 0) return d_in;
 
     DevBuf<uint8_t> mapped(n), keep(n);
     scratch.alloc(n);
-    hipLaunchKernelGGL(k_newline_map, dim3(ceil_div(n, 256)), dim3(256), 0, stream, d_in, n,
+    hipLaunchKernelGGL(k_newline_map, dim3(grid_for(n, 256)), dim3(256), 0, stream, d_in, n,
                        mapped.p, keep.p);
     DevBuf<unsigned long long> d_nsel(1);
     select_flagged(mapped.p, keep.p, scratch.p, d_nsel.p, n, stream);
     unsigned long long nsel = 0;
-    BPE_HIP(hipMemcpyAsync(&nsel, d_nsel.p, 8, hipMemcpyDeviceToHost, stream));
-    BPE_HIP(hipStreamSynchronize(stream));
+    to_host(&nsel, d_nsel.p, 8, stream);
     *n_out = (size_t)nsel;
     return scratch.p;
 }
@@ -627,8 +633,23 @@ void ValidatePass::begin(const uint8_t* d_text, size_t n, hipStream_t stream) {
     s = stream;
     if (!flags.p) flags.alloc(2);
     const unsigned long long h_init[2] = {~0ULL, 0ULL};
-    BPE_HIP(hipMemcpyAsync(flags.p, h_init, sizeof(h_init), hipMemcpyHostToDevice, s));
-    BPE_HIP(hipStreamSynchronize(s));
+    to_device(flags.p, h_init, sizeof(h_init), s);
+    done_units = 0;
+}
+
+size_t ValidatePass::prefix(size_t loaded) {
+    // a unit's window is [16u - 4, 16u + 20) (k_validate): units with 16u + 20 <= loaded see
+    // loaded bytes only, and they are checked against the whole text (end `total`) exactly as
+    // one pass over it would
+    const size_t u1 = loaded >= total ? (total + kValidateBytes - 1) / kValidateBytes
+                                      : (loaded >= 20 ? (loaded - 20) / kValidateBytes + 1 : 0);
+    if (u1 > done_units) {
+        hipLaunchKernelGGL(k_validate, dim3(grid_for(u1 - done_units, 256)), dim3(256), 0, s, text, total,
+                           done_units, u1, flags.p, reinterpret_cast<unsigned*>(flags.p + 1));
+        BPE_HIP(hipGetLastError());
+        done_units = u1;
+    }
+    return std::min(total, done_units * kValidateBytes);
 }
 
 void ValidatePass::range(size_t lo, size_t hi) {
@@ -637,15 +658,14 @@ void ValidatePass::range(size_t lo, size_t hi) {
     const size_t u0 = lo / kValidateBytes;
     const size_t u1 = hi == total ? (hi + kValidateBytes - 1) / kValidateBytes : hi / kValidateBytes;
     if (u1 <= u0) return;
-    hipLaunchKernelGGL(k_validate, dim3(ceil_div(u1 - u0, 256)), dim3(256), 0, s, text, hi, u0, u1, flags.p,
+    hipLaunchKernelGGL(k_validate, dim3(grid_for(u1 - u0, 256)), dim3(256), 0, s, text, hi, u0, u1, flags.p,
                        reinterpret_cast<unsigned*>(flags.p + 1));
     BPE_HIP(hipGetLastError());
 }
 
 void ValidatePass::finish(unsigned long long* err_pos, bool* has_cr) {
     unsigned long long h[2];
-    BPE_HIP(hipMemcpyAsync(h, flags.p, sizeof(h), hipMemcpyDeviceToHost, s));
-    BPE_HIP(hipStreamSynchronize(s));
+    to_host(h, flags.p, sizeof(h), s);
     *err_pos = h[0];
     *has_cr = (unsigned)h[1] != 0;
 }

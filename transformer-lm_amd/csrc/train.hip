@@ -1017,6 +1017,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     __shared__ Cand s_wave[kSelListWave];
     __shared__ Cand s_all[kListCap];
     __shared__ SelKey s_key[kListCap];   // the same entries packed for the ranking loop
+    __shared__ unsigned s_top[kListCap], s_ntop;   // entries with fewer than kTopM larger counts
     __shared__ Cand s_list[kTopM];
     __shared__ long long s_cnt[kListCap];
     __shared__ long long s_cnt_target, s_cnt_last;   // counts at sorted positions kListTarget - 1, ln - 1
@@ -1077,7 +1078,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     unsigned lold = ~0u;
     if (li >= 0) {
         if (li < kTopM) s_list[li] = cand_none();
-        if (li == 0) { s_cnt_target = LLONG_MAX; s_cnt_last = LLONG_MAX; }
+        if (li == 0) { s_cnt_target = LLONG_MAX; s_cnt_last = LLONG_MAX; s_ntop = 0; }
         s_all[li] = x;
         s_key[li] = SelKey{x.cnt, x.ka, x.kb, (unsigned long long)x.b << 32 | x.a};
         s_cnt[li] = x.cnt;
@@ -1090,27 +1091,43 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     __syncthreads();
     if (li == 0) probe_stamp(st, ptrip, 27);
     long long tgt = LLONG_MAX, last = LLONG_MAX;
+    // rank by count alone first (one 8-byte compare per entry); only an entry with fewer than
+    // kTopM larger counts can be among the first kTopM, and every entry ordered before such an
+    // entry has its count or a larger one, so it has fewer than kTopM larger counts too: the
+    // exact order among that small set is the exact order overall
+    int rc = kTopM;
     if (have) {
-        // rank among the entries: (count, a's 8-byte prefix, b's) branch-free, loads independent of
-        // each other so they pipeline; only equal prefixes of different tokens need the bytes (rare:
-        // then the full comparison, as cand_better)
-        int rc = 0, rank = 0;
-        bool tail = false;
+        rc = 0;
 #pragma unroll 8
-        for (int j = 0; j < nl; ++j) {
+        for (int j = 0; j < nl; ++j) rc += s_cnt[j] > x.cnt ? 1 : 0;
+        if (rc < kTopM) s_top[atomicAdd(&s_ntop, 1u)] = li;
+        // the count at sorted position t is the least count whose first position is <= t
+        tgt = rc <= (int)kListTarget - 1 ? x.cnt : LLONG_MAX;
+        last = x.cnt;
+    }
+    if (li == 0) probe_stamp(st, ptrip, 29);   // count ranks done
+    __syncthreads();
+    if (have && rc < kTopM) {
+        // (count, a's 8-byte prefix, b's) branch-free over the small set; only equal prefixes of
+        // different tokens need the bytes (rare: then cand_better)
+        const int m = (int)s_ntop;
+        int rank = 0;
+        bool tail = false;
+        for (int t = 0; t < m; ++t) {
+            const int j = (int)s_top[t];
             const SelKey y = s_key[j];
             const unsigned ya = (unsigned)y.ab, yb = (unsigned)(y.ab >> 32);
             const bool gt = y.cnt > x.cnt, eq = y.cnt == x.cnt && j != li;
             const bool ad = ya != x.a, bd = yb != x.b;
-            rc += gt;
             rank += gt | (eq & ad & (y.ka > x.ka)) | (eq & !ad & bd & (y.kb > x.kb));
             tail |= eq & ((ad & (y.ka == x.ka)) | (!ad & bd & (y.kb == x.kb)));
         }
-        if (li == 0 && rank != -7) probe_stamp(st, ptrip, 29);   // ranking loop done
         if (tail) {
-            rank = rc;
-            for (int j = 0; j < nl; ++j)
-                rank += (s_cnt[j] == x.cnt && j != li && cand_better(s_all[j], x, K.pool, K.off, K.len)) ? 1 : 0;
+            rank = 0;
+            for (int t = 0; t < m; ++t) {
+                const int j = (int)s_top[t];
+                rank += (j != li && cand_better(s_all[j], x, K.pool, K.off, K.len)) ? 1 : 0;
+            }
         }
         if (rank < kTopM) {
             if (!kSelMetaAll) cand_meta(x, K, X, lm, lold);
@@ -1118,11 +1135,8 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
             s_meta[rank] = lm;
             s_nw_old[rank] = lold;
         }
-        // the count at sorted position t is the least count whose first position is <= t
-        tgt = rc <= (int)kListTarget - 1 ? x.cnt : LLONG_MAX;
-        last = x.cnt;
-        if (li == 0 && rank != -7) probe_stamp(st, ptrip, 28);   // ranked
     }
+    if (li == 0) probe_stamp(st, ptrip, 28);   // ranked
     if (li >= 0) {   // wave minima, then one LDS atomic per wave
         for (int o = 32; o > 0; o >>= 1) {
             tgt = min(tgt, (long long)__shfl_xor(tgt, o));
