@@ -114,14 +114,50 @@ void corpus_give(std::unique_ptr<CorpusBuf> x) {
 
 }  // namespace
 
+// Reader threads and DMA streams of one transfer.  Measured on MI355X boxes with a page-cache-warm
+// 11.9 GB file (tools/microbench/numa_ab.hip, profiles/r03/e_load_ab.txt): DMA alone runs at
+// 50-52 GB/s on 1-2 streams but 37 GB/s on 16; pread alone at 45 GB/s on 16 threads; together,
+// 16 readers each with its own stream 34-38 GB/s, 8 readers feeding 2 shared streams 46-47 GB/s.
+// More than 16 readers is slower (24: 30 GB/s, 32: 24 GB/s), as is the NUMA binding of the
+// staging buffers (no difference).
 int io_threads() {
     static const int t = [] {
-        int n = (int)std::thread::hardware_concurrency();
+        int n = 8;
         if (const char* e = std::getenv("BPE355_IO_THREADS")) n = std::atoi(e);
-        return std::max(1, std::min(n > 0 ? n : 8, 16));   // a GPU's share of the host is 16 cores
+        return std::max(1, std::min(n, 16));   // a GPU's share of the host is 16 cores
     }();
     return t;
 }
+
+static int dma_streams() {
+    static const int t = [] {
+        int n = 2;
+        if (const char* e = std::getenv("BPE355_DMA_STREAMS")) n = std::atoi(e);
+        return std::max(1, std::min(n, 16));
+    }();
+    return t;
+}
+
+namespace {
+// the DMA streams the reader threads of one transfer share (thread t copies on stream t % n): a
+// few deep queues keep the copy engines busier than one queue per thread
+struct DmaStreams {
+    std::vector<hipStream_t> s;
+    DmaStreams(int device, int n) {
+        BPE_HIP(hipSetDevice(device));
+        s.resize(n, nullptr);
+        for (auto& x : s) BPE_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    }
+    ~DmaStreams() {
+        for (auto& x : s)
+            if (x) {
+                (void)hipStreamSynchronize(x);
+                (void)hipStreamDestroy(x);
+            }
+    }
+    hipStream_t pick(int t) const { return s[(size_t)t % s.size()]; }
+};
+}  // namespace
 
 // ------------------------------------------------------------------ sources
 Source Source::open_path(const char* path) {
@@ -217,14 +253,14 @@ void stage_to_device(const Source& src, size_t off, size_t len, uint8_t* d_dst, 
     const int t_n = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads, chunks));
     std::atomic<size_t> next{0};
     std::vector<std::exception_ptr> errs(t_n);
+    DmaStreams dma(device, dma_streams());
     auto work = [&](int t) {
-        hipStream_t s = nullptr;
+        const hipStream_t s = dma.pick(t);
         void* buf[2] = {nullptr, nullptr};
         hipEvent_t ev[2] = {nullptr, nullptr};
         bool busy[2] = {false, false};
         try {
             BPE_HIP(hipSetDevice(device));
-            BPE_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
             for (int k = 0; k < 2; ++k) {
                 buf[k] = pool().get();
                 BPE_HIP(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
@@ -239,17 +275,16 @@ void stage_to_device(const Source& src, size_t off, size_t len, uint8_t* d_dst, 
                 BPE_HIP(hipEventRecord(ev[k], s));
                 busy[k] = true;
             }
-            BPE_HIP(hipStreamSynchronize(s));
         } catch (...) {
             errs[t] = std::current_exception();
             next.store(chunks);   // the others stop after their current chunk
-            if (s) (void)hipStreamSynchronize(s);
+            (void)hipStreamSynchronize(s);
         }
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < 2; ++k) {   // this thread's copies are done before its buffers go back
+            if (busy[k]) (void)hipEventSynchronize(ev[k]);
             if (ev[k]) (void)hipEventDestroy(ev[k]);
             if (buf[k]) pool().put(buf[k]);
         }
-        if (s) (void)hipStreamDestroy(s);
     };
     std::vector<std::thread> th;
     for (int t = 1; t < t_n; ++t) th.emplace_back(work, t);
@@ -269,8 +304,9 @@ void device_to_host(const uint8_t* d_src, size_t len, uint8_t* h_dst, int device
     const int t_n = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads, chunks));
     std::atomic<size_t> next{0};
     std::vector<std::exception_ptr> errs(t_n);
+    DmaStreams dma(device, dma_streams());
     auto work = [&](int t) {
-        hipStream_t s = nullptr;
+        const hipStream_t s = dma.pick(t);
         void* buf[2] = {nullptr, nullptr};
         hipEvent_t ev[2] = {nullptr, nullptr};
         size_t pend[2] = {~(size_t)0, ~(size_t)0};   // chunk whose DMA into buf[k] is in flight
@@ -283,7 +319,6 @@ void device_to_host(const uint8_t* d_src, size_t len, uint8_t* h_dst, int device
         };
         try {
             BPE_HIP(hipSetDevice(device));
-            BPE_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
             for (int k = 0; k < 2; ++k) {
                 buf[k] = pool().get();
                 BPE_HIP(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
@@ -302,13 +337,13 @@ void device_to_host(const uint8_t* d_src, size_t len, uint8_t* h_dst, int device
         } catch (...) {
             errs[t] = std::current_exception();
             next.store(chunks);
-            if (s) (void)hipStreamSynchronize(s);
+            (void)hipStreamSynchronize(s);
         }
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < 2; ++k) {   // no DMA into a buffer that goes back to the pool
+            if (pend[k] != ~(size_t)0) (void)hipEventSynchronize(ev[k]);
             if (ev[k]) (void)hipEventDestroy(ev[k]);
             if (buf[k]) pool().put(buf[k]);
         }
-        if (s) (void)hipStreamDestroy(s);
     };
     std::vector<std::thread> th;
     for (int t = 1; t < t_n; ++t) th.emplace_back(work, t);
@@ -388,13 +423,13 @@ bool load_and_count(const Source& src, size_t off, size_t len, uint8_t* d_dst, i
     const int t_n = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads, chunks));
     std::atomic<size_t> next{0};
     std::vector<std::exception_ptr> errs(t_n);
+    DmaStreams dma(device, dma_streams());
     auto reader = [&](int t) {
-        hipStream_t s = nullptr;
+        const hipStream_t s = dma.pick(t);
         void* buf[2] = {nullptr, nullptr};
         size_t last[2] = {~(size_t)0, ~(size_t)0};
         try {
             BPE_HIP(hipSetDevice(device));
-            BPE_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
             for (int k = 0; k < 2; ++k) buf[k] = pool().get();
             for (int k = 0;; k ^= 1) {
                 const size_t i = next.fetch_add(1);
@@ -407,16 +442,16 @@ bool load_and_count(const Source& src, size_t off, size_t len, uint8_t* d_dst, i
                 last[k] = i;
                 track.mark(i);
             }
-            BPE_HIP(hipStreamSynchronize(s));
         } catch (...) {
             errs[t] = std::current_exception();
             next.store(chunks);
             track.fail();
-            if (s) (void)hipStreamSynchronize(s);
+            (void)hipStreamSynchronize(s);
         }
-        for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < 2; ++k) {   // this thread's copies are done before its buffers go back
+            if (last[k] != ~(size_t)0) (void)hipEventSynchronize(track.ev[last[k]]);
             if (buf[k]) pool().put(buf[k]);
-        if (s) (void)hipStreamDestroy(s);
+        }
     };
     std::vector<std::thread> th;
     for (int t = 0; t < t_n; ++t) th.emplace_back(reader, t);
