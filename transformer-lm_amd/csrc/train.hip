@@ -200,6 +200,25 @@ __device__ __forceinline__ Cand shfl_xor_cand(const Cand& c, int o) {
 }
 
 
+// Stores of the trip kernels: write-through (sc1) or plain.  A plain store leaves a dirty line in
+// the XCD's L2 that the end of the kernel writes back before the next launch can start; a
+// write-through store leaves while the kernel still runs (MI355X_MICROARCH.md: sc1 stores drop the
+// line from L2).  Build knobs BPE355_WT_APPLY (pair-table updates) and BPE355_WT_MERGE (word
+// rewrites and the cell clear).
+#ifndef BPE355_WT_APPLY
+#define BPE355_WT_APPLY 0
+#endif
+#ifndef BPE355_WT_MERGE
+#define BPE355_WT_MERGE 0
+#endif
+template <bool WT, class T>
+__device__ __forceinline__ void st_wt(T* p, T v) {
+    if constexpr (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+template <class T> __device__ __forceinline__ void st_apply(T* p, T v) { st_wt<BPE355_WT_APPLY != 0>(p, v); }
+template <class T> __device__ __forceinline__ void st_merge(T* p, T v) { st_wt<BPE355_WT_MERGE != 0>(p, v); }
+
 // ------------------------------------------------------------------ pair table
 // returns the slot of key (inserting it if absent, *inserted = 1), or ~0 if the table is full
 __device__ __forceinline__ size_t pair_slot(const PairsDev& P, unsigned long long key,
@@ -354,17 +373,17 @@ __device__ __forceinline__ uint32_t rewrite_slot(const TokT (&e)[W], TokT* __res
             if (j > 0) D.add(2u * (unsigned)prev, c);                      // (x,a)-=c, (x,new)+=c
             if (q + 2 < W && e[q + 2 < W ? q + 2 : q] != sent)
                 D.add(2u * (unsigned)e[q + 2 < W ? q + 2 : q] + 1, c);     // (b,y)-=c, (new,y)+=c
-            s[1 + j] = nw;
+            st_merge(&s[1 + j], nw);
             prev = nw;
             skip = true;
         } else {
-            if (j != (uint32_t)(q - 1)) s[1 + j] = x;
+            if (j != (uint32_t)(q - 1)) st_merge(&s[1 + j], x);
             prev = x;
         }
         ++j;
     }
-    for (uint32_t p = j; p < (uint32_t)e[0]; ++p) s[1 + p] = sent;
-    s[0] = (TokT)j;
+    for (uint32_t p = j; p < (uint32_t)e[0]; ++p) st_merge(&s[1 + p], sent);
+    st_merge(&s[0], (TokT)j);
     return j;
 }
 
@@ -702,10 +721,10 @@ __device__ __forceinline__ size_t pair_update_from(const PairsDev& P, RoundState
         }
     }
     c += delta;
-    P.cnt[s] = c;
+    st_apply(&P.cnt[s], c);
     if ((inc || ins) && !(f & kPresent)) {
         f |= kPresent;
-        P.flag[s] = f;
+        st_apply(&P.flag[s], f);
     }
     *c_out = c;
     *f_out = f;
@@ -1434,7 +1453,7 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
         const unsigned nprev = 2 * (unsigned)B.ntok;
         const unsigned S = gridDim.x * blockDim.x;
         for (unsigned q = blockIdx.x * blockDim.x + tid; q < (unsigned)B.prev_k * nprev; q += S)
-            LRo[(size_t)(q / nprev) * lr_member + q % nprev] = 0;
+            st_merge(&LRo[(size_t)(q / nprev) * lr_member + q % nprev], 0ull);
     };
     {   // list mode: workgroups past the listed words (and past the members' registrations) have
         // nothing to do -- skip their LDS clear, barriers and flush
@@ -1689,7 +1708,7 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
         if (s == ~(size_t)0 || !(f & kPresent) || c < T) return;
         offer(Cand{c, kp, kq, (unsigned)s, p, q});
         const bool adm = inc && !(f & kInC);
-        if (adm) P.flag[s] = f | kInC;
+        if (adm) st_apply(&P.flag[s], f | kInC);
         admit(adm, s, p, q);
     };
     // step u of a pass takes items base + u * S + g: a wave's 64 items are contiguous (coalesced)
