@@ -906,6 +906,9 @@ __global__ void __launch_bounds__(256) k_argmax(RoundState* __restrict__ st, Pai
 #endif
 constexpr int kMaxBatch = BPE355_MAX_BATCH;   // members per trip (3 * kMaxBatch tokens fit one wave)
 constexpr int kTopM = kMaxBatch + 1;
+// the select's clash check: candidates i < kClashI (a power of two >= kMaxBatch), kClashJ lanes each
+constexpr int kClashI = kMaxBatch <= 16 ? 16 : 32;
+constexpr int kClashJ = 64 / kClashI;
 constexpr unsigned kLdsB = 128;          // LDS-summed cells per member (ids below kLdsB)
 
 struct BatchMember {
@@ -923,6 +926,7 @@ struct Batch {
     unsigned full_scan;  // a member has no usable posting list: scan every word once
     unsigned n_fresh;    // members that create a token
     unsigned nC_base;    // C entries before this trip's admissions (the apply scans them)
+    unsigned idle_from;  // list mode: merge threads from this index on have no word (~0: scan mode)
     unsigned list_pre[kMaxBatch + 1];   // prefix sums of the members' list lengths
     BatchMember m[kMaxBatch];
 };
@@ -1035,8 +1039,9 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     static_assert(kApplyGrid <= 64 * kSelListWave, "one partial per thread of the partial waves");
     __shared__ Cand s_wave[kSelListWave];
     __shared__ Cand s_all[kListCap];
-    __shared__ SelKey s_key[kListCap];   // the same entries packed for the ranking loop
-    __shared__ unsigned s_top[kListCap], s_ntop;   // entries with fewer than kTopM larger counts
+    __shared__ SelKey s_topkey[kListCap];          // the entries with fewer than kTopM larger counts,
+    __shared__ unsigned s_top[kListCap], s_ntop;   // packed for the exact ranking (key, list index)
+    __shared__ Cand s_p1;                          // the exact best (wave 0, beside the ranking)
     __shared__ Cand s_list[kTopM];
     __shared__ long long s_cnt[kListCap];
     __shared__ long long s_cnt_target, s_cnt_last;   // counts at sorted positions kListTarget - 1, ln - 1
@@ -1099,7 +1104,6 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         if (li < kTopM) s_list[li] = cand_none();
         if (li == 0) { s_cnt_target = LLONG_MAX; s_cnt_last = LLONG_MAX; s_ntop = 0; }
         s_all[li] = x;
-        s_key[li] = SelKey{x.cnt, x.ka, x.kb, (unsigned long long)x.b << 32 | x.a};
         s_cnt[li] = x.cnt;
         if (li == 0 && lq.slot != 0xfffffffeu) probe_stamp(st, ptrip, 24);   // the list entry arrived
         if (have && kSelMetaAll) cand_meta(x, K, X, lm, lold);   // overlaps the partials' reduction
@@ -1109,6 +1113,12 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     if (tid == 0 && st->probe && (ptrip % kProbeTrip) == 0) st->probe[kProbeSlots * (size_t)(ptrip / kProbeTrip) + 30] = ln + 1;
     __syncthreads();
     if (li == 0) probe_stamp(st, ptrip, 27);
+    if (wv == 0) {   // P1 over the waves' bests, while the list waves rank (off the rule's path)
+        Cand p = s_wave[0];
+        for (int w = 1; w < kSelListWave; ++w)
+            if (cand_better(s_wave[w], p, K.pool, K.off, K.len)) p = s_wave[w];
+        if (lane == 0) s_p1 = p;
+    }
     long long tgt = LLONG_MAX, last = LLONG_MAX;
     // rank by count alone first (one 8-byte compare per entry); only an entry with fewer than
     // kTopM larger counts can be among the first kTopM, and every entry ordered before such an
@@ -1119,7 +1129,11 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         rc = 0;
 #pragma unroll 8
         for (int j = 0; j < nl; ++j) rc += s_cnt[j] > x.cnt ? 1 : 0;
-        if (rc < kTopM) s_top[atomicAdd(&s_ntop, 1u)] = li;
+        if (rc < kTopM) {
+            const unsigned pos = atomicAdd(&s_ntop, 1u);
+            s_top[pos] = li;
+            s_topkey[pos] = SelKey{x.cnt, x.ka, x.kb, (unsigned long long)x.b << 32 | x.a};
+        }
         // the count at sorted position t is the least count whose first position is <= t
         tgt = rc <= (int)kListTarget - 1 ? x.cnt : LLONG_MAX;
         last = x.cnt;
@@ -1132,9 +1146,10 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         const int m = (int)s_ntop;
         int rank = 0;
         bool tail = false;
+#pragma unroll 4
         for (int t = 0; t < m; ++t) {
             const int j = (int)s_top[t];
-            const SelKey y = s_key[j];
+            const SelKey y = s_topkey[t];
             const unsigned ya = (unsigned)y.ab, yb = (unsigned)(y.ab >> 32);
             const bool gt = y.cnt > x.cnt, eq = y.cnt == x.cnt && j != li;
             const bool ad = ya != x.a, bd = yb != x.b;
@@ -1170,9 +1185,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     if (tid == 0) probe_stamp(st, ptrip, 2);
     if (wv != 0) return;
     // ---- wave 0: the rule and the record, lane i holding candidate i (no workgroup barrier)
-    Cand p1 = s_wave[0];
-    for (int w = 1; w < kSelListWave; ++w)
-        if (cand_better(s_wave[w], p1, K.pool, K.off, K.len)) p1 = s_wave[w];
+    const Cand p1 = s_p1;
     // the list's head is the global best whenever the best is >= T2 and nothing overflowed; the
     // ranks are distinct, so s_list holds a prefix
     if (lane == 0) probe_stamp(st, ptrip, 17);
@@ -1226,21 +1239,36 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     if (lane == 0) probe_stamp(st, ptrip, 18);
     const unsigned long long h = m.ha * m.pb + m.hb;
     const unsigned lk = m.la + m.lb;
-    // (1) tokens disjoint from, and (3) new bytes different from, every earlier candidate's
+    // (1) tokens disjoint from, and (3) new bytes different from, every earlier candidate's.
+    // The kClashI x kClashI (i, j) pairs are spread over the wave: lane L checks i = L % kClashI
+    // against j = L / kClashI + t * kClashJ, then the kClashJ lanes of each i combine (one pass of
+    // lane shuffles instead of a serial readlane chain over j)
     bool clash = false;
-    for (int j = 0; j < kMaxBatch; ++j) {
-        const unsigned aj = __builtin_amdgcn_readlane((int)e.a, j), bj = __builtin_amdgcn_readlane((int)e.b, j);
-        const unsigned long long hj = readlane64(h, j);
-        const unsigned lj = __builtin_amdgcn_readlane((int)lk, j), laj = __builtin_amdgcn_readlane((int)m.la, j);
-        if (j < i && i < nf) {
-            clash |= aj == e.a || aj == e.b || bj == e.a || bj == e.b;
-            if (!clash && hj == h && lj == lk) {
-                bool eq = true;
-                for (unsigned x = 0; x < lk && eq; ++x)
-                    eq = concat_byte(K, aj, laj, bj, x) == concat_byte(K, e.a, m.la, e.b, x);
-                clash = eq;
+    {
+        const int ci = lane % kClashI, cj0 = lane / kClashI;
+        const unsigned ai = __shfl((int)e.a, ci), bi = __shfl((int)e.b, ci);
+        const unsigned long long hi = __shfl(h, ci);
+        const unsigned li_ = __shfl((int)lk, ci), lai = __shfl((int)m.la, ci);
+        const bool iv = ci < nf;
+#pragma unroll
+        for (int t = 0; t < kClashI / kClashJ; ++t) {
+            const int j = cj0 + t * kClashJ;
+            const unsigned aj = __shfl((int)e.a, j), bj = __shfl((int)e.b, j);
+            const unsigned long long hj = __shfl(h, j);
+            const unsigned lj = __shfl((int)lk, j), laj = __shfl((int)m.la, j);
+            if (j < ci && iv) {
+                const bool tc = aj == ai || aj == bi || bj == ai || bj == bi;
+                clash |= tc;
+                if (!tc && hj == hi && lj == li_) {   // equal hashes: compare the bytes (rare)
+                    bool eq = true;
+                    for (unsigned x = 0; x < li_ && eq; ++x)
+                        eq = concat_byte(K, aj, laj, bj, x) == concat_byte(K, ai, lai, bi, x);
+                    clash |= eq;
+                }
             }
         }
+        for (int o = kClashI; o < 64; o <<= 1) clash |= __shfl_xor((int)clash, o) != 0;
+        if (i >= kClashI) clash = false;   // lanes < kClashI hold their own i's result
     }
     // k: the first candidate that fails (count >= T, (2) a != b, fresh, no clash), within the
     // allowed batch; one merge when P1 itself is not batchable
@@ -1300,13 +1328,13 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     const unsigned lu = m.za <= m.zb ? m.za : m.zb, bu = m.za <= m.zb ? m.ba : m.bb;
     const bool use = lu != kNoAnc && lu <= X.full_threshold;
     const unsigned add_pool = mem && fr ? lk : 0u, add_fresh = mem && fr ? 1u : 0u, add_list = mem && use ? lu : 0u;
-    unsigned pre_pool = 0, pre_fresh = 0, pre_list = 0;
-    for (int j = 0; j < kMaxBatch; ++j) {
-        const unsigned pj = __builtin_amdgcn_readlane((int)add_pool, j);
-        const unsigned fj = __builtin_amdgcn_readlane((int)add_fresh, j);
-        const unsigned uj = __builtin_amdgcn_readlane((int)add_list, j);
-        if (j < i) { pre_pool += pj; pre_fresh += fj; pre_list += uj; }
+    unsigned pre_pool = add_pool, pre_fresh = add_fresh, pre_list = add_list;   // inclusive scans
+    for (int d = 1; d <= kMaxBatch; d <<= 1) {
+        const unsigned tp = __shfl_up((int)pre_pool, d), tf = __shfl_up((int)pre_fresh, d),
+                       tl = __shfl_up((int)pre_list, d);
+        if (lane >= d) { pre_pool += tp; pre_fresh += tf; pre_list += tl; }
     }
+    pre_pool -= add_pool; pre_fresh -= add_fresh; pre_list -= add_list;   // exclusive: lanes < i
     // one scan of every word once the members' lists together pass the scan threshold
     const bool full = __ballot(mem && !use) != 0 || __builtin_amdgcn_readlane((int)pre_list, k) > (int)X.full_threshold;
     const unsigned tot_pool = __builtin_amdgcn_readlane((int)pre_pool, k);
@@ -1344,6 +1372,10 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         B.batch_id = bid;
         B.nC_base = nC;
         B.full_scan = full;
+        {   // the merge's idle workgroups: past the listed words, when every member has a list
+            const bool lists = k > 1 ? !full : use;   // lane 0: member 0's own flag
+            B.idle_from = lists ? tot_list : ~0u;
+        }
         B.n_fresh = tot_fresh;
         st->pool_used = pool_used + tot_pool;
         bs->batch_seq = bid;
@@ -1443,36 +1475,37 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
     __shared__ unsigned s_pre[kMaxBatch + 1], s_lbeg[kMaxBatch];   // list prefix sums, list starts
     const int tid = threadIdx.x;
     const Batch& B = *bt;
-    if (B.stop) return;
-    const int k = B.k;
+    // every field the prologue needs in one round trip (none depends on another)
+    const int stop = B.stop, k = B.k, b_trip = B.trip, b_ntok = B.ntok, b_prev_k = B.prev_k;
+    const unsigned idle_from = B.idle_from;
+    unsigned ma = 0, mb = 0, mn = 0, mlb = 0, mpre = 0;
+    if (tid < kMaxBatch) { ma = B.m[tid].a; mb = B.m[tid].b; mn = B.m[tid].nw; mlb = B.m[tid].list_beg; }
+    if (tid <= kMaxBatch) mpre = B.list_pre[tid];
+    if (stop) return;
     // the previous trip's cells (the other parity, read by its apply) are cleared here, spread
     // over the whole grid: workgroups without words do their share at once, the others after
     // their flush, so the stores never wait in front of a rewrite's loads
     auto clear_prev = [&]() {
-        unsigned long long* LRo = LRbase + (size_t)((B.trip + 1) & 1) * lr_parity;
-        const unsigned nprev = 2 * (unsigned)B.ntok;
+        unsigned long long* LRo = LRbase + (size_t)((b_trip + 1) & 1) * lr_parity;
+        const unsigned nprev = 2 * (unsigned)b_ntok;
         const unsigned S = gridDim.x * blockDim.x;
-        for (unsigned q = blockIdx.x * blockDim.x + tid; q < (unsigned)B.prev_k * nprev; q += S)
+        for (unsigned q = blockIdx.x * blockDim.x + tid; q < (unsigned)b_prev_k * nprev; q += S)
             st_merge(&LRo[(size_t)(q / nprev) * lr_member + q % nprev], 0ull);
     };
     {   // list mode: workgroups past the listed words (and past the members' registrations) have
         // nothing to do -- skip their LDS clear, barriers and flush
         const unsigned bid = blockIdx.x;
-        if (bid >= (unsigned)k && bid < W.lblk0) {
-            const bool lists = k > 1 ? !B.full_scan : B.m[0].use_list != 0;
-            const unsigned total = k > 1 ? B.list_pre[k] : B.m[0].list_len;
-            if (lists && bid * blockDim.x >= total) {
-                clear_prev();
-                if (tid == 0) probe_done(st, &st->probe_merge_done, B.trip, 14);
-                return;
-            }
+        if (bid >= (unsigned)k && bid < W.lblk0 && bid * blockDim.x >= idle_from) {
+            clear_prev();
+            if (tid == 0) probe_done(st, &st->probe_merge_done, b_trip, 14);
+            return;
         }
     }
     if (tid < k) {
-        s_ma[tid] = B.m[tid].a; s_mb[tid] = B.m[tid].b; s_mn[tid] = B.m[tid].nw;
-        s_lbeg[tid] = B.m[tid].list_beg;
+        s_ma[tid] = ma; s_mb[tid] = mb; s_mn[tid] = mn;
+        s_lbeg[tid] = mlb;
     }
-    if (tid <= k) s_pre[tid] = B.list_pre[tid];
+    if (tid <= k) s_pre[tid] = mpre;
     if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 5);
     for (unsigned q = tid; q < 2 * kLdsB * (unsigned)k; q += blockDim.x) l_lr[q] = 0;
     unsigned long long* LRt = LRbase + (size_t)(B.trip & 1) * lr_parity;   // member j at + j * lr_member
@@ -1626,16 +1659,24 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     __shared__ uint4 s_cadd[kApplyCLds];
     __shared__ unsigned s_nl, s_nc, s_lbase, s_cbase, s_ins;
     const Batch& B = *bt;
-    if (!scan_only && B.stop) return;   // halted: part[] keeps the lists the next select reads
-    const int k = scan_only ? 0 : B.k;
     const int tid = threadIdx.x;
+    // every field the prologue needs in one round trip (none depends on another); the batch is
+    // valid memory even when stale (scan_only), so its loads need no guard
+    static_assert(offsetof(BatchMember, b) == 4 && offsetof(BatchMember, nw) == 8, "a, b, nw adjacent");
+    const int b_stop = B.stop, b_k = B.k, b_trip = B.trip, b_ntok = B.ntok;
+    const unsigned b_fresh = B.n_fresh, b_nC = B.nC_base;
+    const long long T = st->T, T2raw = bs->T2;
+    const unsigned st_nC = st->nC;   // scan_only: no admissions during the scan, so stable
+    const unsigned t_raw = tid < 3 * kMaxBatch ? reinterpret_cast<const unsigned*>(&B.m[tid / 3])[tid % 3] : ~0u;
+    if (!scan_only && b_stop) return;   // halted: part[] keeps the lists the next select reads
+    const int k = scan_only ? 0 : b_k;
     const bool pw0 = !scan_only && blockIdx.x == 0 && tid == 0;
-    if (pw0) probe_stamp(st, B.trip, 9);
+    if (pw0) probe_stamp(st, b_trip, 9);
     if (tid < 64) {   // wave 0: S deduplicated (a == b is possible only when k == 1), lane i = entry i
         static_assert(3 * kMaxBatch <= 64, "S fits one wave");
         const int i = tid;
         const bool have = i < 3 * k;
-        const unsigned ti = have ? (i % 3 == 0 ? B.m[i / 3].a : (i % 3 == 1 ? B.m[i / 3].b : B.m[i / 3].nw)) : ~0u;
+        const unsigned ti = have ? t_raw : ~0u;
         bool dup = false;
         unsigned roles = 0;   // members' tokens are disjoint for k > 1: one member per token
         for (int j = 0; j < 3 * kMaxBatch; ++j) {
@@ -1661,18 +1702,17 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     }
     __syncthreads();
     const int ns = s_ns;
-    const long long T = st->T;
-    const unsigned long long* LRc = LRbase + (size_t)(B.trip & 1) * lr_parity;
-    if (!scan_only) ntb = min(ntb, (unsigned)B.ntok + B.n_fresh);   // token ids after this trip
+    const unsigned long long* LRc = LRbase + (size_t)(b_trip & 1) * lr_parity;
+    if (!scan_only) ntb = min(ntb, (unsigned)b_ntok + b_fresh);   // token ids after this trip
     const unsigned per_member = 4 * ntb;
     const unsigned n_cell = (unsigned)k * per_member;
     const unsigned n_sp = (unsigned)(ns * ns);
-    const unsigned nC0 = scan_only ? st->nC : B.nC_base;
+    const unsigned nC0 = scan_only ? st_nC : b_nC;
     const unsigned n_items = n_cell + n_sp + nC0;
     const unsigned g = blockIdx.x * blockDim.x + tid;
     const unsigned S = gridDim.x * blockDim.x;
     // (the previous trip's cells were cleared by this trip's merge)
-    if (pw0) probe_stamp(st, B.trip, 10);
+    if (pw0) probe_stamp(st, b_trip, 10);
     auto find_S = [&](unsigned x) -> int {   // x's entry in S, or -1
         if (!((s_filt[(x >> 5) % kSFilterWords] >> (x & 31)) & 1u)) return -1;
         int r = -1;
@@ -1680,7 +1720,7 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
         return r;
     };
     auto in_S = [&](unsigned x) { return find_S(x) >= 0; };
-    const long long T2 = bs->T2 < T ? T : bs->T2;
+    const long long T2 = T2raw < T ? T : T2raw;
     Cand best = cand_none();   // this thread's best candidate (exact argmax)
     unsigned n_ins = 0;        // pair-table keys this thread inserted
     // a candidate for the list (>= T2) and for this thread's best
@@ -1875,32 +1915,67 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
 }
 
 // ------------------------------------------------------------------ word table build
-__global__ void k_collect_words(const unsigned long long* __restrict__ kv,
-                                const unsigned long long* __restrict__ pos, size_t cap,
-                                const uint8_t* __restrict__ text, const uint8_t* __restrict__ sp_bytes,
-                                const uint32_t* __restrict__ sp_off, const uint32_t* __restrict__ sp_len,
-                                int n_sp, unsigned long long* __restrict__ w_off,
-                                uint32_t* __restrict__ w_len, unsigned long long* __restrict__ w_cnt,
-                                unsigned* __restrict__ n_words, unsigned* __restrict__ max_len) {
-    const size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+// Occupied count-table slots -> (offset, len, count) words.  Each workgroup takes
+// kCollectPer * 256 slots and reserves its words' positions with ONE global atomic (one per
+// wave, 262 K same-address atomics at a 16 M-slot table, serialised into ~6 ms).
+constexpr unsigned kCollectThreads = 256;
+constexpr unsigned kCollectPer = 8;
+__global__ void __launch_bounds__(kCollectThreads) k_collect_words(
+    const unsigned long long* __restrict__ kv, const unsigned long long* __restrict__ pos, size_t cap,
+    const uint8_t* __restrict__ text, const uint8_t* __restrict__ sp_bytes, const uint32_t* __restrict__ sp_off,
+    const uint32_t* __restrict__ sp_len, int n_sp, unsigned long long* __restrict__ w_off,
+    uint32_t* __restrict__ w_len, unsigned long long* __restrict__ w_cnt, unsigned* __restrict__ n_words,
+    unsigned* __restrict__ max_len) {
+    __shared__ unsigned s_n, s_base, s_ml;
+    if (threadIdx.x == 0) { s_n = 0; s_ml = 0; }
+    const size_t s0 = (size_t)blockIdx.x * kCollectThreads * kCollectPer + threadIdx.x;
+    unsigned long long key[kCollectPer];
+#pragma unroll
+    for (unsigned u = 0; u < kCollectPer; ++u) {   // coalesced: slot s0 + u * 256
+        const size_t s = s0 + (size_t)u * kCollectThreads;
+        key[u] = s < cap ? kv[2 * s] : 0ULL;
+    }
     // {key, count} entries (text.hip): the key's top bit marks a word stored inline (length in
     // bits 56..62, an occurrence in pos[]), else key = len << 40 | offset + 1
-    const unsigned long long k = s < cap ? kv[2 * s] : 0ULL;
-    bool keep = k != 0;
-    const bool inl = (k >> 63) != 0;
-    const unsigned len = inl ? (unsigned)((k >> 56) & 0x7f) : (unsigned)(k >> 40);
-    const unsigned long long off = inl ? (keep ? pos[s] : 0ULL) : (k & ((1ULL << 40) - 1)) - 1;
-    for (int i = 0; keep && i < n_sp; ++i) {  // train.py:25 skips matches equal to a special
-        if (sp_len[i] != len) continue;
-        bool eq = true;
-        for (unsigned j = 0; j < len && eq; ++j) eq = text[off + j] == sp_bytes[sp_off[i] + j];
-        if (eq) keep = false;
+    unsigned long long off[kCollectPer];
+    unsigned len[kCollectPer];
+    unsigned mine = 0, ml = 0, keepm = 0;
+#pragma unroll
+    for (unsigned u = 0; u < kCollectPer; ++u) {
+        const size_t s = s0 + (size_t)u * kCollectThreads;
+        const unsigned long long k = key[u];
+        bool keep = k != 0;
+        const bool inl = (k >> 63) != 0;
+        len[u] = inl ? (unsigned)((k >> 56) & 0x7f) : (unsigned)(k >> 40);
+        off[u] = inl ? (keep ? pos[s] : 0ULL) : (k & ((1ULL << 40) - 1)) - 1;
+        for (int i = 0; keep && i < n_sp; ++i) {  // train.py:25 skips matches equal to a special
+            if (sp_len[i] != len[u]) continue;
+            bool eq = true;
+            for (unsigned j = 0; j < len[u] && eq; ++j) eq = text[off[u] + j] == sp_bytes[sp_off[i] + j];
+            if (eq) keep = false;
+        }
+        keepm |= (unsigned)keep << u;
+        mine += keep;
+        ml = keep && len[u] > ml ? len[u] : ml;
     }
-    const unsigned idx = wave_append(keep, n_words);
-    const unsigned ml = wave_max(keep ? len : 0u);
-    if ((threadIdx.x & 63) == 0 && ml) atomicMax(max_len, ml);
-    if (!keep) return;
-    w_off[idx] = off; w_len[idx] = len; w_cnt[idx] = kv[2 * s + 1];
+    __syncthreads();   // s_n, s_ml initialised
+    const unsigned at = mine ? atomicAdd(&s_n, mine) : 0u;   // LDS: this thread's first position
+    ml = wave_max(ml);
+    if ((threadIdx.x & 63) == 0 && ml) atomicMax(&s_ml, ml);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        s_base = s_n ? atomicAdd(n_words, s_n) : 0u;
+        if (s_ml) atomicMax(max_len, s_ml);
+    }
+    __syncthreads();
+    unsigned idx = s_base + at;
+#pragma unroll
+    for (unsigned u = 0; u < kCollectPer; ++u) {
+        if (!((keepm >> u) & 1u)) continue;
+        const size_t s = s0 + (size_t)u * kCollectThreads;
+        w_off[idx] = off[u]; w_len[idx] = len[u]; w_cnt[idx] = kv[2 * s + 1];
+        ++idx;
+    }
 }
 
 __global__ void k_len_u64(const uint32_t* __restrict__ w_len, unsigned n, unsigned long long* __restrict__ o) {
@@ -2435,7 +2510,8 @@ void MergeLoop<TokT>::build_words(const WordCounts& wc, const std::vector<std::s
     BPE_HIP(hipMemsetAsync(cnts.p, 0, 8, s_));
     DevBuf<unsigned long long> w_off(wc.cap), w_cnt(wc.cap);
     DevBuf<uint32_t> w_len(wc.cap);
-    hipLaunchKernelGGL(k_collect_words, dim3(ceil_div(wc.cap, 256)), dim3(256), 0, s_, wc.kv.p,
+    hipLaunchKernelGGL(k_collect_words, dim3(ceil_div(wc.cap, (size_t)kCollectThreads * kCollectPer)),
+                       dim3(kCollectThreads), 0, s_, wc.kv.p,
                        wc.pos.p, wc.cap, text_, d_spb.p, d_spo.p, d_spl.p, (int)specials.size(),
                        w_off.p, w_len.p, w_cnt.p, cnts.p, cnts.p + 1);
     BPE_HIP(hipGetLastError());
