@@ -398,8 +398,13 @@ struct ClipWin {   // one block's window with the bytes before window position l
     }
 };
 
+// workgroups per CU the scan's registers are capped for (build knob): 4 caps them at 128 VGPRs
+// and spills ~160 B per lane; 3 leaves room for every live value
+#ifndef BPE355_ENC_SCAN_WG
+#define BPE355_ENC_SCAN_WG 4
+#endif
 template <bool kAligned>
-__global__ void __launch_bounds__(256, 4)
+__global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG)
 k_enc_scan2(const uint8_t* __restrict__ s, size_t n, size_t n_chunks, const Seg* __restrict__ segs,
             int nseg, unsigned long long* __restrict__ kv, unsigned long long* __restrict__ pos,
             size_t mask, unsigned long long max_fill, unsigned long long* __restrict__ fill,
