@@ -1124,11 +1124,15 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     // kTopM larger counts can be among the first kTopM, and every entry ordered before such an
     // entry has its count or a larger one, so it has fewer than kTopM larger counts too: the
     // exact order among that small set is the exact order overall
-    int rc = kTopM;
+    int rc = kTopM, ec = 0;   // entries with a larger count, with an equal count (itself included)
     if (have) {
         rc = 0;
 #pragma unroll 8
-        for (int j = 0; j < nl; ++j) rc += s_cnt[j] > x.cnt ? 1 : 0;
+        for (int j = 0; j < nl; ++j) {
+            const long long cj = s_cnt[j];
+            rc += cj > x.cnt ? 1 : 0;
+            ec += cj == x.cnt ? 1 : 0;
+        }
         if (rc < kTopM) {
             const unsigned pos = atomicAdd(&s_ntop, 1u);
             s_top[pos] = li;
@@ -1140,11 +1144,15 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     }
     if (li == 0) probe_stamp(st, ptrip, 29);   // count ranks done
     __syncthreads();
+    if (li == 0) probe_stamp(st, ptrip, 31);   // every list thread's count rank done
     if (have && rc < kTopM) {
         // (count, a's 8-byte prefix, b's) branch-free over the small set; only equal prefixes of
         // different tokens need the bytes (rare: then cand_better)
-        const int m = (int)s_ntop;
-        int rank = 0;
+        // with no other entry of its count, the count rank is the exact rank (the usual case);
+        // otherwise the ties are ordered by bytes over the packed top entries, which hold every
+        // entry of this count (each has the same rc < kTopM)
+        const int m = ec > 1 ? (int)s_ntop : 0;
+        int rank = ec > 1 ? 0 : rc;
         bool tail = false;
 #pragma unroll 4
         for (int t = 0; t < m; ++t) {
@@ -1640,6 +1648,10 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
 #define BPE355_APPLY_ITEMS 2
 #endif
 constexpr unsigned kBatchApplyItems = BPE355_APPLY_ITEMS;   // items per thread per pass of k_apply_batch
+#ifndef BPE355_APPLY_C_FIRST
+#define BPE355_APPLY_C_FIRST 0
+#endif
+constexpr bool kApplyCFirst = BPE355_APPLY_C_FIRST != 0;
 constexpr unsigned kApplyBatchThreads = 256;
 constexpr unsigned kApplyCLds = 256;
 constexpr unsigned kSFilterWords = 128;   // C admissions a workgroup stages in LDS (more: direct appends)
@@ -1754,6 +1766,15 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     // step u of a pass takes items base + u * S + g: a wave's 64 items are contiguous (coalesced)
     // and its steps far apart, so the dense start of each member's cells (the byte tokens, which
     // neighbour everything) spreads over many waves instead of serialising in a few
+    // item order: cells, S pairs, C entries; kApplyCFirst puts the C entries (every one a live
+    // offer) and the S pairs first -- measured no faster (the apply's tail moves into its items,
+    // profiles/r03/h_apply_c_first_ab.txt), so it is off
+    auto item = [&](unsigned v) -> unsigned {   // position -> index in the cells, S, C numbering
+        if (!kApplyCFirst || v >= n_items) return v;
+        if (v < nC0) return n_cell + n_sp + v;
+        if (v < nC0 + n_sp) return n_cell + (v - nC0);
+        return v - nC0 - n_sp;
+    };
     for (unsigned base = 0; base < n_items; base += S * kBatchApplyItems) {
         // three stages over the thread's items, so that their dependent loads overlap instead of
         // chaining item after item: (1) each item's first load -- its cell, an S key's two cells, a
@@ -1764,7 +1785,7 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
         uint4 ce[kBatchApplyItems];
 #pragma unroll
         for (unsigned u = 0; u < kBatchApplyItems; ++u) {
-            const unsigned v = base + u * S + g;
+            const unsigned v = item(base + u * S + g);
             dv[u] = 0;
             dw[u] = 0;
             ce[u] = make_uint4(0, 0, 0, 0);
@@ -1789,7 +1810,7 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
         bool touched[kBatchApplyItems];
 #pragma unroll
         for (unsigned u = 0; u < kBatchApplyItems; ++u) {
-            const unsigned v = base + u * S + g;
+            const unsigned v = item(base + u * S + g);
             how[u] = 0; ip[u] = 0; iq[u] = 0; delta[u] = 0; touched[u] = false;
             hk[u] = 0; hc[u] = 0; hf[u] = 0; kp[u] = 0; kq[u] = 0;
             if (v < n_cell) {
@@ -2245,6 +2266,53 @@ __global__ void k_index_emit(WordsDev<TokT> W, unsigned n, const uint32_t* __res
     }
 }
 
+// The same two passes per slot class, the slot in registers (one 16-byte load per 16 bytes of
+// slot, every index a compile-time constant): the first occurrence of each token of a word is a
+// register compare, not a dependent load per pair (k_index_count / k_index_emit load element by
+// element; kept for reference and the A/B)
+template <class TokT, int C, bool kEmit>
+__global__ void __launch_bounds__(256) k_index_cls(WordsDev<TokT> W, const uint32_t* __restrict__ pos,
+                                                   uint32_t* __restrict__ cnt, uint32_t* __restrict__ keys,
+                                                   uint32_t* __restrict__ vals) {
+    constexpr int Wd = slot_w(C);
+    constexpr int V = Wd * (int)sizeof(TokT) / 16;
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= W.c[C].n) return;
+    const unsigned f = W.off[C] + i;
+    uint4 r[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) r[v] = reinterpret_cast<const uint4*>(W.c[C].slot + (size_t)i * Wd)[v];
+    TokT e[Wd];
+    __builtin_memcpy(e, r, sizeof(e));
+    const uint32_t len = e[0];
+    uint32_t o = kEmit ? pos[f] : 0u, d = 0;
+    if (len >= 2) {
+#pragma unroll
+        for (int k = 1; k < Wd; ++k) {   // no early exit: a constant trip count keeps e[] in registers
+            bool first = (uint32_t)k <= len;
+#pragma unroll
+            for (int q = 1; q < k; ++q) first &= e[q] != e[k];
+            if (first) {
+                if (kEmit) { keys[o] = e[k]; vals[o] = f; ++o; }
+                else ++d;
+            }
+        }
+    }
+    if (!kEmit) cnt[f] = d;
+}
+
+template <class TokT, bool kEmit>
+void index_pass(const WordsDev<TokT>& W, const uint32_t* pos, uint32_t* cnt, uint32_t* keys, uint32_t* vals,
+                hipStream_t s) {
+    if (W.c[0].n) hipLaunchKernelGGL((k_index_cls<TokT, 0, kEmit>), dim3(ceil_div(W.c[0].n, 256u)), dim3(256), 0, s, W, pos, cnt, keys, vals);
+    if (W.c[1].n) hipLaunchKernelGGL((k_index_cls<TokT, 1, kEmit>), dim3(ceil_div(W.c[1].n, 256u)), dim3(256), 0, s, W, pos, cnt, keys, vals);
+    if (W.c[2].n) hipLaunchKernelGGL((k_index_cls<TokT, 2, kEmit>), dim3(ceil_div(W.c[2].n, 256u)), dim3(256), 0, s, W, pos, cnt, keys, vals);
+    if (W.c[3].n) hipLaunchKernelGGL((k_index_cls<TokT, 3, kEmit>), dim3(ceil_div(W.c[3].n, 256u)), dim3(256), 0, s, W, pos, cnt, keys, vals);
+}
+#ifndef BPE355_INDEX_REGS
+#define BPE355_INDEX_REGS 1
+#endif
+
 __global__ void k_index_bounds(const uint32_t* __restrict__ keys, unsigned long long e,
                                uint32_t* __restrict__ beg, uint32_t* __restrict__ len) {
     const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2619,7 +2687,8 @@ void MergeLoop<TokT>::build_index() {
     cnt.reserve(std::max(n, 1u));
     pos.reserve(std::max(n, 1u));
     if (n) {
-        hipLaunchKernelGGL(k_index_count<TokT>, dim3(ceil_div(n, 256)), dim3(256), 0, s_, wdev_, n, cnt.p);
+        if (BPE355_INDEX_REGS) index_pass<TokT, false>(wdev_, nullptr, cnt.p, nullptr, nullptr, s_);
+        else hipLaunchKernelGGL(k_index_count<TokT>, dim3(ceil_div(n, 256)), dim3(256), 0, s_, wdev_, n, cnt.p);
         exclusive_sum(cnt.p, pos.p, n, s_, &tmp);
         uint32_t last[2];
         BPE_HIP(hipMemcpyAsync(&last[0], pos.p + n - 1, 4, hipMemcpyDeviceToHost, s_));
@@ -2632,8 +2701,9 @@ void MergeLoop<TokT>::build_index() {
     keys2.reserve(std::max<unsigned long long>(E, 1));
     ilist_.reserve(std::max<unsigned long long>(E, 1));
     if (E) {
-        hipLaunchKernelGGL(k_index_emit<TokT>, dim3(ceil_div(n, 256)), dim3(256), 0, s_, wdev_, n, pos.p,
-                           keys.p, vals.p);
+        if (BPE355_INDEX_REGS) index_pass<TokT, true>(wdev_, pos.p, nullptr, keys.p, vals.p, s_);
+        else hipLaunchKernelGGL(k_index_emit<TokT>, dim3(ceil_div(n, 256)), dim3(256), 0, s_, wdev_, n, pos.p,
+                                keys.p, vals.p);
         int bits = 1;
         while ((1u << bits) < tcap) ++bits;
         radix_sort_pairs(keys.p, keys2.p, vals.p, ilist_.p, E, (unsigned)bits, s_, &tmp);
@@ -3167,6 +3237,22 @@ void MergeLoop<TokT>::report_probe() {
             const unsigned long long* p = &pr[kProbeSlots * t];
             if (p[30]) nls.push_back((double)p[30] - 1);
             if (p[27] && p[29]) rl.push_back(((long long)p[29] - (long long)p[27]) * 0.01);
+        }
+        {   // the rank stretch split: count ranks (27 -> 29), the barrier behind them (29 -> 31), the
+            // exact ranking and the top entries' stores (31 -> 28)
+            double a = 0, b = 0, c = 0;
+            int n = 0;
+            for (size_t t = 0; t + 1 < pr.size() / kProbeSlots; ++t) {
+                const unsigned long long* p = &pr[kProbeSlots * t];
+                if (!p[27] || !p[29] || !p[31] || !p[28]) continue;
+                a += ((long long)p[29] - (long long)p[27]) * 0.01;
+                b += ((long long)p[31] - (long long)p[29]) * 0.01;
+                c += ((long long)p[28] - (long long)p[31]) * 0.01;
+                ++n;
+            }
+            if (n)
+                std::fprintf(stderr, "[bpe355 probe] select rank: count ranks %.2f | barrier %.2f | exact rank + stores %.2f (%d trips)\n",
+                             a / n, b / n, c / n, n);
         }
         std::sort(nls.begin(), nls.end());
         std::sort(rl.begin(), rl.end());
