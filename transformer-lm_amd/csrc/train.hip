@@ -2715,7 +2715,9 @@ void MergeLoop<TokT>::build_index() {
     BPE_HIP(hipStreamSynchronize(s_));
     static const unsigned full_div = [] {
         const char* e = std::getenv("BPE355_FULL_DIV");   // experiment knob: scan when lists > n / div
-        return e ? (unsigned)std::max(1, std::atoi(e)) : 6u;
+        // n / 4 (r03 sweep, profiles/r03/m_full_div_sweep.txt: 2-4 give 258-264 ms of merges,
+        // 6 264-268, 9 275, 14 299)
+        return e ? (unsigned)std::max(1, std::atoi(e)) : 4u;
     }();
     idev_ = IndexDev{ilist_.p, ibeg_.p, ilen_.p, n / full_div, n};
     out_.stats.n_index_builds++;
