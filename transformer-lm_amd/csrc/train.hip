@@ -2867,6 +2867,16 @@ int MergeLoop<TokT>::rebuild() {
     return 0;
 }
 
+// posting lists are rebuilt (with a compaction) when the round count has grown by this factor
+// since the last build (experiment knob BPE355_INDEX_GROWTH)
+static double index_growth() {
+    static const double g = [] {
+        const char* e = std::getenv("BPE355_INDEX_GROWTH");
+        return e ? std::max(1.1, std::atof(e)) : 2.5;
+    }();
+    return g;
+}
+
 template <class TokT>
 void MergeLoop<TokT>::run() {
     st_.alloc(1);
@@ -3028,7 +3038,7 @@ void MergeLoop<TokT>::run() {
                 reset_tags();
                 push_state();
                 h_ms[2] += since(t0);
-                next_index_round_ = std::max(hs_.round + 512, (int)(hs_.round * 2.5));
+                next_index_round_ = std::max(hs_.round + 512, (int)(hs_.round * index_growth()));
             }
             continue;
         }
