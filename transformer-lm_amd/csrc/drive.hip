@@ -143,10 +143,20 @@ namespace {
 // few deep queues keep the copy engines busier than one queue per thread
 struct DmaStreams {
     std::vector<hipStream_t> s;
-    DmaStreams(int device, int n) {
+    DmaStreams(int device, int n) {   // on `device`; the calling thread's current device is kept
+        int cur = 0;
+        BPE_HIP(hipGetDevice(&cur));
         BPE_HIP(hipSetDevice(device));
         s.resize(n, nullptr);
-        for (auto& x : s) BPE_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+        hipError_t e = hipSuccess;
+        for (auto& x : s)
+            if (e == hipSuccess) e = hipStreamCreateWithFlags(&x, hipStreamNonBlocking);
+        BPE_HIP(hipSetDevice(cur));
+        if (e != hipSuccess) {
+            for (auto& x : s)
+                if (x) (void)hipStreamDestroy(x);
+            BPE_HIP(e);
+        }
     }
     ~DmaStreams() {
         for (auto& x : s)
