@@ -973,14 +973,19 @@ struct DeltaSinkN {
 // next trip's select start, 17-19 inside select's rule, 20/21 the last merge/apply workgroup's index
 constexpr int kProbeTrip = 8;
 constexpr int kProbeSlots = 32;   // 24-28: inside k_select's first phase
+// BPE355_PROBE_CODE=0 compiles the stamps out (code-size experiment; the default keeps them,
+// behind the run-time BPE355_PROBE switch)
+#ifndef BPE355_PROBE_CODE
+#define BPE355_PROBE_CODE 1
+#endif
 __device__ __forceinline__ void probe_stamp(const RoundState* st, int trip, int k) {
-    if (st->probe && (trip % kProbeTrip) == 0)
+    if (BPE355_PROBE_CODE && st->probe && (trip % kProbeTrip) == 0)
         st->probe[kProbeSlots * (size_t)(trip / kProbeTrip) + k] = __builtin_amdgcn_s_memrealtime();
 }
 // one workgroup of a sampled trip's kernel is done (thread 0, after the workgroup's work): the
 // last of the grid stamps slot k
 __device__ __forceinline__ void probe_done(RoundState* st, unsigned* ctr, int trip, int k) {
-    if (st->probe && (trip % kProbeTrip) == 0) {
+    if (BPE355_PROBE_CODE && st->probe && (trip % kProbeTrip) == 0) {
         const unsigned o = atomicAdd(ctr, 1u);
         if (o % gridDim.x == gridDim.x - 1) {
             probe_stamp(st, trip, k);
@@ -1051,7 +1056,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     const int ptrip = bs->trip;
     if (tid == 0) {
         probe_stamp(st, ptrip, 0);
-        if (ptrip > 0 && st->probe && ((ptrip - 1) % kProbeTrip) == 0)
+        if (BPE355_PROBE_CODE && ptrip > 0 && st->probe && ((ptrip - 1) % kProbeTrip) == 0)
             st->probe[kProbeSlots * (size_t)((ptrip - 1) / kProbeTrip) + 16] = __builtin_amdgcn_s_memrealtime();
     }
     // ---- every independent load first
@@ -1110,7 +1115,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         if (li == 0 && lold != 0xfffffffeu && lm.la != 0xfffffffeu) probe_stamp(st, ptrip, 25);   // metadata + dedupe
     }
     if (tid == 0) probe_stamp(st, ptrip, 26);   // wave 0's partials reduced
-    if (tid == 0 && st->probe && (ptrip % kProbeTrip) == 0) st->probe[kProbeSlots * (size_t)(ptrip / kProbeTrip) + 30] = ln + 1;
+    if (BPE355_PROBE_CODE && tid == 0 && st->probe && (ptrip % kProbeTrip) == 0) st->probe[kProbeSlots * (size_t)(ptrip / kProbeTrip) + 30] = ln + 1;
     __syncthreads();
     if (li == 0) probe_stamp(st, ptrip, 27);
     if (wv == 0) {   // P1 over the waves' bests, while the list waves rank (off the rule's path)
@@ -1628,7 +1633,7 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
     }
     if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 8);
     clear_prev();
-    if (st->probe) {
+    if (BPE355_PROBE_CODE && st->probe) {
         __syncthreads();
         if (tid == 0) probe_done(st, &st->probe_merge_done, B.trip, 14);
     }
@@ -1924,7 +1929,7 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
         }
     }
     if (pw0) probe_stamp(st, B.trip, 13);
-    if (!scan_only && st->probe) {
+    if (BPE355_PROBE_CODE && !scan_only && st->probe) {
         __syncthreads();
         if (tid == 0 && (B.trip % kProbeTrip) == 0) {   // workgroups that reserved list / C space
             unsigned long long* pr = st->probe + kProbeSlots * (size_t)(B.trip / kProbeTrip);
