@@ -195,7 +195,9 @@ int bpe_tok_encode_chunks_device(bpe_tokenizer* tok, const uint8_t* d_utf8, size
  * each piece encoded on its own, and the ids written as np.uint16 (encode.py:37; an id past
  * 65535 fails with BPE_E_LIMIT instead of wrapping) into ids_out (host memory, cap ids; the
  * file's byte count always suffices).  The device buffers are kept by the tokenizer across
- * calls.  The stages overlap: the file streams in by 1 GiB slabs while the pieces already read
+ * calls (about 3 bytes of HBM per file byte: the text and its uint16 ids, on top of the
+ * encoder's per-call arrays) until bpe_tok_release_buffers or bpe_tok_free.  The stages overlap:
+ * the file streams in by 1 GiB slabs while the pieces already read
  * are validated, encoded and copied out (a text with a carriage return is redone in one pass
  * once read).  phase_ms (NULL or 4 doubles): busy milliseconds of the reader, of validation +
  * piece starts, of the encodes and of the copy to host. */
@@ -206,6 +208,10 @@ int bpe_tok_encode_file_u16(bpe_tokenizer* tok, const char* path, size_t chars_p
  * piece, the ids are concatenated -- identical to bpe_tok_encode (tokenizer.py:111-138). */
 int bpe_tok_encode_gpus(bpe_tokenizer* tok, const uint8_t* utf8, size_t n, uint32_t* ids_out, size_t cap,
                         size_t* n_out, int n_gpus);
+/* Frees the device buffers the tokenizer keeps across calls (the encoder's record and scratch
+ * arrays, the bulk encoder's text and uint16 ids, the other devices' copies); the next call
+ * allocates them again.  The tables of the tokenizer itself stay. */
+int bpe_tok_release_buffers(bpe_tokenizer* tok);
 void bpe_tok_free(bpe_tokenizer* tok);
 
 /* ---------------------------------------------------------------- decode */

@@ -768,94 +768,127 @@ static int enc_segment(encoder* E, const uint8_t* s, size_t n, bbuf* out) {
     return c.rc;
 }
 
-int oracle_encode(const uint8_t* vocab_blob, size_t vocab_n, const uint8_t* merges_blob,
-                  size_t merges_n, const uint8_t* specials_blob, size_t specials_n,
-                  int specials_is_none, const uint8_t* text, size_t n, oracle_blob* out) {
-    encoder E; memset(&E, 0, sizeof(E));
-    st_init(&E.tok, 1 << 12);
-    st_init(&E.cache, 1 << 12);
-    pt_init(&E.rank);
+/* Tokenizer.__init__ (tokenizer.py:12-38) into E; the caller frees it with enc_free */
+static int enc_setup(encoder* E, const uint8_t* vocab_blob, size_t vocab_n, const uint8_t* merges_blob,
+                     size_t merges_n, const uint8_t* specials_blob, size_t specials_n, speclist* raw) {
+    memset(E, 0, sizeof(*E));
+    memset(raw, 0, sizeof(*raw));
+    st_init(&E->tok, 1 << 12);
+    st_init(&E->cache, 1 << 12);
+    pt_init(&E->rank);
     /* vocab blob: u32 count, then (i64 id, u32 len, bytes) in dict order; vocab_inv is
      * {v: k for k, v in vocab.items()} -> the last id wins (tokenizer.py:19) */
     uint32_t vc; size_t off = 4;
     if (vocab_n < 4) return OR_E_ARG;
     memcpy(&vc, vocab_blob, 4);
-    int64_t max_id = -1; size_t vsize = 0;
+    size_t vsize = 0;
     for (uint32_t i = 0; i < vc; i++) {
         int64_t id; uint32_t l;
         memcpy(&id, vocab_blob + off, 8); off += 8;
         memcpy(&l, vocab_blob + off, 4); off += 4;
-        size_t tid = st_intern(&E.tok, vocab_blob + off, l, NULL);
+        size_t tid = st_intern(&E->tok, vocab_blob + off, l, NULL);
         off += l;
-        enc_inv_set(&E, tid, id);
-        if (id > max_id) max_id = id;
+        enc_inv_set(E, tid, id);
         vsize++;
     }
     /* merges blob: u32 count, then (u32 la, a, u32 lb, b) */
     uint32_t mc; off = 4;
     memcpy(&mc, merges_blob, 4);
-    E.prod = malloc((mc ? mc : 1) * sizeof(uint32_t));
+    E->prod = malloc((mc ? mc : 1) * sizeof(uint32_t));
     for (uint32_t i = 0; i < mc; i++) {
         uint32_t la, lb;
         memcpy(&la, merges_blob + off, 4); off += 4;
         const uint8_t* pa = merges_blob + off; off += la;
         memcpy(&lb, merges_blob + off, 4); off += 4;
         const uint8_t* pb = merges_blob + off; off += lb;
-        uint32_t ta = (uint32_t)st_intern(&E.tok, pa, la, NULL);
-        uint32_t tb = (uint32_t)st_intern(&E.tok, pb, lb, NULL);
+        uint32_t ta = (uint32_t)st_intern(&E->tok, pa, la, NULL);
+        uint32_t tb = (uint32_t)st_intern(&E->tok, pb, lb, NULL);
         uint8_t* cat = malloc(la + lb + 1);
         memcpy(cat, pa, la); memcpy(cat + la, pb, lb);
-        E.prod[i] = (uint32_t)st_intern(&E.tok, cat, la + lb, NULL);
+        E->prod[i] = (uint32_t)st_intern(&E->tok, cat, la + lb, NULL);
         free(cat);
-        pslot* s = pt_get(&E.rank, PKEY(ta, tb), 1);
+        pslot* s = pt_get(&E->rank, PKEY(ta, tb), 1);
         s->count = i;                                     /* later duplicates overwrite */
     }
     /* specials: set() dedupe, then stable sort by length descending (tokenizer.py:29-30);
      * equal-length order only affects ids of missing specials -- we keep input order */
-    speclist raw;
-    int rc = parse_specials(specials_blob, specials_n, &raw);
+    int rc = parse_specials(specials_blob, specials_n, raw);
     if (rc) return rc;
-    E.sp.p = malloc((raw.count + 1) * sizeof(*E.sp.p));
-    E.sp.n = malloc((raw.count + 1) * sizeof(*E.sp.n));
-    for (size_t i = 0; i < raw.count; i++)
-        if (!is_special(&E.sp, raw.p[i], raw.n[i])) {
-            E.sp.p[E.sp.count] = raw.p[i]; E.sp.n[E.sp.count] = raw.n[i]; E.sp.count++;
+    E->sp.p = malloc((raw->count + 1) * sizeof(*E->sp.p));
+    E->sp.n = malloc((raw->count + 1) * sizeof(*E->sp.n));
+    for (size_t i = 0; i < raw->count; i++)
+        if (!is_special(&E->sp, raw->p[i], raw->n[i])) {
+            E->sp.p[E->sp.count] = raw->p[i]; E->sp.n[E->sp.count] = raw->n[i]; E->sp.count++;
         }
-    for (size_t i = 1; i < E.sp.count; i++) {             /* insertion sort, stable */
-        const uint8_t* pp = E.sp.p[i]; size_t nn = E.sp.n[i]; size_t j = i;
-        while (j > 0 && E.sp.n[j - 1] < nn) { E.sp.p[j] = E.sp.p[j - 1]; E.sp.n[j] = E.sp.n[j - 1]; j--; }
-        E.sp.p[j] = pp; E.sp.n[j] = nn;
+    for (size_t i = 1; i < E->sp.count; i++) {            /* insertion sort, stable */
+        const uint8_t* pp = E->sp.p[i]; size_t nn = E->sp.n[i]; size_t j = i;
+        while (j > 0 && E->sp.n[j - 1] < nn) { E->sp.p[j] = E->sp.p[j - 1]; E->sp.n[j] = E->sp.n[j - 1]; j--; }
+        E->sp.p[j] = pp; E->sp.n[j] = nn;
     }
-    (void)specials_is_none;
     /* missing specials get ids len(vocab), len(vocab)+1, ... (tokenizer.py:35-38) */
     size_t next_id = vsize;
-    for (size_t i = 0; i < E.sp.count; i++) {
-        size_t tid = st_intern(&E.tok, E.sp.p[i], E.sp.n[i], NULL);
-        if (enc_inv_get(&E, tid) < 0) { enc_inv_set(&E, tid, (int64_t)next_id); next_id++; }
+    for (size_t i = 0; i < E->sp.count; i++) {
+        size_t tid = st_intern(&E->tok, E->sp.p[i], E->sp.n[i], NULL);
+        if (enc_inv_get(E, tid) < 0) { enc_inv_set(E, tid, (int64_t)next_id); next_id++; }
     }
-    (void)max_id;
+    return OR_OK;
+}
 
-    /* segment (63-66): leftmost match, alternatives longest-first */
-    bbuf ob = {0};
+static void enc_free(encoder* E, speclist* raw) {
+    st_free(&E->tok); st_free(&E->cache); free(E->cache_ids.p); free(E->inv);
+    free(E->rank.s); free(E->prod); free(E->sp.p); free(E->sp.n); free(raw->p); free(raw->n);
+}
+
+/* Tokenizer.encode(text) (tokenizer.py:111-138): segment (63-66: leftmost match, alternatives
+ * longest-first), then each segment on its own; ids appended to ob */
+static int enc_text(encoder* E, const uint8_t* text, size_t n, bbuf* ob) {
+    int rc = OR_OK;
     size_t segstart = 0;
     for (size_t p = 0; p < n && rc == OR_OK;) {
         size_t hit = 0; int found = 0;
-        for (size_t k = 0; k < E.sp.count; k++)
-            if (E.sp.n[k] > 0 && p + E.sp.n[k] <= n && memcmp(text + p, E.sp.p[k], E.sp.n[k]) == 0) {
-                hit = E.sp.n[k]; found = 1; break;
+        for (size_t k = 0; k < E->sp.count; k++)
+            if (E->sp.n[k] > 0 && p + E->sp.n[k] <= n && memcmp(text + p, E->sp.p[k], E->sp.n[k]) == 0) {
+                hit = E->sp.n[k]; found = 1; break;
             }
         if (!found) { p++; continue; }
-        rc = enc_segment(&E, text + segstart, p - segstart, &ob);
-        if (rc == OR_OK) rc = enc_segment(&E, text + p, hit, &ob);
+        rc = enc_segment(E, text + segstart, p - segstart, ob);
+        if (rc == OR_OK) rc = enc_segment(E, text + p, hit, ob);
         p += hit; segstart = p;
     }
-    if (rc == OR_OK) rc = enc_segment(&E, text + segstart, n - segstart, &ob);
-
-    out->data = ob.p; out->n = ob.n;
-    st_free(&E.tok); st_free(&E.cache); free(E.cache_ids.p); free(E.inv);
-    free(E.rank.s); free(E.prod); free(E.sp.p); free(E.sp.n); free(raw.p); free(raw.n);
-    if (rc) { free(ob.p); out->data = NULL; out->n = 0; }
+    if (rc == OR_OK) rc = enc_segment(E, text + segstart, n - segstart, ob);
     return rc;
+}
+
+int oracle_encode(const uint8_t* vocab_blob, size_t vocab_n, const uint8_t* merges_blob,
+                  size_t merges_n, const uint8_t* specials_blob, size_t specials_n,
+                  int specials_is_none, const uint8_t* text, size_t n, oracle_blob* out) {
+    (void)specials_is_none;
+    return oracle_encode_pieces(vocab_blob, vocab_n, merges_blob, merges_n, specials_blob, specials_n,
+                                text, n, NULL, 0, out);
+}
+
+/* encode.py:31-36: the text read in pieces (f.read(1 M characters)), each piece encoded on its
+ * own and the ids concatenated.  starts: sorted byte offsets where pieces begin (0 implied). */
+int oracle_encode_pieces(const uint8_t* vocab_blob, size_t vocab_n, const uint8_t* merges_blob,
+                         size_t merges_n, const uint8_t* specials_blob, size_t specials_n,
+                         const uint8_t* text, size_t n, const uint64_t* starts, size_t n_starts,
+                         oracle_blob* out) {
+    encoder E; speclist raw;
+    out->data = NULL; out->n = 0;
+    int rc = enc_setup(&E, vocab_blob, vocab_n, merges_blob, merges_n, specials_blob, specials_n, &raw);
+    bbuf ob = {0};
+    size_t lo = 0;
+    for (size_t i = 0; i <= n_starts && rc == OR_OK; i++) {
+        size_t hi = i < n_starts ? (size_t)starts[i] : n;
+        if (hi > n) hi = n;
+        if (hi < lo) { rc = OR_E_ARG; break; }
+        if (hi > lo) rc = enc_text(&E, text + lo, hi - lo, &ob);
+        lo = hi;
+    }
+    enc_free(&E, &raw);
+    if (rc) { free(ob.p); return rc; }
+    out->data = ob.p; out->n = ob.n;
+    return OR_OK;
 }
 
 void oracle_free(oracle_blob* b) {

@@ -34,6 +34,11 @@ int oracle_pretokenize(const uint8_t* text, size_t n, oracle_blob* out);
 int oracle_encode(const uint8_t* vocab, size_t vocab_n, const uint8_t* merges, size_t merges_n,
                   const uint8_t* specials, size_t specials_n, int specials_is_none,
                   const uint8_t* text, size_t n, oracle_blob* out);
+/* encode.py:31-36: each piece [starts[i-1], starts[i]) (starts sorted byte offsets, 0 implied)
+ * encoded on its own, ids concatenated */
+int oracle_encode_pieces(const uint8_t* vocab, size_t vocab_n, const uint8_t* merges, size_t merges_n,
+                         const uint8_t* specials, size_t specials_n, const uint8_t* text, size_t n,
+                         const uint64_t* starts, size_t n_starts, oracle_blob* out);
 /* Chunked word counting + training (large corpora that do not fit in memory twice).  Each
  * fed piece must end at a safe split point (see bpe_oracle.c).  _train consumes the counts;
  * _words returns them as oracle_word_counts does. */

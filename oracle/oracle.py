@@ -7,6 +7,8 @@ Functions mirror the reference's semantics:
   train_raw(data, vocab_size, specials)      reference models/tokenizer/train.py:142-231
   word_counts(text_bytes, specials)          reference models/tokenizer/train.py:16-28
   encode(vocab, merges, specials, text)      reference models/tokenizer/tokenizer.py:111-138
+  PieceEncoder(...).encode(addr, n, starts)  reference models/tokenizer/encode.py:31-36 (each
+                                             piece encoded on its own), ids as numpy uint32
 """
 from __future__ import annotations
 
@@ -48,6 +50,9 @@ def lib():
         L.oracle_encode.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, u8p,
                                     ctypes.c_size_t, ctypes.c_int, u8p, ctypes.c_size_t,
                                     ctypes.POINTER(_Blob)]
+        L.oracle_encode_pieces.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, u8p,
+                                           ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                                           ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(_Blob)]
         L.oracle_decode_text.argtypes = [u8p, ctypes.c_size_t,
                                          ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)),
                                          ctypes.POINTER(ctypes.c_size_t),
@@ -224,6 +229,32 @@ def encode(vocab: dict, merges, specials, text: str):
     _check(rc, "encode")
     data = _take(blob)
     return list(struct.unpack(f"<{len(data) // 4}I", data)) if data else []
+
+
+class PieceEncoder:
+    """Tokenizer(vocab, merges, specials).encode over raw memory, for corpora too large for
+    Python strings: encode(addr, n, starts) encodes text[0:n) at address `addr` cut at the byte
+    offsets `starts` (each piece on its own, encode.py:31-36; no starts = encode(text)) and
+    returns the ids as a numpy uint32 array.  The call releases the GIL (ctypes), so one
+    PieceEncoder serves several threads."""
+
+    def __init__(self, vocab: dict, merges, specials):
+        self.vb, self.mb, self.sb = vocab_blob(vocab), merges_blob(merges), specials_blob(specials)
+
+    def encode(self, addr: int, n: int, starts=()):
+        import numpy as np
+        st = np.ascontiguousarray(np.asarray(starts, dtype=np.uint64))
+        blob = _Blob()
+        rc = lib().oracle_encode_pieces(self.vb, len(self.vb), self.mb, len(self.mb), self.sb,
+                                        len(self.sb), ctypes.c_void_p(addr), n,
+                                        ctypes.c_void_p(st.ctypes.data if st.size else 0), st.size,
+                                        ctypes.byref(blob))
+        _check(rc, "encode")
+        ids = np.empty(blob.n // 4, dtype=np.uint32)
+        if blob.n:
+            ctypes.memmove(ids.ctypes.data, blob.data, blob.n)
+        lib().oracle_free(ctypes.byref(blob))
+        return ids
 
 
 if os.environ.get("ORACLE_SELFTEST"):

@@ -303,3 +303,33 @@ def test_encode_file_late_carriage_return_and_bad_utf8(tmp_path, monkeypatch):
     with pytest.raises(UnicodeDecodeError) as e:
         encode_file(tok, src, chars_per_piece=k)
     assert e.value.start == pos
+
+
+@pytest.mark.parametrize("with_cr", [False, True])
+def test_encode_file_read_error_raises(tmp_path, monkeypatch, with_cr):
+    """a read that fails part way (EIO, a file truncated while read; injected by a test knob)
+    raises OSError and leaves no thread behind -- also on the carriage-return path, where the
+    text is redone in one pass once read (ADVICE r03: that path used to end in std::terminate)"""
+    from bpe_amd import Tokenizer
+    from bpe_amd.encode import encode_file
+    vocab, merges = gpt2_files.load_gpt2(["<|endoftext|>"])
+    tok = Tokenizer(dict(vocab), list(merges), ["<|endoftext|>"])
+    text = _mixed_text(13, 60000).replace("\r", "")
+    if with_cr:
+        text = "first line\r\n" + text
+    src = tmp_path / "t.txt"
+    src.write_bytes(text.encode("utf-8"))
+    monkeypatch.setenv("BPE355_READ_SLAB", "65536")
+    monkeypatch.setenv("BPE355_ENC_REGION", "30000")
+    monkeypatch.setenv("BPE355_TEST_READ_FAIL_AT", "150000")
+    assert src.stat().st_size > 200000
+    with pytest.raises(OSError):
+        encode_file(tok, src, chars_per_piece=4096)
+    monkeypatch.delenv("BPE355_TEST_READ_FAIL_AT")
+    # the tokenizer still works, with its buffers kept or released
+    with open(src, "r", encoding="utf-8") as f:
+        whole = f.read()
+    want = _encode_chunks(tok, whole.encode("utf-8"), _piece_starts(whole, 4096))
+    assert encode_file(tok, src, chars_per_piece=4096, keep_device_buffers=True).tolist() == want
+    tok.release_device_buffers()
+    assert encode_file(tok, src, chars_per_piece=4096).tolist() == want

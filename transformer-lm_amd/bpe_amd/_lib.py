@@ -105,6 +105,7 @@ _SIGS = [
     ("bpe_tok_encode_chunks_device", ctypes.c_int, [_P, _P, _SZ, _P, _SZ, _P, ctypes.POINTER(_SZ), _P]),
     ("bpe_tok_encode_file_u16", ctypes.c_int, [_P, ctypes.c_char_p, _SZ, _P, _SZ, ctypes.POINTER(_SZ),
                                                ctypes.POINTER(ctypes.c_double)]),
+    ("bpe_tok_release_buffers", ctypes.c_int, [_P]),
     ("bpe_tok_free", None, [_P]),
     ("bpe_dec_create", ctypes.c_int, [_U8P, _SZ, ctypes.POINTER(_P)]),
     ("bpe_dec_decode", ctypes.c_int, [_P, _P, _SZ, _P, _SZ, ctypes.POINTER(_SZ)]),

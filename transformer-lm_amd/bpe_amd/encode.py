@@ -124,10 +124,17 @@ def encode_file_native(tokenizer: Tokenizer, path, chars_per_piece: int = CHARS_
 
 
 def encode_file(tokenizer: Tokenizer, input_path, output_path=None, fmt: str = "pt",
-                chars_per_piece: int = CHARS_PER_PIECE) -> np.ndarray:
-    """Encode a text file like encode.py:main; write it if output_path is given."""
+                chars_per_piece: int = CHARS_PER_PIECE, keep_device_buffers: bool = False) -> np.ndarray:
+    """Encode a text file like encode.py:main; write it if output_path is given.  The device
+    buffers of the bulk encoder (about 3 bytes of HBM per file byte) are released afterwards
+    unless keep_device_buffers (several files in a row: re-allocating tens of GB costs the driver
+    up to seconds per call)."""
     if stat.S_ISREG(os.stat(input_path).st_mode):   # missing: FileNotFoundError, as open() raises
-        pt = encode_file_native(tokenizer, input_path, chars_per_piece)
+        try:
+            pt = encode_file_native(tokenizer, input_path, chars_per_piece)
+        finally:
+            if not keep_device_buffers:
+                tokenizer.release_device_buffers()
     else:
         with open(input_path, "rb") as f:
             data = f.read()

@@ -112,6 +112,12 @@ class Tokenizer:
             except Exception:  # noqa: BLE001
                 pass
 
+    def release_device_buffers(self) -> None:
+        """Free the device memory the encoder keeps between calls (its per-call arrays and the
+        bulk encoder's text and uint16 ids, about 3 bytes per input byte); the tables stay."""
+        if self._handle is not None:
+            _lib.check(_lib.lib().bpe_tok_release_buffers(self._handle), "release")
+
     # ------------------------------------------------------------------ encode / decode
     def encode(self, text: str) -> List[int]:
         """tokenizer.py:111-138 on the GPU."""

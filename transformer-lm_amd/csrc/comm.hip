@@ -81,6 +81,9 @@ struct InProcShared {
     std::vector<int64_t> acc, result;
     std::vector<uint8_t> gather;   // all-gather: rank r's segment at r * bytes
     int g_entered = 0, g_readers = 0;
+    // a rank left a collective with an error: every rank waiting in (or later entering) one
+    // throws instead of waiting for it forever
+    bool failed = false;
 };
 
 struct InProcComm final : Comm {
@@ -91,62 +94,89 @@ struct InProcComm final : Comm {
         rank = r;
         device = dev;
     }
+    // runs op; any exception it throws marks the group failed (waking every waiter) and goes on
+    template <class Op>
+    void guarded(const Op& op) {
+        try {
+            op();
+        } catch (...) {
+            {
+                std::lock_guard<std::mutex> g(sh->m);
+                sh->failed = true;
+            }
+            sh->cv.notify_all();
+            throw;
+        }
+    }
+    void check_failed() const {   // sh->m held
+        BPE_REQUIRE(!sh->failed, BPE_E_RCCL, "in-process collective: another rank failed");
+    }
     void allreduce_i64(int64_t* d_buf, size_t count, hipStream_t stream) override {
         if (count == 0) return;
-        h.resize(count);
-        BPE_HIP(hipMemcpyAsync(h.data(), d_buf, count * 8, hipMemcpyDeviceToHost, stream));
-        BPE_HIP(hipStreamSynchronize(stream));
-        {
-            std::unique_lock<std::mutex> lk(sh->m);
-            const uint64_t g = sh->gen;
-            if (sh->arrived == 0) sh->acc.assign(count, 0);
-            BPE_REQUIRE(sh->acc.size() == count, BPE_E_RCCL, "in-process all-reduce: ranks disagree on the size");
-            for (size_t i = 0; i < count; ++i) sh->acc[i] += h[i];
-            if (++sh->arrived == nranks) {
-                sh->result.swap(sh->acc);
-                sh->arrived = 0;
-                ++sh->gen;
-                sh->cv.notify_all();
-            } else {
-                sh->cv.wait(lk, [&] { return sh->gen != g; });
+        guarded([&] {
+            h.resize(count);
+            BPE_HIP(hipMemcpyAsync(h.data(), d_buf, count * 8, hipMemcpyDeviceToHost, stream));
+            BPE_HIP(hipStreamSynchronize(stream));
+            {
+                std::unique_lock<std::mutex> lk(sh->m);
+                check_failed();
+                const uint64_t g = sh->gen;
+                if (sh->arrived == 0) sh->acc.assign(count, 0);
+                BPE_REQUIRE(sh->acc.size() == count, BPE_E_RCCL, "in-process all-reduce: ranks disagree on the size");
+                for (size_t i = 0; i < count; ++i) sh->acc[i] += h[i];
+                if (++sh->arrived == nranks) {
+                    sh->result.swap(sh->acc);
+                    sh->arrived = 0;
+                    ++sh->gen;
+                    sh->cv.notify_all();
+                } else {
+                    sh->cv.wait(lk, [&] { return sh->gen != g || sh->failed; });
+                    check_failed();
+                }
+                h = sh->result;
             }
-            h = sh->result;
-        }
-        BPE_HIP(hipMemcpyAsync(d_buf, h.data(), count * 8, hipMemcpyHostToDevice, stream));
-        BPE_HIP(hipStreamSynchronize(stream));
+            BPE_HIP(hipMemcpyAsync(d_buf, h.data(), count * 8, hipMemcpyHostToDevice, stream));
+            BPE_HIP(hipStreamSynchronize(stream));
+        });
     }
     // ncclAllGather's contract: every rank copies its segment into one shared host buffer, and
     // after the last rank arrives each one copies the whole buffer back (no zero-padded sum)
     void allgather_bytes(const void* d_send, size_t bytes, void* d_recv, hipStream_t stream) override {
         if (bytes == 0) return;
-        std::unique_lock<std::mutex> lk(sh->m);
-        // a rank done with the previous gather may not reset the buffer others still read
-        sh->cv.wait(lk, [&] { return sh->g_readers == 0; });
-        const uint64_t g = sh->gen;
-        if (sh->g_entered++ == 0) sh->gather.assign((size_t)nranks * bytes, 0);
-        BPE_REQUIRE(sh->gather.size() == (size_t)nranks * bytes, BPE_E_RCCL,
-                    "in-process all-gather: ranks disagree on the size");
-        uint8_t* mine = sh->gather.data() + (size_t)rank * bytes;
-        lk.unlock();   // the copies of the ranks' own segments run concurrently
-        BPE_HIP(hipMemcpyAsync(mine, d_send, bytes, hipMemcpyDeviceToHost, stream));
-        BPE_HIP(hipStreamSynchronize(stream));
-        lk.lock();
-        if (++sh->arrived == nranks) {
-            sh->arrived = 0;
-            sh->g_entered = 0;
-            sh->g_readers = nranks;
-            ++sh->gen;
+        guarded([&] {
+            std::unique_lock<std::mutex> lk(sh->m);
+            // a rank done with the previous gather may not reset the buffer others still read
+            sh->cv.wait(lk, [&] { return sh->g_readers == 0 || sh->failed; });
+            check_failed();
+            const uint64_t g = sh->gen;
+            if (sh->g_entered == 0) sh->gather.assign((size_t)nranks * bytes, 0);
+            BPE_REQUIRE(sh->gather.size() == (size_t)nranks * bytes, BPE_E_RCCL,
+                        "in-process all-gather: ranks disagree on the size");
+            ++sh->g_entered;
+            uint8_t* mine = sh->gather.data() + (size_t)rank * bytes;
+            lk.unlock();   // the copies of the ranks' own segments run concurrently
+            BPE_HIP(hipMemcpyAsync(mine, d_send, bytes, hipMemcpyDeviceToHost, stream));
+            BPE_HIP(hipStreamSynchronize(stream));
+            lk.lock();
+            check_failed();
+            if (++sh->arrived == nranks) {
+                sh->arrived = 0;
+                sh->g_entered = 0;
+                sh->g_readers = nranks;
+                ++sh->gen;
+                sh->cv.notify_all();
+            } else {
+                sh->cv.wait(lk, [&] { return sh->gen != g || sh->failed; });
+                check_failed();
+            }
+            const uint8_t* all = sh->gather.data();
+            lk.unlock();
+            BPE_HIP(hipMemcpyAsync(d_recv, all, (size_t)nranks * bytes, hipMemcpyHostToDevice, stream));
+            BPE_HIP(hipStreamSynchronize(stream));
+            lk.lock();
+            --sh->g_readers;
             sh->cv.notify_all();
-        } else {
-            sh->cv.wait(lk, [&] { return sh->gen != g; });
-        }
-        const uint8_t* all = sh->gather.data();
-        lk.unlock();
-        BPE_HIP(hipMemcpyAsync(d_recv, all, (size_t)nranks * bytes, hipMemcpyHostToDevice, stream));
-        BPE_HIP(hipStreamSynchronize(stream));
-        lk.lock();
-        --sh->g_readers;
-        sh->cv.notify_all();
+        });
     }
 };
 

@@ -1331,11 +1331,16 @@ size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint
     // experiment knob: BPE355_ENC_OVERLAP=0 reads the whole file before the first encode
     const char* ov = std::getenv("BPE355_ENC_OVERLAP");
     const bool overlap_read = !(ov && ov[0] == '0');
+    // test knob: the read fails once it reaches this byte offset (an EIO or a file truncated
+    // while it is read)
+    const size_t fail_at = env_size("BPE355_TEST_READ_FAIL_AT", 0);
     std::thread reader([&] {
         const auto t0 = clk::now();
         try {
             for (size_t off = 0; off < n && !stop.load(); off += read_slab) {
                 const size_t len = std::min(read_slab, n - off);
+                if (fail_at && off + len >= fail_at)
+                    throw Error{BPE_E_IO, "read failed (injected by BPE355_TEST_READ_FAIL_AT)"};
                 stage_to_device(src, off, len, text + off, dev, io_n);
                 std::lock_guard<std::mutex> g(m);
                 loaded = off + len;
@@ -1450,10 +1455,17 @@ size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint
         finish_threads();
         throw;
     }
-    if (serial) {   // the rest of the file first
-        std::unique_lock<std::mutex> g(m);
-        cv.wait(g, [&] { return read_done; });
-        if (read_err) std::rethrow_exception(read_err);
+    if (serial) {   // the rest of the file first; on a read error both threads are joined first
+        std::exception_ptr e;
+        {
+            std::unique_lock<std::mutex> g(m);
+            cv.wait(g, [&] { return read_done; });
+            e = read_err;
+        }
+        if (e) {
+            finish_threads();
+            std::rethrow_exception(e);
+        }
     }
     finish_threads();
     if (copy_err) std::rethrow_exception(copy_err);
@@ -1594,6 +1606,17 @@ int bpe_tok_encode_gpus(bpe_tokenizer* tok, const uint8_t* utf8, size_t n, uint3
         *n_out = 0;
         if (n == 0) return;
         *n_out = bpe::encode_gpus(*tok, utf8, n, ids_out, n_gpus);
+    });
+}
+
+int bpe_tok_release_buffers(bpe_tokenizer* tok) {
+    return bpe::guarded_enc([&] {
+        BPE_REQUIRE(tok, BPE_E_ARG, "NULL argument");
+        BPE_HIP(hipStreamSynchronize(tok->stream));
+        tok->recs_cache = bpe::DevBuf<uint32_t>();
+        tok->sc = bpe_tokenizer::Scratch();
+        std::lock_guard<std::mutex> g(tok->copies_m);
+        tok->copies.clear();
     });
 }
 

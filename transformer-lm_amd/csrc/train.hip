@@ -905,6 +905,10 @@ __global__ void __launch_bounds__(256) k_argmax(RoundState* __restrict__ st, Pai
 #define BPE355_MAX_BATCH 16
 #endif
 constexpr int kMaxBatch = BPE355_MAX_BATCH;   // members per trip (3 * kMaxBatch tokens fit one wave)
+static_assert(kMaxBatch >= 1 && kMaxBatch <= 21, "BPE355_MAX_BATCH: 1..21 (3 * members fit one wave)");
+// the largest power of two <= kMaxBatch - 1: the first step of a binary search over members
+constexpr int top_step(int m) { int p = 1; while (2 * p <= m) p *= 2; return m >= 1 ? p : 0; }
+constexpr int kListTopStep = top_step(kMaxBatch - 1);
 constexpr int kTopM = kMaxBatch + 1;
 // the select's clash check: candidates i < kClashI (a power of two >= kMaxBatch), kClashJ lanes each
 constexpr int kClashI = kMaxBatch <= 16 ? 16 : 32;
@@ -1594,8 +1598,9 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
             const unsigned total = B.list_pre[k];
             for (unsigned i = bid * blockDim.x + tid; i < total; i += nb * blockDim.x) {
                 int j = 0;
-                // the member whose list holds entry i: binary search of the LDS prefix sums
-                for (int step = kMaxBatch / 2; step > 0; step >>= 1)
+                // the member whose list holds entry i: binary search of the LDS prefix sums, steps
+                // from the largest power of two below kMaxBatch (any cap, not only powers of two)
+                for (int step = kListTopStep; step > 0; step >>= 1)
                     if (j + step < k && i >= s_pre[j + step]) j += step;
                 const unsigned f = X.list[s_lbeg[j] + (i - s_pre[j])];
                 // a word on several members' lists is rewritten by the first thread to claim it
