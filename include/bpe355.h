@@ -157,6 +157,9 @@ typedef struct {
     int64_t n_count_records;  /* pre-tokens (or cache entries) spilled as records by the counter */
     double count_partial_ms;  /* device time of the aggregations done while the file was loading */
     int64_t n_count_batches;  /* aggregation batches (1 + those done during the load) */
+    double t_gather_ms;       /* multi-GPU word exchange: the all-gather of the segments */
+    double t_union_ms;        /* multi-GPU word exchange: the union-table inserts */
+    int64_t exchange_seg_bytes; /* multi-GPU word exchange: one rank's segment (all ranks' equal) */
 } bpe_train_stats;
 int bpe_result_stats(const bpe_result* r, bpe_train_stats* out);
 void bpe_result_free(bpe_result* r);

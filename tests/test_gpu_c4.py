@@ -103,6 +103,15 @@ def test_c4_eight_ranks_words_full_owt(inproc):
     assert st["n_exchanged_words"] >= o["n_words_multibyte"]
     assert st["n_words"] == o["n_words_multibyte"]
     _check(o, vocab, merges, "C4 words x8")
+    # the exchange's measured parts (DESIGN.md section 5's table): recorded when asked
+    out = os.environ.get("BPE355_STATS_OUT")
+    if out:
+        keep = ("t_total_ms", "t_load_ms", "t_count_ms", "t_exchange_ms", "t_gather_ms", "t_union_ms",
+                "exchange_seg_bytes", "n_exchanged_words", "n_words", "t_words_ms", "t_merge_ms", "n_gpus")
+        with open(out, "w") as f:
+            json.dump({"test": "test_c4_eight_ranks_words_full_owt", "ranks": "8 in-process ranks sharing one "
+                       "GPU; all-gather through host memory (the in-process communicator)",
+                       **{k: st[k] for k in keep}}, f, indent=1)
 
 
 def test_c4_two_ranks_rounds_1g(inproc):

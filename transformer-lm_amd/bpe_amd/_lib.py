@@ -43,6 +43,8 @@ class TrainStats(ctypes.Structure):
         ("t_load_ms", ctypes.c_double), ("n_gpus", ctypes.c_int64),
         ("count_reduce_ms", ctypes.c_double), ("n_count_records", ctypes.c_int64),
         ("count_partial_ms", ctypes.c_double), ("n_count_batches", ctypes.c_int64),
+        ("t_gather_ms", ctypes.c_double), ("t_union_ms", ctypes.c_double),
+        ("exchange_seg_bytes", ctypes.c_int64),
     ]
 
     def as_dict(self):

@@ -1,12 +1,15 @@
 """Communicators for sharded training (one process per GPU).
 
-The per-round exchange of the sharded merge loop is ONE int64 sum all-reduce of the pair-count
-delta cells.  Two ways to provide it:
+The default exchange is ONE all-gather of the ranks' unique-word tables after the local counts;
+every rank then runs the merge loop on the union.  The per-round protocol
+(BPE355_EXCHANGE=rounds: one int64 sum all-reduce of the pair-count delta cells per merge round,
+SURVEY.md 8e) is kept and tested but slower.  Two ways to provide the collectives:
 
   Communicator.from_torch()   RCCL over xGMI (bpe_comm_init): the id is created on rank 0 and
                               broadcast through an initialised torch.distributed group.
   HostCommunicator(group)     host-staged: the library hands a host buffer to a callback that
-                              all-reduces it with torch.distributed (e.g. gloo).  For tests and
+                              all-reduces it with torch.distributed (e.g. gloo); the library's
+                              all-gather goes through it as a sum of zero-padded segments.  For tests and
                               for several ranks sharing one GPU, which RCCL refuses.
 
 Either is passed as `comm=` to train_bpe / train_bpe_bytes / train_bpe_device and must be

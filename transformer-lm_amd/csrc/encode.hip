@@ -8,15 +8,19 @@
 //           merge rank (ties: leftmost) until no pair is ranked; ids via vocab_inv (KeyError)
 //
 // Device pipeline (one stream):
-//   1. k_find_specials marks where a special starts (first-byte bitmap, then compare);
-//      the sparse candidate list is resolved left-to-right on the host into segments.
-//   2. k_scan<INSERT>: threads own byte spans that start/stop at boundary points (segment
-//      starts, or safe points inside normal segments) and insert every pre-token into a
-//      unique-word table keyed by (length, first offset), exactly like training's count.
-//   3. k_encode_words: one thread per unique word runs the rank-ordered merge loop against a
-//      device hash map (pair -> rank, product) and writes its vocab ids once (word cache).
-//   4. k_scan<COUNT> + exclusive scan + k_scan<WRITE>: re-walk the pre-tokens and emit each
-//      occurrence's cached ids at its output offset, specials as their ids.
+//   0. (once per tokenizer) build_dictionary: every vocab entry of 2..16 bytes encoded by
+//      k_encode_words into an L2-sized open-addressing table, and the one-byte words' ids.
+//   1. k_find_specials marks where a special starts (first-byte bitmap, then compare); the
+//      sorted matches become the segment table on the device (k_sp_*), or on the host when
+//      matches overlap.
+//   2. k_enc_scan3: persistent workgroups stage 16 KiB chunks in LDS, evaluate the token-start
+//      predicate per 64-byte block, and write one u32 record per pre-token, each chunk's records
+//      one dense run: a direct id (one-byte words, one-id dictionary words, via an LDS word
+//      cache), a special, a dictionary entry, or the slot of a word-table entry (the long tail).
+//   3. k_collect + k_encode_words: the word table's words get their rank-ordered merges once.
+//   4. k_enc_emit: one pass over the records -- per chunk, ids counted (gathers issued together),
+//      the chunk's output offset by decoupled look-back, ids assembled in LDS and stored with
+//      coalesced writes.
 
 #include <algorithm>
 #include <atomic>
@@ -165,18 +169,53 @@ __global__ void k_sp_emit(const unsigned long long* __restrict__ keys, size_t me
     }
 }
 
-// ------------------------------------------------------------------ 2. segment-aware scan
-// Persistent workgroups stream the text in kChunk pieces staged in LDS (stage.h), like the
-// training counter.  Scan boundaries are segment starts and safe points inside normal
-// segments; thread t of chunk c owns the pre-tokens starting in [first boundary >= its nominal
-// start, first boundary >= its nominal end).  Each pre-token is found or inserted in the word
-// table (an LDS cache maps words <= 16 bytes to their slot) and recorded as one u32 -- its
-// slot, or kSpecialRec | special index -- at recs[span start + k]: a span of B bytes holds at
-// most B pre-tokens, so the records of all spans fit in an n-entry array with no prefix sum.
-constexpr uint32_t kSpecialRec = 0x80000000u;
-constexpr int kEncCache = 512;    // with 4 workgroups per CU (k_enc_scan2): 36.0 vs 34.9 GB/s at 1024 / 3
+// ------------------------------------------------------------------ 2. the scan: one record per pre-token
+// Records.  Every pre-token becomes one u32; the top two bits say what it names:
+//   kRecDirect | id    a word of exactly one vocab id, known during the scan: one-byte words
+//                      (the byte table) and the dictionary's one-id words
+//   kRecSpecial | k    special token k (one id)
+//   kRecDict | slot    a dictionary word of several ids (or none), ids in the dictionary's pool
+//   slot               a word-table slot: a word first met in this text, encoded after the scan
+//                      by k_encode_words (slot_info)
+// The dictionary (built once per tokenizer, build_dictionary) holds every vocab entry of 2..16
+// bytes with its encoding: a pre-token's ids depend only on its bytes (tokenizer.py:124-136), so
+// any word found there needs neither the word table nor a gather later.  Frequent words of a
+// corpus are the vocab's own entries, so most pre-tokens resolve in the LDS cache, the byte
+// table or the dictionary (2 MB, L2-resident), and only the long tail reaches the word table.
+constexpr uint32_t kRecKind = 0xC0000000u;
+constexpr uint32_t kRecDirect = 0xC0000000u;
+constexpr uint32_t kRecSpecial = 0x80000000u;
+constexpr uint32_t kRecDict = 0x40000000u;
+constexpr uint32_t kRecPayload = 0x3FFFFFFFu;   // ids and slots of direct / dictionary records < this
+constexpr uint32_t kRecNone = 0xFFFFFFFFu;      // byte table / dictionary lookup: no record
+
+struct DictEnt {               // 32 bytes: one probe is one aligned 32-byte read
+    uint64_t lo, hi;           // packed bytes
+    uint32_t len;              // 0: an empty slot
+    uint32_t rec;              // the word's record (kRecDirect | id, or kRecDict | this slot)
+    unsigned long long info;   // its ids (slot_info format below; the pool is the dictionary's)
+};
+struct EncDict {
+    const DictEnt* ent;
+    unsigned long long mask;   // slots - 1
+    const uint32_t* pool;
+    const uint32_t* byte_rec;  // 256 records of the one-byte words (kRecNone: through the table)
+};
+
+__device__ __forceinline__ uint32_t dict_find(const EncDict& D, uint64_t wl, uint64_t wh, uint32_t len, uint64_t h) {
+    size_t sl = h & D.mask;
+    for (;;) {
+        const DictEnt e = D.ent[sl];
+        if (e.len == 0) return kRecNone;
+        if (e.len == len && e.lo == wl && e.hi == wh) return e.rec;
+        sl = (sl + 1) & D.mask;
+    }
+}
+
+constexpr int kEncCache = 512;    // LDS word cache (2-way): word -> record
 constexpr int kEncEpoch = 4;
 constexpr unsigned kEncKeep = 2;
+constexpr int kSegLds = 64;
 
 __device__ __forceinline__ int seg_of(const Seg* __restrict__ segs, int nseg, size_t p) {
     int lo = 0, hi = nseg - 1;  // last segment with start <= p
@@ -187,203 +226,6 @@ __device__ __forceinline__ int seg_of(const Seg* __restrict__ segs, int nseg, si
     }
     return lo;
 }
-
-// first scan boundary at or after global position p, looking no further than `limit`
-// (returns ~0 if none below it).  Reads go through `byte(q)`.
-template <class ByteAt>
-__device__ __forceinline__ size_t first_boundary(const Seg* __restrict__ segs, int nseg, size_t p,
-                                                 size_t limit, const ByteAt& byte) {
-    int k = seg_of(segs, nseg, p);
-    while (p < limit) {
-        const Seg sg = segs[k];
-        if (p == sg.start) return p;
-        if (sg.special >= 0) {           // inside a special: the next segment starts a scan
-            p = sg.end;
-            ++k;
-            continue;
-        }
-        const size_t stop = sg.end < limit ? sg.end : limit;
-        for (; p < stop; ++p) {
-            if (p + 1 < sg.end && byte(p) == 0x20 && ascii_nonspace(byte(p - 1)) &&
-                ascii_nonspace(byte(p + 1)))
-                return p;
-        }
-        if (p == sg.end) ++k;            // p is the next segment's start: a boundary
-    }
-    return ~(size_t)0;
-}
-
-template <bool kAligned>
-__global__ void __launch_bounds__(256, 3)
-k_enc_scan(const uint8_t* __restrict__ s, size_t n, size_t n_chunks, const Seg* __restrict__ segs,
-           int nseg, unsigned long long* __restrict__ kv, unsigned long long* __restrict__ pos,
-           size_t mask, unsigned long long max_fill, unsigned long long* __restrict__ fill,
-           uint32_t* __restrict__ recs, unsigned long long* __restrict__ t_start,
-           uint32_t* __restrict__ t_count, unsigned* __restrict__ status, int use_cache) {
-    __shared__ unsigned long long c_key[kEncCache];
-    __shared__ uint64_t c_lo[kEncCache], c_hi[kEncCache];
-    __shared__ uint32_t c_slot[kEncCache];
-    __shared__ uint16_t c_hit[kEncCache], c_mark[kEncCache];   // hit counts mod 2^16 per epoch
-    __shared__ uint32_t s_start[257];   // relative to the chunk; kNotFound: past the window
-    __shared__ unsigned long long s_red[4];
-    __shared__ int s_stop;
-    const int tid = threadIdx.x;
-    for (int i = tid; i < kEncCache; i += blockDim.x) { c_key[i] = 0; c_hit[i] = 0; c_mark[i] = 0; }
-    unsigned long long inserted = 0;
-
-    // one pre-token [p, p + len) of src (global position gp); returns its record
-    auto word_rec = [&](const auto& src, auto p, size_t len, size_t gp) -> uint32_t {
-        if (len >= (1ULL << 24)) { atomicOr(status, 2u); return 0u; }
-        bool ins = false;
-        if (len <= (size_t)kInline) {
-            uint64_t wl = 0, wh = 0;
-            for (uint32_t i = 0; i < (uint32_t)len; ++i) {
-                const uint64_t b = src[p + i];
-                if (i < 8) wl |= b << (8 * i);
-                else wh |= b << (8 * (i - 8));
-            }
-            const uint64_t h = short_hash(wl, wh, len);
-            const unsigned ls = (unsigned)(h >> 40) & (kEncCache - 2);
-            for (int way = 0; way < 2 && use_cache; ++way) {
-                const unsigned sl = ls + way;
-                const unsigned long long k = c_key[sl];
-                if (k != 0 && k != kBusy && (k >> 40) == len) {
-                    __asm__ volatile("" ::: "memory");
-                    if (c_lo[sl] == wl && c_hi[sl] == wh) {
-                        c_hit[sl] = (uint16_t)(c_hit[sl] + 1);   // a heuristic: races may drop hits
-                        return c_slot[sl];
-                    }
-                }
-            }
-            const size_t slot = table_add(s, s, gp, len, wl, wh, h, 0, kv, pos, mask, status, &ins);
-            inserted += ins;
-            if (slot == ~(size_t)0) return 0u;
-            for (int way = 0; way < 2 && use_cache; ++way) {   // cache it if a way is free
-                const unsigned sl = ls + way;
-                if (c_key[sl] == 0 && atomicCAS(&c_key[sl], 0ULL, kBusy) == 0) {
-                    c_lo[sl] = wl;
-                    c_hi[sl] = wh;
-                    c_slot[sl] = (uint32_t)slot;
-                    // the entry's LDS writes complete before the key publishes it
-                    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    atomicExch(&c_key[sl], ((unsigned long long)len << 40) | (gp + 1));
-                    break;
-                }
-            }
-            return (uint32_t)slot;
-        }
-        const size_t slot = table_add(s, s, gp, len, 0, 0, hash_word(s, gp, len), 0, kv, pos, mask,
-                                      status, &ins);
-        inserted += ins;
-        return slot == ~(size_t)0 ? 0u : (uint32_t)slot;
-    };
-
-    uint4 pre[kVec];
-    if (blockIdx.x < n_chunks) stage_fetch<kAligned>(pre, s, n, (size_t)blockIdx.x * kChunk, tid);
-    for (size_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
-        __syncthreads();
-        stage_store(pre, tid);
-        if (tid == 0) s_stop = *(volatile unsigned long long*)fill > max_fill;
-        __syncthreads();
-        if (s_stop) {
-            if (tid == 0) atomicOr(status, 1u);
-            break;
-        }
-        if (c + gridDim.x < n_chunks) stage_fetch<kAligned>(pre, s, n, (c + gridDim.x) * kChunk, tid);
-
-        const size_t base = c * kChunk;
-        const size_t rem = n - base;
-        const bool text_ends = rem <= (size_t)kWin;
-        const size_t wend = base + (text_ends ? rem : (size_t)kWin);   // staged: [base, wend)
-        const LdsText L{};
-        // staged reads, one byte left of the window from global memory
-        auto byte_at = [&](size_t q) -> uint8_t {
-            return q >= base ? L[(uint32_t)(q - base)] : s[q];
-        };
-        // span starts: first boundary >= nominal start, searched inside the window
-        // (~0: past it; at the end of the text, n)
-        auto find = [&](size_t q) -> uint32_t {
-            if (q >= n) return (uint32_t)(n - base);
-            const size_t lim = text_ends ? n : wend - 2;
-            const size_t b = first_boundary(segs, nseg, q, lim, byte_at);
-            return b != ~(size_t)0 ? (uint32_t)(b - base) : (text_ends ? (uint32_t)(n - base) : kNotFound);
-        };
-        s_start[tid] = find(base + (size_t)tid * 64);
-        if (tid == 0) s_start[256] = find(base + kChunk);
-        __syncthreads();
-        const uint32_t r0 = s_start[tid], r1 = s_start[tid + 1];
-        const unsigned long long g0 = r0 == kNotFound ? ~0ULL : base + r0;
-        const unsigned long long g1 = r1 == kNotFound ? ~0ULL : base + r1;
-        const size_t gt = c * 256 + tid;
-        uint32_t k = 0;
-        if (g0 != ~0ULL) {
-            const bool fast = g1 != ~0ULL;
-            const size_t hi = base + (size_t)tid * 64 + 64;
-            size_t p = g0;
-            int sk = seg_of(segs, nseg, p);
-            Seg sg = segs[sk];                  // current segment, kept in registers
-            for (;;) {
-                if (fast ? p >= g1 : p >= n) break;
-                while (p >= sg.end && sk + 1 < nseg) sg = segs[++sk];
-                if (!fast && p >= hi && (p == sg.start || (sg.special < 0 && p + 1 < sg.end &&
-                                                           is_safe_point(s, (size_t)sg.end, p))))
-                    break;
-                size_t e;
-                uint32_t rec;
-                if (sg.special >= 0) {
-                    rec = kSpecialRec | (uint32_t)sg.special;
-                    e = sg.end;
-                } else if (fast) {
-                    const uint32_t r = (uint32_t)(p - base);
-                    const uint32_t se = (uint32_t)((sg.end < wend ? sg.end : wend) - base);
-                    e = base + token_end(L, se, r);
-                    rec = word_rec(L, r, e - p, p);
-                } else {
-                    e = token_end(s, (size_t)sg.end, p);
-                    rec = word_rec(s, p, e - p, p);
-                }
-                // a span of B bytes holds at most B records; anything else is a bug: report it
-                // (status 16) rather than write past the span
-                if (e <= p || g0 + k >= (fast ? g1 : n)) { atomicOr(status, 16u); break; }
-                recs[g0 + k] = rec;
-                ++k;
-                p = e;
-            }
-        }
-        t_start[gt] = g0 == ~0ULL ? 0 : g0;
-        t_count[gt] = k;
-        // cache eviction every kEncEpoch chunks (see k_count_words)
-        if ((c - blockIdx.x) / gridDim.x % kEncEpoch == kEncEpoch - 1) {
-            __syncthreads();
-            for (int i = tid; i < kEncCache; i += blockDim.x) {
-                const unsigned long long kk = c_key[i];
-                if (kk == 0 || kk == kBusy) continue;
-                const uint16_t hh = c_hit[i];
-                if ((uint16_t)(hh - c_mark[i]) >= kEncKeep) { c_mark[i] = hh; continue; }
-                c_key[i] = 0;
-                c_hit[i] = 0;
-                c_mark[i] = 0;
-            }
-        }
-        const unsigned long long ins = wave_sum(inserted);
-        inserted = 0;
-        if ((tid & 63) == 0) s_red[tid >> 6] = ins;
-        __syncthreads();
-        if (tid == 0) {
-            const unsigned long long b = s_red[0] + s_red[1] + s_red[2] + s_red[3];
-            if (b) atomicAdd(fill, b);
-        }
-    }
-}
-
-// ------------------------------------------------------------------ 2'. the byte-parallel scan
-// The same pass with tokstart.h's predicate: every thread turns its 64-byte block into a
-// token-start mask, evaluated once per segment that overlaps the block on a window clipped to
-// that segment (bytes before the segment start read '\n', the segment end is the text end: each
-// segment is pre-tokenized on its own, tokenizer.py:68-90); a special segment is one token.  The
-// thread then records the pre-tokens that start in its block at recs[block + k] (a 64-byte block
-// holds at most 64), its span is (block, k).  The segments of a chunk's window sit in LDS.
-constexpr int kSegLds = 64;
 
 struct ClipWin {   // one block's window with the bytes before window position lo read as '\n'
     int r0, lo;
@@ -398,109 +240,133 @@ struct ClipWin {   // one block's window with the bytes before window position l
     }
 };
 
-// workgroups per CU the scan's registers are capped for (build knob): 4 caps them at 128 VGPRs
-// and spills ~160 B per lane; 3 leaves room for every live value
+struct ScanArgs {
+    const uint8_t* s;
+    size_t n, n_chunks;
+    const Seg* segs;
+    int nseg, use_cache;
+    unsigned long long* kv;           // the word table (stage.h)
+    unsigned long long* pos;
+    size_t mask;
+    unsigned long long max_fill;
+    unsigned long long* fill;
+    uint32_t* recs;                   // records, each chunk's run contiguous
+    unsigned long long rec_cap;
+    unsigned long long* rec_fill;
+    unsigned long long* rec_base;     // per chunk: its run in recs
+    uint32_t* rec_n;
+    unsigned* status;
+};
+
+// Persistent workgroups stream 16 KiB chunks through LDS (stage2.h).  Every thread turns its
+// 64-byte block into a token-start mask with tokstart.h's predicate, evaluated once per segment
+// that overlaps the block on a window clipped to that segment (bytes before the segment start
+// read '\n', the segment end is the text end: each segment is pre-tokenized on its own,
+// tokenizer.py:68-90); a special segment is one token.  A block's pre-tokens are the set bits of
+// its mask, so the chunk's record count and every thread's offset in the chunk's run are one
+// block scan of popcounts, and the records of a chunk are written densely.
+// workgroups per CU the scan's registers are capped for (build knob)
 #ifndef BPE355_ENC_SCAN_WG
 #define BPE355_ENC_SCAN_WG 4
 #endif
 template <bool kAligned>
-__global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG)
-k_enc_scan2(const uint8_t* __restrict__ s, size_t n, size_t n_chunks, const Seg* __restrict__ segs,
-            int nseg, unsigned long long* __restrict__ kv, unsigned long long* __restrict__ pos,
-            size_t mask, unsigned long long max_fill, unsigned long long* __restrict__ fill,
-            uint32_t* __restrict__ recs, unsigned long long* __restrict__ t_start,
-            uint32_t* __restrict__ t_count, unsigned* __restrict__ status, int use_cache) {
+__global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan3(ScanArgs A, EncDict D) {
     __shared__ uint64_t s_mask[kWords];
     __shared__ unsigned long long c_key[kEncCache];
     __shared__ uint64_t c_lo[kEncCache], c_hi[kEncCache];
-    __shared__ uint32_t c_slot[kEncCache];
-    __shared__ uint16_t c_hit[kEncCache];   // hits this epoch (4 workgroups per CU fit the LDS)
+    __shared__ uint32_t c_rec[kEncCache];
+    __shared__ uint16_t c_hit[kEncCache];   // hits this epoch
+    __shared__ uint32_t s_brec[256];
     __shared__ Seg s_seg[kSegLds];
     __shared__ int s_seg0, s_segn;   // first segment of the chunk window and how many are in LDS (-1: too many)
     __shared__ unsigned long long s_red[4];
+    __shared__ uint32_t s_wsum[4];
+    __shared__ unsigned long long s_rbase;
     __shared__ int s_stop;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint8_t* __restrict__ s = A.s;
+    const size_t n = A.n;
     for (int i = tid; i < kEncCache; i += blockDim.x) { c_key[i] = 0; c_hit[i] = 0; }
+    s_brec[tid] = D.byte_rec[tid];
     load_cls2(tid, blockDim.x);
     unsigned long long inserted = 0;
 
-    // one pre-token [p, p + len) of src (global position gp); returns its record
-    auto word_rec = [&](const auto& src, auto p, size_t len, size_t gp) -> uint32_t {
-        if (len >= (1ULL << 24)) { atomicOr(status, 2u); return 0u; }
+    // a word through the table: its slot as the record (0 when the table is full: the host
+    // retries with a larger one)
+    auto table_rec = [&](size_t len, size_t gp, uint64_t wl, uint64_t wh, uint64_t h) -> uint32_t {
         bool ins = false;
-        if (len <= (size_t)kInline) {
-            uint64_t wl = 0, wh = 0;
-            for (uint32_t i = 0; i < (uint32_t)len; ++i) {
-                const uint64_t b = src[p + i];
-                if (i < 8) wl |= b << (8 * i);
-                else wh |= b << (8 * (i - 8));
-            }
-            const uint64_t h = short_hash(wl, wh, len);
-            const unsigned ls = (unsigned)(h >> 40) & (kEncCache - 2);
-            for (int way = 0; way < 2 && use_cache; ++way) {
+        const size_t slot = table_add(s, s, gp, len, wl, wh, h, 0, A.kv, A.pos, A.mask, A.status, &ins);
+        inserted += ins;
+        return slot == ~(size_t)0 ? 0u : (uint32_t)slot;
+    };
+    // a pre-token of 2..16 bytes at stage position r (global gp): LDS cache, dictionary, table
+    auto short_rec = [&](uint32_t r, size_t len, size_t gp) -> uint32_t {
+        uint64_t wl, wh;
+        pack_stage(kPre + (int)r, (int)len, wl, wh);
+        const uint64_t h = short_hash(wl, wh, len);
+        const unsigned ls = (unsigned)(h >> 40) & (kEncCache - 2);
+        if (A.use_cache) {
+            for (int way = 0; way < 2; ++way) {
                 const unsigned sl = ls + way;
                 const unsigned long long k = c_key[sl];
                 if (k != 0 && k != kBusy && (k >> 40) == len) {
                     __asm__ volatile("" ::: "memory");
                     if (c_lo[sl] == wl && c_hi[sl] == wh) {
                         c_hit[sl] = (uint16_t)(c_hit[sl] + 1);   // a heuristic: races may drop hits
-                        return c_slot[sl];
+                        return c_rec[sl];
                     }
                 }
             }
-            const size_t slot = table_add(s, s, gp, len, wl, wh, h, 0, kv, pos, mask, status, &ins);
-            inserted += ins;
-            if (slot == ~(size_t)0) return 0u;
-            for (int way = 0; way < 2 && use_cache; ++way) {   // cache it if a way is free
+        }
+        uint32_t rec = dict_find(D, wl, wh, (uint32_t)len, h);
+        if (rec == kRecNone) rec = table_rec(len, gp, wl, wh, h);
+        if (A.use_cache) {
+            for (int way = 0; way < 2; ++way) {   // cache it if a way is free
                 const unsigned sl = ls + way;
                 if (c_key[sl] == 0 && atomicCAS(&c_key[sl], 0ULL, kBusy) == 0) {
                     c_lo[sl] = wl;
                     c_hi[sl] = wh;
-                    c_slot[sl] = (uint32_t)slot;
+                    c_rec[sl] = rec;
                     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                     atomicExch(&c_key[sl], ((unsigned long long)len << 40) | (gp + 1));
                     break;
                 }
             }
-            return (uint32_t)slot;
         }
-        const size_t slot = table_add(s, s, gp, len, 0, 0, hash_word(s, gp, len), 0, kv, pos, mask,
-                                      status, &ins);
-        inserted += ins;
-        return slot == ~(size_t)0 ? 0u : (uint32_t)slot;
+        return rec;
     };
 
     uint4 pre[kSVec];
-    if (blockIdx.x < n_chunks) fetch2<kAligned>(pre, s, n, (size_t)blockIdx.x * kChunk, tid);
-    for (size_t c = blockIdx.x; c < n_chunks; c += gridDim.x) {
+    if (blockIdx.x < A.n_chunks) fetch2<kAligned>(pre, s, n, (size_t)blockIdx.x * kChunk, tid);
+    for (size_t c = blockIdx.x; c < A.n_chunks; c += gridDim.x) {
         __syncthreads();
         store2(pre, tid);
         const size_t base = c * kChunk;
         if (tid < 64) {   // wave 0: the segments that overlap the staged window, into LDS
             const size_t w0 = base >= (size_t)kPre ? base - kPre : 0, w1 = base + kWin + kPost;
-            const int k0 = seg_of(segs, nseg, w0);
+            const int k0 = seg_of(A.segs, A.nseg, w0);
             const int i = k0 + tid;
             Seg sg{};
-            if (i < nseg) sg = segs[i];
-            const bool in = i < nseg && sg.start < w1;
+            if (i < A.nseg) sg = A.segs[i];
+            const bool in = i < A.nseg && sg.start < w1;
             if (in) s_seg[tid] = sg;
             const unsigned long long b = __ballot(in);
             if (tid == 0) {
                 s_seg0 = k0;
-                s_segn = (b == ~0ULL && k0 + 64 < nseg && segs[k0 + 64].start < w1) ? -1 : __popcll(b);
-                s_stop = *(volatile unsigned long long*)fill > max_fill;
+                s_segn = (b == ~0ULL && k0 + 64 < A.nseg && A.segs[k0 + 64].start < w1) ? -1 : __popcll(b);
+                s_stop = *(volatile unsigned long long*)A.fill > A.max_fill;
             }
         }
         __syncthreads();
         if (s_stop) {
-            if (tid == 0) atomicOr(status, 1u);
+            if (tid == 0) atomicOr(A.status, 1u);
             break;
         }
         const int seg0 = s_seg0, segn = s_segn;
-        auto seg_at = [&](int i) -> Seg { return segn >= 0 ? s_seg[i - seg0] : segs[i]; };
-        const int seg_end = segn >= 0 ? seg0 + segn : nseg;
+        auto seg_at = [&](int i) -> Seg { return segn >= 0 ? s_seg[i - seg0] : A.segs[i]; };
+        const int seg_end = segn >= 0 ? seg0 + segn : A.nseg;
         auto seg_find = [&](size_t p) -> int {   // the segment holding position p
-            if (segn < 0) return seg_of(segs, nseg, p);
+            if (segn < 0) return seg_of(A.segs, A.nseg, p);
             int lo = seg0, hi = seg_end - 1;
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
@@ -538,50 +404,87 @@ k_enc_scan2(const uint8_t* __restrict__ s, size_t n, size_t n_chunks, const Seg*
             }
         }
         s_mask[tid] = starts;
-        if (c + gridDim.x < n_chunks) fetch2<kAligned>(pre, s, n, (c + gridDim.x) * kChunk, tid);
+        // the thread's offset in the chunk's run: a block scan of the per-block record counts
+        const uint32_t cnt = (uint32_t)__popcll(starts);
+        uint32_t x = cnt;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_wsum[wave] = x;
+        if (c + gridDim.x < A.n_chunks) fetch2<kAligned>(pre, s, n, (c + gridDim.x) * kChunk, tid);
         __syncthreads();
+        uint32_t toff = x - cnt;
+        for (int w = 0; w < wave; ++w) toff += s_wsum[w];
+        if (tid == 0) {
+            const uint32_t total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+            unsigned long long b = atomicAdd(A.rec_fill, (unsigned long long)total);
+            if (b + total > A.rec_cap) {   // the record buffer is too small: the host retries
+                atomicOr(A.status, 256u);
+                b = ~0ULL;
+            }
+            s_rbase = b;
+            A.rec_base[c] = b == ~0ULL ? 0 : b;
+            A.rec_n[c] = b == ~0ULL ? 0 : total;
+        }
+        __syncthreads();
+        const unsigned long long rbase = s_rbase;
 
         // ---- one record per pre-token that starts in the block
-        const size_t rem = n > base ? n - base : 0;
-        const uint32_t tend = rem < (size_t)kWin ? (uint32_t)rem : (uint32_t)kWin;
-        const size_t gt = c * 256 + tid;
-        uint32_t k = 0;
-        uint64_t m = starts;
-        while (m) {
-            const uint32_t j = (uint32_t)__builtin_ctzll(m);
-            m &= m - 1;
-            const uint32_t r = 64u * tid + j;
-            const size_t gp = base + r;
-            size_t e;   // end (global)
-            if (m) {
-                e = base + 64u * tid + (uint32_t)__builtin_ctzll(m);
-            } else {
-                e = ~(size_t)0;
-                for (int w = tid + 1; w < kWords; ++w) {
-                    const uint64_t x = s_mask[w];
-                    if (x) { e = base + 64u * w + (uint32_t)__builtin_ctzll(x); break; }
-                }
-                if (e == ~(size_t)0) {   // the chunk's last pre-token: its segment decides
-                    const Seg sg = seg_at(seg_find(gp));
-                    if ((spec >> j) & 1ULL) {
-                        e = sg.end;
+        if (rbase != ~0ULL) {
+            uint32_t* const out = A.recs + rbase + toff;
+            const size_t rem = n > base ? n - base : 0;
+            const uint32_t tend = rem < (size_t)kWin ? (uint32_t)rem : (uint32_t)kWin;
+            uint32_t k = 0;
+            uint64_t m = starts;
+            while (m) {
+                const uint32_t j = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1;
+                const uint32_t r = 64u * tid + j;
+                const size_t gp = base + r;
+                uint32_t rec;
+                if ((spec >> j) & 1ULL) {
+                    rec = kRecSpecial | (uint32_t)seg_at(seg_find(gp)).special;
+                } else {
+                    size_t e;   // end (global)
+                    if (m) {
+                        e = base + 64u * tid + (uint32_t)__builtin_ctzll(m);
                     } else {
-                        const size_t lim = sg.end < base + tend ? sg.end : base + tend;
-                        e = base + token_end(StageText{}, (uint32_t)(lim - base), r);
-                        if (lim != sg.end && e + 4 > lim) e = token_end(s, (size_t)sg.end, gp);
+                        e = ~(size_t)0;
+                        for (int w = tid + 1; w < kWords; ++w) {
+                            const uint64_t xw = s_mask[w];
+                            if (xw) { e = base + 64u * w + (uint32_t)__builtin_ctzll(xw); break; }
+                        }
+                        if (e == ~(size_t)0) {   // the chunk's last pre-token: its segment decides
+                            const Seg sg = seg_at(seg_find(gp));
+                            const size_t lim = sg.end < base + tend ? sg.end : base + tend;
+                            e = base + token_end(StageText{}, (uint32_t)(lim - base), r);
+                            if (lim != sg.end && e + 4 > lim) e = token_end(s, (size_t)sg.end, gp);
+                        }
+                    }
+                    if (e <= gp) { atomicOr(A.status, 16u); rec = 0; }
+                    else {
+                        const size_t len = e - gp;
+                        if (len == 1) {
+                            rec = s_brec[StageText{}[r]];
+                            if (rec == kRecNone) {
+                                uint64_t wl, wh;
+                                pack_stage(kPre + (int)r, 1, wl, wh);
+                                rec = table_rec(1, gp, wl, wh, short_hash(wl, wh, 1));
+                            }
+                        } else if (len <= (size_t)kInline) {
+                            rec = short_rec(r, len, gp);
+                        } else if (len >= (1ULL << 24)) {
+                            atomicOr(A.status, 2u);
+                            rec = 0;
+                        } else {
+                            rec = table_rec(len, gp, 0, 0, hash_word(s, gp, len));
+                        }
                     }
                 }
+                out[k++] = rec;
             }
-            uint32_t rec;
-            if ((spec >> j) & 1ULL) rec = kSpecialRec | (uint32_t)seg_at(seg_find(gp)).special;
-            else if (e - gp <= (size_t)kInline) rec = word_rec(StageText{}, r, e - gp, gp);
-            else rec = word_rec(s, gp, e - gp, gp);
-            if (e <= gp || k >= 64) { atomicOr(status, 16u); break; }
-            recs[blk + k] = rec;
-            ++k;
         }
-        t_start[gt] = k ? blk : 0;
-        t_count[gt] = k;
         if ((c - blockIdx.x) / gridDim.x % kEncEpoch == kEncEpoch - 1) {   // cache eviction
             __syncthreads();
             for (int i = tid; i < kEncCache; i += blockDim.x) {
@@ -594,11 +497,11 @@ k_enc_scan2(const uint8_t* __restrict__ s, size_t n, size_t n_chunks, const Seg*
         }
         const unsigned long long ins = wave_sum(inserted);
         inserted = 0;
-        if ((tid & 63) == 0) s_red[tid >> 6] = ins;
+        if (lane == 0) s_red[wave] = ins;
         __syncthreads();
         if (tid == 0) {
             const unsigned long long b = s_red[0] + s_red[1] + s_red[2] + s_red[3];
-            if (b) atomicAdd(fill, b);
+            if (b) atomicAdd(A.fill, b);
         }
     }
 }
@@ -617,127 +520,234 @@ __global__ void k_collect(const unsigned long long* __restrict__ kv, const unsig
     w_len[w] = inl ? (uint32_t)((k >> 56) & 0x7f) : (uint32_t)(k >> 40);
 }
 
-// ------------------------------------------------------------------ 5. ids per span, then write
-// slot_info[slot] (k_encode_words): the word's ids in one 8-byte cell -- kOneId | id for a word
-// of one id, nids << 39 | offset into the id pool for more, 0 for none (a pre-token equal to a
-// special) -- so a pre-token costs one dependent load from its record
+// ------------------------------------------------------------------ 5. ids, in one pass
+// slot_info[slot] (k_encode_words) and a dictionary entry's info: a word's ids in one 8-byte
+// cell -- kOneId | id for a word of one id, nids << 39 | offset into an id pool for more (the
+// dictionary's pool when kDictPool is set), 0 for none (a pre-token equal to a special)
 constexpr unsigned long long kOneId = 1ULL << 63;
+constexpr unsigned long long kDictPool = 1ULL << 38;
+constexpr unsigned long long kPoolOff = kDictPool - 1;
 
 __device__ __forceinline__ uint32_t info_nids(unsigned long long info) {
     return (info & kOneId) ? 1u : (uint32_t)((info >> 39) & 0xffffffu);
 }
 
-__global__ void k_enc_count(const uint32_t* __restrict__ recs, const unsigned long long* __restrict__ t_start,
-                            const uint32_t* __restrict__ t_count, size_t n_spans,
-                            const unsigned long long* __restrict__ slot_info, size_t cap,
-                            unsigned* __restrict__ status, unsigned long long* __restrict__ per) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_spans) return;
-    const uint32_t* r = recs + t_start[t];
-    const uint32_t m = t_count[t];
-    unsigned long long ids = 0;
-    for (uint32_t i = 0; i < m; ++i) {
-        const uint32_t rec = r[i];
-        if (rec & kSpecialRec) { ++ids; continue; }
-        if (rec >= cap) { atomicOr(status, 32u); continue; }   // a record naming no slot: a bug
-        ids += info_nids(slot_info[rec]);
-    }
-    per[t] = ids;
+struct EmitArgs {
+    const uint32_t* recs;
+    const unsigned long long* rec_base;
+    const uint32_t* rec_n;
+    size_t n_chunks;
+    const unsigned long long* slot_info;   // word-table slot -> ids
+    const uint32_t* pool;
+    size_t cap;                            // word-table slots
+    EncDict D;
+    const int64_t* sp_vid;
+    unsigned* ticket;                      // chunks in the order workgroups take them
+    unsigned long long* flags;             // per chunk: look-back state | id count
+    unsigned* status;
+};
+
+// a record's ids in slot_info format (one load at most: a one-id word carries its id)
+__device__ __forceinline__ unsigned long long rec_info(const EmitArgs& A, uint32_t rec) {
+    const uint32_t kind = rec & kRecKind, pl = rec & kRecPayload;
+    if (kind == kRecDirect) return kOneId | pl;
+    if (kind == kRecSpecial) return kOneId | (uint32_t)A.sp_vid[pl];
+    if (kind == kRecDict) return A.D.ent[pl].info;
+    if (rec >= A.cap) { atomicOr(A.status, 32u); return 0; }   // a record naming no slot: a bug
+    return A.slot_info[rec];
 }
 
-// One workgroup per chunk: its 256 spans' ids form one contiguous output range, so they are
-// assembled in LDS and stored with coalesced 16-byte writes (a lane writing its own span straight
-// to memory leaves partial lines behind).  A chunk whose ids do not fit writes directly.
-constexpr unsigned kWriteLds = 12288;   // ids staged per chunk (48 KB; a chunk averages ~5 K)
-
-// a span's ids, in order, through put(position, id)
+// the ids of one info through put(position, id), from position o; returns how many
 template <class Put>
-__device__ __forceinline__ void emit_span(const uint32_t* __restrict__ r, uint32_t m,
-                                          const unsigned long long* __restrict__ slot_info,
-                                          const uint32_t* __restrict__ ids_pool, const int64_t* __restrict__ sp_vid,
-                                          size_t cap, unsigned long long o, const Put& put) {
-    for (uint32_t i = 0; i < m; ++i) {
-        const uint32_t rec = r[i];
-        if (rec & kSpecialRec) {
-            put(o++, (uint32_t)sp_vid[rec & ~kSpecialRec]);
-            continue;
-        }
-        if (rec >= cap) continue;   // reported by k_enc_count
-        const unsigned long long info = slot_info[rec];
-        if (info & kOneId) {
-            put(o++, (uint32_t)info);
-            continue;
-        }
-        const uint32_t nm = info_nids(info);
-        const uint32_t* src = ids_pool + (info & ((1ULL << 39) - 1));
-        for (uint32_t j = 0; j < nm; ++j) put(o + j, src[j]);
-        o += nm;
+__device__ __forceinline__ uint32_t put_ids(const EmitArgs& A, unsigned long long info, uint32_t o, const Put& put) {
+    if (info & kOneId) {
+        put(o, (uint32_t)info);
+        return 1;
     }
+    const uint32_t nm = info_nids(info);
+    const uint32_t* src = ((info & kDictPool) ? A.D.pool : A.pool) + (info & kPoolOff);
+    for (uint32_t j = 0; j < nm; ++j) put(o + j, src[j]);
+    return nm;
 }
 
-// OutT uint32_t: the ids; uint16_t: np.uint16 as encode.py saves them (encode.py:37), an id past
-// 65535 reported in status (bit 128) instead of wrapped
-template <class OutT>
-__global__ void __launch_bounds__(256) k_enc_write(const uint32_t* __restrict__ recs,
-                                                   const unsigned long long* __restrict__ t_start,
-                                                   const uint32_t* __restrict__ t_count, size_t n_spans,
-                                                   const unsigned long long* __restrict__ slot_info,
-                                                   const uint32_t* __restrict__ ids_pool,
-                                                   const int64_t* __restrict__ sp_vid,
-                                                   const unsigned long long* __restrict__ per,
-                                                   const unsigned long long* __restrict__ per_off, size_t cap,
-                                                   OutT* __restrict__ out, unsigned* __restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint32_t buf[kWriteLds];
-    __shared__ unsigned s_wide;
-    const size_t t0 = (size_t)blockIdx.x * 256, t = t0 + threadIdx.x;
-    const size_t tl = t0 + 255 < n_spans ? t0 + 255 : n_spans - 1;   // the chunk's last span
-    const unsigned long long o0 = per_off[t0], o1 = per_off[tl] + per[tl];
-    const unsigned long long total = o1 - o0;
-    constexpr bool kNarrow = sizeof(OutT) == 2;
-    if (total > kWriteLds) {   // too many ids for LDS: straight to memory
-        bool wide = false;
-        if (t < n_spans)
-            emit_span(recs + t_start[t], t_count[t], slot_info, ids_pool, sp_vid, cap, per_off[t],
-                      [&](unsigned long long q, uint32_t v) { out[q] = (OutT)v; wide |= kNarrow && v > 0xffffu; });
-        if (wide) atomicOr(status, 128u);
-        return;
+// exclusive scan of v over the 256 threads: this thread's offset; *total = the sum
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_ws, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
     }
-    if (threadIdx.x == 0) s_wide = 0;
-    if (t < n_spans)
-        emit_span(recs + t_start[t], t_count[t], slot_info, ids_pool, sp_vid, cap, per_off[t] - o0,
-                  [&](unsigned long long q, uint32_t v) { buf[q] = v; });
+    if (lane == 63) s_ws[wave] = x;
     __syncthreads();
-    // out + o0 is OutT-aligned: a scalar head up to 16-byte alignment, then 16-byte stores
-    constexpr unsigned kPer = 16 / sizeof(OutT);   // ids per 16-byte store
-    const unsigned head = (unsigned)(((16 - ((uintptr_t)(out + o0) & 15)) & 15) / sizeof(OutT));
-    const unsigned h = head < total ? head : (unsigned)total;
-    bool wide = false;
-    if (threadIdx.x < h) { out[o0 + threadIdx.x] = (OutT)buf[threadIdx.x]; wide |= buf[threadIdx.x] > 0xffffu; }
-    const unsigned body = (unsigned)(total - h) / kPer;
-    uint4* dst = reinterpret_cast<uint4*>(out + o0 + h);
-    for (unsigned i = threadIdx.x; i < body; i += 256) {
-        const unsigned q = h + kPer * i;
-        if (kNarrow) {
-            uint32_t w[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t lo = buf[q + 2 * k], hi = buf[q + 2 * k + 1];
-                wide |= (lo | hi) > 0xffffu;
-                w[k] = (lo & 0xffffu) | (hi << 16);
-            }
-            dst[i] = make_uint4(w[0], w[1], w[2], w[3]);
-        } else {
-            dst[i] = make_uint4(buf[q], buf[q + 1], buf[q + 2], buf[q + 3]);
+    uint32_t off = x - v;
+    for (int w = 0; w < wave; ++w) off += s_ws[w];
+    *total = s_ws[0] + s_ws[1] + s_ws[2] + s_ws[3];
+    __syncthreads();
+    return off;
+}
+
+// Decoupled look-back (single-pass prefix over chunks): chunk c publishes its id count as an
+// aggregate, then walks back over its predecessors 64 at a time, summing aggregates until one
+// that holds an inclusive prefix, and publishes its own inclusive prefix.  State and value share
+// one 64-bit word, read and written with agent-scope atomics (coherent across the XCDs' L2s).
+// Workgroups take chunks by ticket, so every predecessor is running or done: it publishes its
+// aggregate without waiting for anyone.  Called by all 64 lanes of one wave; returns the ids of
+// the chunks before c.
+constexpr unsigned long long kLbAgg = 1ULL << 62, kLbIncl = 2ULL << 62, kLbVal = (1ULL << 62) - 1;
+
+__device__ __forceinline__ unsigned long long lb_load(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ unsigned long long lookback(unsigned long long* flags, unsigned c, unsigned long long T) {
+    const int lane = threadIdx.x & 63;
+    if (c == 0) {
+        if (lane == 0) lb_store(flags, kLbIncl | T);
+        return 0;
+    }
+    if (lane == 0) lb_store(flags + c, kLbAgg | T);
+    unsigned long long acc = 0;
+    long long j = (long long)c - 1;   // the window [j - 63, j], nearest predecessor in lane 0
+    for (;;) {
+        const long long q = j - lane;
+        unsigned long long v = q >= 0 ? lb_load(flags + q) : kLbIncl;
+        while (__any((v >> 62) == 0)) {   // every chunk of the window has published something
+            __builtin_amdgcn_s_sleep(2);
+            if ((v >> 62) == 0) v = lb_load(flags + q);
         }
+        const unsigned long long incl = __ballot((v >> 62) == 2);
+        if (incl) {
+            const int f = __ffsll((long long)incl) - 1;   // the nearest inclusive prefix
+            acc += wave_sum(lane <= f ? (v & kLbVal) : 0ULL);
+            break;
+        }
+        acc += wave_sum(v & kLbVal);
+        j -= 64;
     }
-    for (unsigned q = h + kPer * body + threadIdx.x; q < total; q += 256) {
-        out[o0 + q] = (OutT)buf[q];
-        wide |= buf[q] > 0xffffu;
-    }
-    if (kNarrow && wide) s_wide = 1;
-    if (kNarrow) {
+    if (lane == 0) lb_store(flags + c, kLbIncl | (acc + T));
+    return acc;
+}
+
+// One chunk per workgroup at a time: its records' ids counted (gathers issued together, kept in
+// registers), its output offset by look-back, its ids assembled in LDS and stored with coalesced
+// 16-byte writes (a chunk averages ~5 K ids).  OutT uint32_t: the ids; uint16_t: np.uint16 as
+// encode.py saves them (encode.py:37), an id past 65535 reported in status (bit 128) instead of
+// wrapped.
+constexpr unsigned kEmitIds = 12288;   // ids staged per chunk (48 KB)
+constexpr int kEmitR = 16;             // records per thread held in registers: chunks of <= 4096
+
+template <class OutT>
+__global__ void __launch_bounds__(256) k_enc_emit(EmitArgs A, OutT* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t buf[kEmitIds];
+    __shared__ uint32_t s_ws[4];
+    __shared__ unsigned s_c, s_wide;
+    __shared__ unsigned long long s_pre;
+    const int tid = threadIdx.x;
+    constexpr bool kNarrow = sizeof(OutT) == 2;
+    bool wide = false;
+    if (tid == 0) s_wide = 0;
+    auto prefix = [&](unsigned c, uint32_t T) -> unsigned long long {
+        if (tid < 64) {
+            const unsigned long long p = lookback(A.flags, c, T);
+            if (tid == 0) s_pre = p;
+        }
         __syncthreads();
-        if (threadIdx.x == 0 && s_wide) atomicOr(status, 128u);
+        return s_pre;
+    };
+    for (;;) {
+        if (tid == 0) s_c = atomicAdd(A.ticket, 1u);
+        __syncthreads();
+        const unsigned c = s_c;
+        if (c >= A.n_chunks) break;
+        const uint32_t m = A.rec_n[c];
+        const uint32_t* __restrict__ r = A.recs + A.rec_base[c];
+        if (m <= 256u * kEmitR) {
+            const uint32_t R = (m + 255) >> 8;
+            const uint32_t lo = tid * R, hi = lo + R < m ? lo + R : m;
+            unsigned long long info[kEmitR];
+#pragma unroll
+            for (int i = 0; i < kEmitR; ++i) info[i] = lo + i < hi ? rec_info(A, r[lo + i]) : 0ULL;
+            uint32_t sum = 0;
+#pragma unroll
+            for (int i = 0; i < kEmitR; ++i) sum += lo + i < hi ? info_nids(info[i]) : 0u;
+            uint32_t T;
+            const uint32_t toff = block_excl_scan(sum, s_ws, &T);
+            const unsigned long long P = prefix(c, T);
+            if (T <= kEmitIds) {
+                uint32_t o = toff;
+#pragma unroll
+                for (int i = 0; i < kEmitR; ++i)
+                    if (lo + i < hi) o += put_ids(A, info[i], o, [&](uint32_t q, uint32_t v) { buf[q] = v; });
+                __syncthreads();
+                // out + P is OutT-aligned: a scalar head up to 16-byte alignment, then 16-byte stores
+                constexpr unsigned kPer = 16 / sizeof(OutT);
+                const unsigned head = (unsigned)(((16 - ((uintptr_t)(out + P) & 15)) & 15) / sizeof(OutT));
+                const unsigned h = head < T ? head : T;
+                if ((unsigned)tid < h) {
+                    out[P + tid] = (OutT)buf[tid];
+                    wide |= buf[tid] > 0xffffu;
+                }
+                const unsigned body = (T - h) / kPer;
+                uint4* dst = reinterpret_cast<uint4*>(out + P + h);
+                for (unsigned i = tid; i < body; i += 256) {
+                    const unsigned q = h + kPer * i;
+                    if (kNarrow) {
+                        uint32_t w[4];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const uint32_t a = buf[q + 2 * k], b = buf[q + 2 * k + 1];
+                            wide |= (a | b) > 0xffffu;
+                            w[k] = (a & 0xffffu) | (b << 16);
+                        }
+                        dst[i] = make_uint4(w[0], w[1], w[2], w[3]);
+                    } else {
+                        dst[i] = make_uint4(buf[q], buf[q + 1], buf[q + 2], buf[q + 3]);
+                    }
+                }
+                for (unsigned q = h + kPer * body + tid; q < T; q += 256) {
+                    out[P + q] = (OutT)buf[q];
+                    wide |= buf[q] > 0xffffu;
+                }
+            } else {   // too many ids for LDS: straight to memory
+                uint32_t o = toff;
+#pragma unroll
+                for (int i = 0; i < kEmitR; ++i)
+                    if (lo + i < hi)
+                        o += put_ids(A, info[i], o, [&](uint32_t q, uint32_t v) {
+                            out[P + q] = (OutT)v;
+                            wide |= kNarrow && v > 0xffffu;
+                        });
+            }
+        } else {   // many records: rounds of 256, counted first, then re-read and written
+            uint32_t sum = 0;
+            for (uint32_t b = 0; b < m; b += 256)
+                if (b + tid < m) sum += info_nids(rec_info(A, r[b + tid]));
+            uint32_t T;
+            (void)block_excl_scan(sum, s_ws, &T);
+            const unsigned long long P = prefix(c, T);
+            uint32_t run = 0;
+            for (uint32_t b = 0; b < m; b += 256) {
+                const unsigned long long inf = b + tid < m ? rec_info(A, r[b + tid]) : 0ULL;
+                uint32_t rt;
+                const uint32_t off = block_excl_scan(b + tid < m ? info_nids(inf) : 0u, s_ws, &rt);
+                if (b + tid < m)
+                    put_ids(A, inf, run + off, [&](uint32_t q, uint32_t v) {
+                        out[P + q] = (OutT)v;
+                        wide |= kNarrow && v > 0xffffu;
+                    });
+                run += rt;
+            }
+        }
+        __syncthreads();   // buf and s_c are reused by the next chunk
+    }
+    if (kNarrow) {
+        if (wide) s_wide = 1;
+        __syncthreads();
+        if (tid == 0 && s_wide) atomicOr(A.status, 128u);
     }
 }
 
@@ -813,16 +823,21 @@ struct bpe_tokenizer {
     bpe::DevBuf<uint32_t> sp_off, sp_len;
     bpe::DevBuf<int64_t> sp_vid;
     bpe::DevBuf<unsigned> first_mask;
-    // the per-pre-token record buffer (4 B per input byte), kept for the next call: freeing and
-    // re-allocating tens of GB per call costs up to seconds in the driver (measured 0.5 -> 2.8 s
-    // for an 11.9 GB encode).  Calls on one handle are serialized on its stream.
+    // the encoder's dictionary (build_dictionary): every vocab entry of 2..16 bytes with its ids,
+    // the one-byte words' records
+    bpe::DevBuf<bpe::DictEnt> dict_ent;
+    bpe::DevBuf<uint32_t> dict_pool, byte_rec;
+    size_t dict_slots = 0, dict_words = 0;
+    // the per-pre-token record buffer, kept for the next call: freeing and re-allocating tens of
+    // GB per call costs up to seconds in the driver (measured 0.5 -> 2.8 s for an 11.9 GB
+    // encode).  Calls on one handle are serialized on its stream.
     bpe::DevBuf<uint32_t> recs_cache;
-    // the other per-call device arrays, kept the same way (grow-only): per 64-byte span, per
-    // word-table slot, per unique word, the id pool, the u16 output of the bulk encoder
+    // the other per-call device arrays, kept the same way (grow-only): per chunk, per word-table
+    // slot, per unique word, the id pool, the u16 output of the bulk encoder
     struct Scratch {
-        bpe::DevBuf<uint32_t> t_count, w_slot, w_len, pool;
-        bpe::DevBuf<unsigned long long> t_start, fill, kv, pos, w_off, len64, idoff, slot_info, per, per_off;
-        bpe::DevBuf<unsigned> status, d_nw;
+        bpe::DevBuf<uint32_t> rec_n, w_slot, w_len, pool;
+        bpe::DevBuf<unsigned long long> rec_base, rec_fill, flags, fill, kv, pos, w_off, len64, idoff, slot_info;
+        bpe::DevBuf<unsigned> status, d_nw, ticket;
         bpe::DevBuf<bpe::Seg> segs;
         bpe::DevBuf<unsigned long long> sp_key, sp_sorted;   // special matches, (position << 16 | index)
         bpe::DevBuf<unsigned long long> sp_cnt, sp_off, cuts;   // the device segment builder's arrays
@@ -846,6 +861,9 @@ struct bpe_tokenizer {
                               byte2tok.p, sp_bytes.p, sp_off.p, sp_len.p, sp_vid.p,
                               (int)specials.size()};
     }
+    bpe::EncDict dict() const {
+        return bpe::EncDict{dict_ent.p, (unsigned long long)(dict_slots - 1), dict_pool.p, byte_rec.p};
+    }
 };
 
 namespace bpe {
@@ -857,6 +875,107 @@ uint32_t rd_u32(const uint8_t*& p, const uint8_t* end) {
     std::memcpy(&v, p, 4);
     p += 4;
     return v;
+}
+
+// The encoder's dictionary: every vocab entry of 2..16 bytes, encoded once on the device by
+// k_encode_words exactly as a pre-token of those bytes is (tokenizer.py:124-136), in an open-
+// addressing table keyed by the packed bytes; plus the record of every one-byte word.  Entries
+// whose encoding has an id outside the direct range (or a missing vocab id: the KeyError path)
+// are left out, so those words take the word table as before.
+void build_dictionary(bpe_tokenizer& T, const std::unordered_map<std::string, uint32_t>& intern,
+                      const std::vector<int64_t>& vid, const std::vector<uint32_t>& b2t) {
+    std::vector<const std::string*> cand;
+    for (const auto& kv : intern)
+        if (kv.first.size() >= 2 && kv.first.size() <= (size_t)kInline && vid[kv.second] >= 0)
+            cand.push_back(&kv.first);
+    std::sort(cand.begin(), cand.end(), [](const std::string* a, const std::string* b) { return *a < *b; });
+    const size_t nc = cand.size();
+    std::vector<unsigned long long> info(nc);
+    std::vector<uint32_t> pool;
+    if (nc) {
+        std::string text;
+        std::vector<unsigned long long> off(nc), idoff(nc);
+        std::vector<uint32_t> len(nc), slot(nc);
+        for (size_t i = 0; i < nc; ++i) {
+            off[i] = text.size();
+            idoff[i] = text.size();   // ids <= bytes: the pool mirrors the text
+            len[i] = (uint32_t)cand[i]->size();
+            slot[i] = (uint32_t)i;
+            text += *cand[i];
+        }
+        DevBuf<uint8_t> d_text(text.size());
+        DevBuf<unsigned long long> d_off(nc), d_idoff(nc), d_info(nc);
+        DevBuf<uint32_t> d_len(nc), d_slot(nc), d_pool(text.size());
+        DevBuf<unsigned> d_status(1);
+        to_device(d_text.p, text.data(), text.size(), T.stream);
+        to_device(d_off.p, off.data(), nc * 8, T.stream);
+        to_device(d_idoff.p, idoff.data(), nc * 8, T.stream);
+        to_device(d_len.p, len.data(), nc * 4, T.stream);
+        to_device(d_slot.p, slot.data(), nc * 4, T.stream);
+        BPE_HIP(hipMemsetAsync(d_status.p, 0, 4, T.stream));
+        hipLaunchKernelGGL(k_encode_words, dim3(ceil_div(nc, 256)), dim3(256), 0, T.stream, d_text.p, T.tables(),
+                           d_off.p, d_len.p, d_idoff.p, d_slot.p, (unsigned)nc, d_pool.p, d_info.p, d_status.p,
+                           text.size());
+        BPE_HIP(hipGetLastError());
+        pool.resize(text.size());
+        to_host(info.data(), d_info.p, nc * 8, T.stream);
+        to_host(pool.data(), d_pool.p, text.size() * 4, T.stream);
+    }
+    T.dict_slots = next_pow2(std::max<size_t>(64, 2 * nc));
+    std::vector<DictEnt> ent(T.dict_slots);
+    std::memset(ent.data(), 0, ent.size() * sizeof(DictEnt));
+    std::vector<uint32_t> dpool;
+    size_t words = 0;
+    for (size_t i = 0; i < nc; ++i) {
+        const unsigned long long inf = info[i];
+        std::vector<uint32_t> ids;
+        if (inf & kOneId) ids.push_back((uint32_t)inf);
+        else if (inf) {
+            const uint32_t nm = (uint32_t)((inf >> 39) & 0xffffffu);
+            const size_t o = (size_t)(inf & ((1ULL << 39) - 1));
+            ids.assign(pool.begin() + o, pool.begin() + o + nm);
+        }
+        bool ok = true;
+        for (uint32_t x : ids) ok = ok && x < kRecPayload;
+        if (!ok) continue;
+        const std::string& w = *cand[i];
+        uint64_t lo = 0, hi = 0;
+        for (size_t j = 0; j < w.size(); ++j) {
+            const uint64_t b = (uint8_t)w[j];
+            if (j < 8) lo |= b << (8 * j);
+            else hi |= b << (8 * (j - 8));
+        }
+        size_t sl = short_hash(lo, hi, w.size()) & (T.dict_slots - 1);
+        while (ent[sl].len) sl = (sl + 1) & (T.dict_slots - 1);
+        DictEnt& e = ent[sl];
+        e.lo = lo;
+        e.hi = hi;
+        e.len = (uint32_t)w.size();
+        if (ids.size() == 1) {
+            e.rec = kRecDirect | ids[0];
+            e.info = kOneId | ids[0];
+        } else {
+            e.rec = kRecDict | (uint32_t)sl;
+            e.info = ids.empty() ? 0ULL : (((unsigned long long)ids.size() << 39) | kDictPool | dpool.size());
+            dpool.insert(dpool.end(), ids.begin(), ids.end());
+        }
+        ++words;
+    }
+    T.dict_words = words;
+    std::vector<uint32_t> brec(256, kRecNone);
+    for (int b = 0; b < 256; ++b) {
+        const int64_t v = vid[b2t[b]];
+        bool special = false;
+        for (const auto& sp : T.specials) special = special || (sp.size() == 1 && (uint8_t)sp[0] == b);
+        if (v >= 0 && v < (int64_t)kRecPayload && !special) brec[b] = kRecDirect | (uint32_t)v;
+    }
+    T.dict_ent.alloc(ent.size());
+    to_device(T.dict_ent.p, ent.data(), ent.size() * sizeof(DictEnt), T.stream);
+    T.dict_pool.alloc(std::max<size_t>(dpool.size(), 1));
+    if (!dpool.empty()) to_device(T.dict_pool.p, dpool.data(), dpool.size() * 4, T.stream);
+    T.byte_rec.alloc(256);
+    to_device(T.byte_rec.p, brec.data(), 256 * 4, T.stream);
+    BPE_HIP(hipStreamSynchronize(T.stream));
 }
 
 void build_tokenizer(bpe_tokenizer& T, const uint8_t* vb, size_t vn, const uint8_t* mb, size_t mn,
@@ -957,6 +1076,7 @@ void build_tokenizer(bpe_tokenizer& T, const uint8_t* vb, size_t vn, const uint8
     up(T.sp_vid, T.special_vid);
     up(T.first_mask, fm);
     BPE_HIP(hipStreamSynchronize(T.stream));
+    build_dictionary(T, intern, vid, b2t);
 }
 
 // encode d_text[0..n) into d_out; returns the id count.  `cuts` (sorted byte offsets) make the
@@ -1067,51 +1187,64 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
         to_device(d_segs.p, segs.data(), nseg * sizeof(Seg), s);
     }
 
-    // 2. one staged pass: unique pre-tokens into the word table, one record per pre-token
+    // 2. one staged pass: unique pre-tokens into the word table, one record per pre-token, each
+    // chunk's records one dense run
     const size_t n_chunks = (n + kChunk - 1) / kChunk;
-    const size_t n_spans = n_chunks * 256;
+    BPE_REQUIRE(n_chunks < (1ull << 32), BPE_E_LIMIT, "text too long for one encode");
     const bool aligned = (reinterpret_cast<uintptr_t>(d_text) & 15u) == 0;
-    static const bool v1 = std::getenv("BPE355_ENC_SCAN_V1") != nullptr;   // A/B knob: the serial scan
-    auto kern = v1 ? (aligned ? k_enc_scan<true> : k_enc_scan<false>)
-                   : (aligned ? k_enc_scan2<true> : k_enc_scan2<false>);
-    const int lds = v1 ? kPadded : kStage;
+    auto kern = aligned ? k_enc_scan3<true> : k_enc_scan3<false>;
     int per_cu = 0, dev = 0, n_cu = 0;
-    BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds));
+    BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, kStage));
     BPE_HIP(hipGetDevice(&dev));
     BPE_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
     unsigned sgrid = (unsigned)std::min<size_t>(n_chunks, (size_t)std::max(1, per_cu) * std::max(1, n_cu));
     if (const char* e = std::getenv("BPE355_STREAM_WG"))   // test knob (see count_words)
         sgrid = std::max(1u, std::min(sgrid, (unsigned)std::atoi(e)));
-    // first guess: small texts have many more unique words per byte than large corpora
+    // first guesses: small texts have many more unique words per byte than large corpora; natural
+    // text has ~0.15 pre-tokens per byte (at most one per byte: the retry's size)
     size_t cap = next_pow2(std::max<size_t>(1 << 16, n < (1u << 26) ? n / 16 : n / 1024));
+    unsigned long long rec_cap = n < (1u << 26) ? n + 64 : n / 4 + (1u << 20);
+    if (const char* e = std::getenv("BPE355_ENC_REC_CAP"))   // test knob: force the record retry
+        rec_cap = std::max<unsigned long long>(1, std::strtoull(e, nullptr, 10));
     DevBuf<unsigned long long>&kv = S.kv, &pos = S.pos;
-    if (T.recs_cache.n < std::max<size_t>(n, 1)) T.recs_cache.alloc(std::max<size_t>(n, 1));
-    uint32_t* const recs = T.recs_cache.p;
-    DevBuf<uint32_t>& t_count = S.t_count;
-    DevBuf<unsigned long long>&t_start = S.t_start, &fill = S.fill;
+    DevBuf<unsigned long long>&rec_base = S.rec_base, &rec_fill = S.rec_fill, &fill = S.fill;
+    DevBuf<uint32_t>& rec_n = S.rec_n;
     DevBuf<unsigned>& status = S.status;
-    t_count.reserve(n_spans);
-    t_start.reserve(n_spans);
+    rec_base.reserve(n_chunks);
+    rec_n.reserve(n_chunks);
+    rec_fill.reserve(1);
     fill.reserve(1);
     status.reserve(1);
+    const EncDict D = T.dict();
     for (int attempt = 0;; ++attempt) {
+        BPE_REQUIRE(cap <= (size_t)kRecPayload, BPE_E_LIMIT, "too many distinct words for one encode");
         kv.reserve(2 * cap);
         pos.reserve(cap);
+        T.recs_cache.reserve(rec_cap);
         BPE_HIP(hipMemsetAsync(kv.p, 0, 2 * cap * sizeof(unsigned long long), s));
         BPE_HIP(hipMemsetAsync(status.p, 0, 4, s));
         BPE_HIP(hipMemsetAsync(fill.p, 0, 8, s));
-        hipLaunchKernelGGL(kern, dim3(sgrid), dim3(256), lds, s, d_text, n, n_chunks, d_segs.p, nseg,
-                           kv.p, pos.p, cap - 1, (unsigned long long)(cap / 2), fill.p, recs,
-                           t_start.p, t_count.p, status.p,
-                           std::getenv("BPE355_NOCACHE") ? 0 : 1);   // test knob: global table only
+        BPE_HIP(hipMemsetAsync(rec_fill.p, 0, 8, s));
+        ScanArgs A{d_text, n, n_chunks, d_segs.p, nseg, std::getenv("BPE355_NOCACHE") ? 0 : 1, kv.p, pos.p,
+                   cap - 1, (unsigned long long)(cap / 2), fill.p, T.recs_cache.p, rec_cap, rec_fill.p,
+                   rec_base.p, rec_n.p, status.p};
+        hipLaunchKernelGGL(kern, dim3(sgrid), dim3(256), kStage, s, A, D);
         BPE_HIP(hipGetLastError());
         unsigned st = 0;
         to_host(&st, status.p, 4, s);
         if (st & 2u) throw Error{BPE_E_LIMIT, "a pre-token is longer than 16 MiB"};
-        BPE_REQUIRE(!(st & 16u), BPE_E_HIP, "internal error: encode scan overran a span");
-        if (!(st & 1u)) break;
-        BPE_REQUIRE(attempt < 6, BPE_E_NOMEM, "word table overflow");
-        cap *= 4;
+        BPE_REQUIRE(!(st & 16u), BPE_E_HIP, "internal error: encode scan found an empty pre-token");
+        BPE_REQUIRE(attempt < 8, BPE_E_NOMEM, "word table overflow");
+        if (st & 1u) {
+            cap *= 4;
+            continue;
+        }
+        if (st & 256u) {   // more pre-tokens than guessed: one per byte at most
+            BPE_REQUIRE(rec_cap < n + 64, BPE_E_HIP, "internal error: encode records overflow");
+            rec_cap = n + 64;
+            continue;
+        }
+        break;
     }
     DevBuf<uint32_t>&w_slot = S.w_slot, &w_len = S.w_len;
     DevBuf<unsigned long long>& w_off = S.w_off;
@@ -1126,7 +1259,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
     unsigned nw = 0;
     to_host(&nw, d_nw.p, 4, s);
 
-    // 3. encode each unique word once
+    // 3. encode each word of the table once
     DevBuf<unsigned long long>&len64 = S.len64, &idoff = S.idoff;
     len64.reserve(std::max(nw, 1u));
     idoff.reserve(std::max(nw, 1u) + 1);
@@ -1142,6 +1275,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
         to_host(&last[1], len64.p + nw - 1, 8, s);
         pool_n = last[0] + last[1];
     }
+    BPE_REQUIRE(pool_n < kDictPool, BPE_E_LIMIT, "too many distinct words for one encode");
     DevBuf<uint32_t>& pool = S.pool;
     pool.reserve(std::max<unsigned long long>(pool_n, 1));
     BPE_HIP(hipMemsetAsync(status.p, 0, 4, s));
@@ -1150,31 +1284,33 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
                            w_len.p, idoff.p, w_slot.p, nw, pool.p, slot_info.p, status.p, n);
         BPE_HIP(hipGetLastError());
     }
-    // 4. ids per span, offsets, then write: two streams over the records
-    DevBuf<unsigned long long>&per = S.per, &per_off = S.per_off;
-    per.reserve(n_spans);
-    per_off.reserve(n_spans);
-    hipLaunchKernelGGL(k_enc_count, dim3(ceil_div(n_spans, 256)), dim3(256), 0, s, recs, t_start.p,
-                       t_count.p, n_spans, slot_info.p, cap, status.p, per.p);
-    exclusive_sum(per.p, per_off.p, n_spans, s, &S.tmp);
-    unsigned long long last[2];
+    // 4. ids: one pass over the records, chunk offsets by look-back
+    DevBuf<unsigned long long>& flags = S.flags;
+    DevBuf<unsigned>& ticket = S.ticket;
+    flags.reserve(n_chunks);
+    ticket.reserve(1);
+    BPE_HIP(hipMemsetAsync(flags.p, 0, n_chunks * 8, s));
+    BPE_HIP(hipMemsetAsync(ticket.p, 0, 4, s));
+    auto ekern = k_enc_emit<OutT>;
+    int e_cu = 0;
+    BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&e_cu, ekern, 256, 0));
+    const unsigned egrid = (unsigned)std::min<size_t>(n_chunks, (size_t)std::max(1, e_cu) * std::max(1, n_cu));
+    EmitArgs EA{T.recs_cache.p, rec_base.p, rec_n.p, n_chunks, slot_info.p, pool.p, cap, D, E.sp_vid,
+                ticket.p, flags.p, status.p};
+    hipLaunchKernelGGL(ekern, dim3(egrid), dim3(256), 0, s, EA, d_out);
+    BPE_HIP(hipGetLastError());
+    unsigned long long last_flag = 0;
     unsigned st = 0;
-    to_host(&last[0], per_off.p + n_spans - 1, 8, s);
-    to_host(&last[1], per.p + n_spans - 1, 8, s);
+    to_host(&last_flag, flags.p + n_chunks - 1, 8, s);
     to_host(&st, status.p, 4, s);
     if (st & 4u) throw Error{BPE_E_KEY, "a merged token is not in the vocab"};
-    BPE_REQUIRE(!(st & 112u), BPE_E_HIP, "internal error: encode records inconsistent (status " +
-                                           std::to_string(st) + ")");
-    const size_t total = last[0] + last[1];
-    BPE_REQUIRE(total <= n, BPE_E_HIP, "encode produced more ids than input bytes");
-    if (sizeof(OutT) == 2) BPE_HIP(hipMemsetAsync(status.p, 0, 4, s));
-    hipLaunchKernelGGL(k_enc_write<OutT>, dim3(ceil_div(n_spans, 256)), dim3(256), 0, s, recs, t_start.p,
-                       t_count.p, n_spans, slot_info.p, pool.p, E.sp_vid, per.p, per_off.p, cap, d_out, status.p);
-    BPE_HIP(hipGetLastError());
-    if (sizeof(OutT) == 2) {
-        to_host(&st, status.p, 4, s);
+    BPE_REQUIRE(!(st & 96u), BPE_E_HIP, "internal error: encode records inconsistent (status " +
+                                          std::to_string(st) + ")");
+    BPE_REQUIRE((last_flag >> 62) == 2, BPE_E_HIP, "internal error: encode look-back incomplete");
+    if (sizeof(OutT) == 2)
         BPE_REQUIRE(!(st & 128u), BPE_E_LIMIT, "a token id does not fit np.uint16 (vocab larger than 65536)");
-    }
+    const size_t total = last_flag & kLbVal;
+    BPE_REQUIRE(total <= n, BPE_E_HIP, "encode produced more ids than input bytes");
     BPE_HIP(hipStreamSynchronize(s));
     return total;
 }

@@ -21,6 +21,8 @@
 #include <cstdlib>
 #include <vector>
 
+#include <chrono>
+
 #include "internal.h"
 #include "prims.h"
 #include "stage.h"
@@ -108,7 +110,9 @@ void Comm::allgather_bytes(const void* d_send, size_t bytes, void* d_recv, hipSt
 }
 
 void union_word_tables(const uint8_t* text, WordCounts& wc, Comm* comm, hipStream_t stream,
-                       DevBuf<uint8_t>& all, uint64_t* union_words) {
+                       DevBuf<uint8_t>& all, uint64_t* union_words, bpe_train_stats* stats) {
+    using clk = std::chrono::steady_clock;
+    auto ms = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
     const int R = comm->nranks;
     // ---- local records
     DevBuf<unsigned> nwd(1);
@@ -165,8 +169,16 @@ void union_word_tables(const uint8_t* text, WordCounts& wc, Comm* comm, hipStrea
     { WordCounts drop = std::move(wc); }
     w_off.release(); w_cnt.release(); w_len.release(); b_off.release(); len64.release();
     all.alloc((size_t)R * seg_bytes);
+    BPE_HIP(hipStreamSynchronize(stream));
+    const auto tg = clk::now();
     comm->allgather_bytes(seg.p, seg_bytes, all.p, stream);
+    BPE_HIP(hipStreamSynchronize(stream));
+    if (stats) {
+        stats->t_gather_ms = ms(tg);
+        stats->exchange_seg_bytes = (int64_t)seg_bytes;
+    }
     seg.release();
+    const auto tu = clk::now();
     // ---- union table (load <= 1/2 even if no word repeats across ranks)
     DevBuf<unsigned long long> d_nw(R);
     BPE_HIP(hipMemcpyAsync(d_nw.p, nw_r.data(), R * 8, hipMemcpyHostToDevice, stream));
@@ -185,6 +197,7 @@ void union_word_tables(const uint8_t* text, WordCounts& wc, Comm* comm, hipStrea
     BPE_HIP(hipMemcpyAsync(&st, status.p, 4, hipMemcpyDeviceToHost, stream));
     BPE_HIP(hipStreamSynchronize(stream));
     BPE_REQUIRE(!(st & 1u), BPE_E_NOMEM, "union word table overflow");
+    if (stats) stats->t_union_ms = ms(tu);
     if (union_words) *union_words = total_w;
     if (std::getenv("BPE355_TRACE"))
         std::fprintf(stderr, "[bpe355 r%d] word exchange: %u local words, %llu bytes; segment %zu B x %d ranks\n",

@@ -118,8 +118,9 @@ struct Prepared {
 // ---------------------------------------------------------------- multi-GPU word exchange
 // Replace this rank's word table by the union of every rank's (counts summed), whose words'
 // bytes live in `all` (exchange.hip).  One all-gather; afterwards no rank needs the others.
+// stats (may be null): t_gather_ms, t_union_ms and exchange_seg_bytes are filled in.
 void union_word_tables(const uint8_t* text, WordCounts& wc, Comm* comm, hipStream_t stream,
-                       DevBuf<uint8_t>& all, uint64_t* union_words);
+                       DevBuf<uint8_t>& all, uint64_t* union_words, bpe_train_stats* stats = nullptr);
 
 // ---------------------------------------------------------------- training driver
 struct TrainOutput {

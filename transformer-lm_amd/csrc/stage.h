@@ -30,7 +30,7 @@ constexpr int kPadded = kWin + (kWin / 64) * 4;   // +4 B per 64 B: threads' spa
 constexpr int kVec = (kWin + 16 * 256 - 1) / (16 * 256);   // 16-B loads per thread per chunk
 constexpr unsigned long long kBusy = 1ULL << 63;
 
-__device__ __forceinline__ uint64_t short_hash(uint64_t lo, uint64_t hi, size_t len) {
+__host__ __device__ inline uint64_t short_hash(uint64_t lo, uint64_t hi, size_t len) {
     return mix64(lo ^ mix64(hi ^ (len << 56) ^ 0x9E3779B97F4A7C15ULL));
 }
 

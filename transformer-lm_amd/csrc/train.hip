@@ -3587,7 +3587,7 @@ void train_on_device(const uint8_t* d_raw, size_t n, int vocab_size,
     if (comm && !per_round && (comm->nranks > 1 || std::getenv("BPE355_FORCE_EXCHANGE"))) {
         auto te = std::chrono::steady_clock::now();
         uint64_t uw = 0;
-        union_word_tables(text, wc, comm, stream, union_text, &uw);
+        union_word_tables(text, wc, comm, stream, union_text, &uw, &out.stats);
         text = union_text.p;
         loop_comm = nullptr;
         out.stats.t_exchange_ms = ms_since(te);
