@@ -110,3 +110,39 @@ def test_encode_several_devices_equals_one(ranks, monkeypatch):
         bpe_amd.set_num_gpus(None)
     assert many == one
     assert one == oracle.encode(vocab, merges, specials, text)
+
+
+@pytest.mark.parametrize("knobs", [
+    {"BPE355_ENC_PEND_CAP": "0"},                                # no pending pool: the scan resolves words
+    {"BPE355_ENC_PEND_CAP": "40000", "BPE355_STREAM_WG": "2"},   # the pool runs out part way
+    {"BPE355_NOCACHE": "1"},                                     # no LDS cache: every word pending
+    {"BPE355_ENC_REC_CAP": "1000"},                              # too few records: the retry
+])
+def test_encode_resolution_paths(monkeypatch, knobs):
+    """the encoder's record paths against the oracle: pending entries resolved by k_enc_resolve,
+    words resolved in the scan itself, no LDS cache, the record buffer's retry -- with the
+    dictionary (GPT-2 vocab entries), one-byte words and specials all present"""
+    import synth_text
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    vocab, merges = gpt2_files.load_gpt2(["<|endoftext|>"])
+    text = synth_text.generate(23, 1_500_000, "mixed") + "<|endoftext|>" + synth_text.generate(24, 300_000, "space")
+    tok = bpe_amd.Tokenizer(dict(vocab), list(merges), ["<|endoftext|>"])
+    assert tok.encode(text) == oracle.encode(vocab, merges, ["<|endoftext|>"], text)
+
+
+def test_encode_special_in_vocab_and_dictionary_edge_words():
+    """words the dictionary must leave out or treat specially: a vocab entry equal to a special
+    (0 ids when met as a pre-token is impossible -- re.split takes it -- but the dictionary still
+    holds it), merges whose product is missing from the vocab (KeyError, as vocab_inv[...] raises),
+    one-byte specials, and several-id dictionary words"""
+    vocab = {i: bytes([i]) for i in range(256)}
+    merges = [(b" ", b"a"), (b" a", b"b"), (b"c", b"d"), (b"x", b"y")]
+    for a, b in merges[:3]:
+        vocab[len(vocab)] = a + b
+    vocab[len(vocab)] = b"<s>"
+    tok = bpe_amd.Tokenizer(dict(vocab), list(merges), ["<s>", "q"])
+    text = " ab cd <s> abq cdcd  ab x"
+    assert tok.encode(text) == oracle.encode(vocab, merges, ["<s>", "q"], text)
+    with pytest.raises(KeyError):
+        tok.encode(" xy")   # (x, y) merges to b"xy", which has no id

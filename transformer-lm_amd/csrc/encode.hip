@@ -78,28 +78,56 @@ __device__ __forceinline__ bool bytes_eq(const uint8_t* x, const uint8_t* y, siz
 // Matches are appended as position << 16 | special index (sorted on the device afterwards).
 constexpr int kSpShift = 16;
 
-__global__ void k_find_specials(const uint8_t* __restrict__ s, size_t n, EncTables E,
-                                const unsigned* __restrict__ first_mask,
-                                unsigned long long* __restrict__ key_out,
-                                unsigned* __restrict__ n_out, unsigned long long cap) {
+__global__ void __launch_bounds__(256) k_find_specials(const uint8_t* __restrict__ s, size_t n, EncTables E,
+                                                       const unsigned* __restrict__ first_mask,
+                                                       unsigned long long* __restrict__ key_out,
+                                                       unsigned* __restrict__ n_out, unsigned long long cap) {
     // Every special matching at i is recorded (sorted longest first, the host takes the first
     // that fits): when the longest one straddles a piece cut, re.split on that piece still
     // matches a shorter special that is its prefix (tokenizer.py:63-66).
-    // grid-stride over the text, the trip count uniform over the workgroup (wave_append needs
-    // every lane of the wave)
-    for (size_t b0 = (size_t)blockIdx.x * blockDim.x; b0 < n; b0 += (size_t)gridDim.x * blockDim.x) {
-        const size_t i = b0 + threadIdx.x;
-        bool cand = false;
-        if (i < n) {
-            const unsigned b = s[i];
-            cand = (first_mask[b >> 5] >> (b & 31)) & 1u;
+    // A thread takes 16 bytes (one aligned 16-byte load; the text is streamed once), marks the
+    // bytes that may start a special (first-byte bitmap) and compares only those.  Grid-stride,
+    // the trip count uniform over the workgroup (wave_append needs every lane of the wave).
+    __shared__ unsigned s_fm[8];
+    if (threadIdx.x < 8) s_fm[threadIdx.x] = first_mask[threadIdx.x];
+    __syncthreads();
+    const uintptr_t a0 = reinterpret_cast<uintptr_t>(s) & ~(uintptr_t)15;
+    const size_t lead = reinterpret_cast<uintptr_t>(s) - a0;
+    const size_t nv = (n + lead + 15) / 16;   // 16-byte units covering [s, s + n)
+    for (size_t v0 = (size_t)blockIdx.x * blockDim.x; v0 < nv; v0 += (size_t)gridDim.x * blockDim.x) {
+        const size_t v = v0 + threadIdx.x;
+        uint32_t w[4] = {0, 0, 0, 0};
+        unsigned cm = 0;   // bytes of the unit that may start a special
+        if (v < nv) {
+            const long long p0 = (long long)(16 * v) - (long long)lead;   // text position of byte 0
+            if (p0 >= 0 && p0 + 16 <= (long long)n) {
+                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a0 + 16 * v));
+                w[0] = q.x; w[1] = q.y; w[2] = q.z; w[3] = q.w;
+            } else {
+                for (int j = 0; j < 16; ++j) {
+                    const long long p = p0 + j;
+                    if (p >= 0 && p < (long long)n) w[j >> 2] |= (uint32_t)s[p] << (8 * (j & 3));
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const long long p = p0 + j;
+                const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
+                if (p >= 0 && p < (long long)n && ((s_fm[b >> 5] >> (b & 31)) & 1u)) cm |= 1u << j;
+            }
         }
-        if (!__any(cand)) continue;
-        for (int k = 0; k < E.n_sp; ++k) {
-            const unsigned l = E.sp_len[k];
-            const bool hit = cand && i + l <= n && bytes_eq(s + i, E.sp_bytes + E.sp_off[k], l);
-            const unsigned idx = wave_append(hit, n_out);
-            if (hit && idx < cap) key_out[idx] = ((unsigned long long)i << kSpShift) | (unsigned)k;
+        if (!__any(cm != 0)) continue;
+        for (int j = 0; j < 16; ++j) {
+            const bool cand = (cm >> j) & 1u;
+            if (!__any(cand)) continue;
+            const size_t i = 16 * v + j - lead;
+            for (int k = 0; k < E.n_sp; ++k) {
+                const unsigned l = E.sp_len[k];
+                const bool hit = cand && i + l <= n && bytes_eq(s + i, E.sp_bytes + E.sp_off[k], l);
+                const unsigned idx = wave_append(hit, n_out);
+                if (hit && idx < cap) key_out[idx] = ((unsigned long long)i << kSpShift) | (unsigned)k;
+            }
         }
     }
 }
@@ -171,28 +199,32 @@ __global__ void k_sp_emit(const unsigned long long* __restrict__ keys, size_t me
 
 // ------------------------------------------------------------------ 2. the scan: one record per pre-token
 // Records.  Every pre-token becomes one u32; the top two bits say what it names:
-//   kRecDirect | id    a word of exactly one vocab id, known during the scan: one-byte words
-//                      (the byte table) and the dictionary's one-id words
+//   kRecDirect | id    a word of exactly one vocab id: one-byte words (the byte table) and the
+//                      dictionary's one-id words
 //   kRecSpecial | k    special token k (one id)
-//   kRecDict | slot    a dictionary word of several ids (or none), ids in the dictionary's pool
-//   slot               a word-table slot: a word first met in this text, encoded after the scan
-//                      by k_encode_words (slot_info)
+//   kRecPend | pw      (scan output only) a word the scan left to k_enc_resolve: pending entry pw,
+//                      which the resolve overwrites with the word's final record
+//   slot               kind 0: a word-table slot (slot < cap: a word first met in this text,
+//                      encoded after the scan by k_encode_words), or cap + a dictionary slot (a
+//                      dictionary word of several ids, or none)
 // The dictionary (built once per tokenizer, build_dictionary) holds every vocab entry of 2..16
 // bytes with its encoding: a pre-token's ids depend only on its bytes (tokenizer.py:124-136), so
-// any word found there needs neither the word table nor a gather later.  Frequent words of a
-// corpus are the vocab's own entries, so most pre-tokens resolve in the LDS cache, the byte
-// table or the dictionary (2 MB, L2-resident), and only the long tail reaches the word table.
+// a word found there needs no word-table entry.  The scan itself touches no global table: a word
+// its LDS cache does not hold becomes a pending entry (its position and length, 8 bytes), and a
+// separate kernel with registers to spare resolves all of them with many lookups in flight --
+// the dictionary (2 MB, L2-resident) first, then the word table.
 constexpr uint32_t kRecKind = 0xC0000000u;
 constexpr uint32_t kRecDirect = 0xC0000000u;
 constexpr uint32_t kRecSpecial = 0x80000000u;
-constexpr uint32_t kRecDict = 0x40000000u;
-constexpr uint32_t kRecPayload = 0x3FFFFFFFu;   // ids and slots of direct / dictionary records < this
+constexpr uint32_t kRecPend = 0x40000000u;
+constexpr uint32_t kRecPayload = 0x3FFFFFFFu;   // ids, slots and pending indices are below this
 constexpr uint32_t kRecNone = 0xFFFFFFFFu;      // byte table / dictionary lookup: no record
+constexpr uint32_t kDictMark = 0x40000000u;     // DictEnt.rec of a several-id word: kDictMark | slot
 
 struct DictEnt {               // 32 bytes: one probe is one aligned 32-byte read
     uint64_t lo, hi;           // packed bytes
     uint32_t len;              // 0: an empty slot
-    uint32_t rec;              // the word's record (kRecDirect | id, or kRecDict | this slot)
+    uint32_t rec;              // the word's record (kRecDirect | id, or kDictMark | this slot)
     unsigned long long info;   // its ids (slot_info format below; the pool is the dictionary's)
 };
 struct EncDict {
@@ -255,8 +287,23 @@ struct ScanArgs {
     unsigned long long* rec_fill;
     unsigned long long* rec_base;     // per chunk: its run in recs
     uint32_t* rec_n;
+    unsigned long long* pend;         // pending entries: position << 24 | length
+    unsigned pend_blocks;             // blocks of kPendBlock entries in the pool
+    unsigned* pend_nblk;              // blocks handed out
+    uint32_t* block_used;             // entries used per block
     unsigned* status;
 };
+
+// A workgroup appends its pending entries to a block of the pool it holds; a block is
+// chunk-sized (a chunk has at most one pre-token per byte), so a chunk that does not fit the
+// rest of the block takes a new one before its token phase and the appends never check.
+constexpr unsigned kPendBlock = kChunk;
+constexpr int kPendShift = 24;        // pending entry: position << 24 | length (< 2^24)
+
+// a dictionary record as the emit reads it: several-id words are cap + their dictionary slot
+__device__ __forceinline__ uint32_t dict_rec(uint32_t rec, size_t cap) {
+    return (rec & kRecKind) == kDictMark ? (uint32_t)(cap + (rec & kRecPayload)) : rec;
+}
 
 // Persistent workgroups stream 16 KiB chunks through LDS (stage2.h).  Every thread turns its
 // 64-byte block into a token-start mask with tokstart.h's predicate, evaluated once per segment
@@ -264,13 +311,16 @@ struct ScanArgs {
 // read '\n', the segment end is the text end: each segment is pre-tokenized on its own,
 // tokenizer.py:68-90); a special segment is one token.  A block's pre-tokens are the set bits of
 // its mask, so the chunk's record count and every thread's offset in the chunk's run are one
-// block scan of popcounts, and the records of a chunk are written densely.
+// block scan of popcounts, and the records of a chunk are written densely.  Per pre-token: a
+// special or a one-byte word is its record; a word of 2..16 bytes is looked up in the LDS cache
+// (word -> record); anything else becomes a pending entry, cached as such.  Only when the pool
+// of pending entries is spent does the scan resolve words itself (dictionary, word table).
 // workgroups per CU the scan's registers are capped for (build knob)
 #ifndef BPE355_ENC_SCAN_WG
 #define BPE355_ENC_SCAN_WG 4
 #endif
 template <bool kAligned>
-__global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan3(ScanArgs A, EncDict D) {
+__global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan4(ScanArgs A, EncDict D) {
     __shared__ uint64_t s_mask[kWords];
     __shared__ unsigned long long c_key[kEncCache];
     __shared__ uint64_t c_lo[kEncCache], c_hi[kEncCache];
@@ -282,24 +332,47 @@ __global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan3(ScanArgs 
     __shared__ unsigned long long s_red[4];
     __shared__ uint32_t s_wsum[4];
     __shared__ unsigned long long s_rbase;
-    __shared__ int s_stop;
+    __shared__ int s_stop, s_pblk;   // s_pblk: the pending block held (-2: none yet, -1: pool spent)
+    __shared__ unsigned s_pused;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint8_t* __restrict__ s = A.s;
     const size_t n = A.n;
+    const size_t cap = A.mask + 1;
     for (int i = tid; i < kEncCache; i += blockDim.x) { c_key[i] = 0; c_hit[i] = 0; }
     s_brec[tid] = D.byte_rec[tid];
+    if (tid == 0) {
+        s_pblk = A.pend ? -2 : -1;
+        s_pused = 0;
+    }
     load_cls2(tid, blockDim.x);
     unsigned long long inserted = 0;
 
-    // a word through the table: its slot as the record (0 when the table is full: the host
-    // retries with a larger one)
-    auto table_rec = [&](size_t len, size_t gp, uint64_t wl, uint64_t wh, uint64_t h) -> uint32_t {
+    // a word resolved here (the pool is spent): dictionary, then the word table (its slot; 0 when
+    // the table is full: the host retries with a larger one)
+    auto resolve_here = [&](size_t len, size_t gp, uint64_t wl, uint64_t wh, uint64_t h) -> uint32_t {
+        if (len <= (size_t)kInline && len >= 2) {
+            const uint32_t rec = dict_find(D, wl, wh, (uint32_t)len, h);
+            if (rec != kRecNone) return dict_rec(rec, cap);
+        }
         bool ins = false;
         const size_t slot = table_add(s, s, gp, len, wl, wh, h, 0, A.kv, A.pos, A.mask, A.status, &ins);
         inserted += ins;
         return slot == ~(size_t)0 ? 0u : (uint32_t)slot;
     };
-    // a pre-token of 2..16 bytes at stage position r (global gp): LDS cache, dictionary, table
+    // a word left to k_enc_resolve, or resolved here when the pool is spent
+    auto pending = [&](size_t len, size_t gp, uint64_t wl, uint64_t wh, bool packed) -> uint32_t {
+        const int pb = s_pblk;
+        if (pb >= 0) {
+            const unsigned idx = atomicAdd(&s_pused, 1u);   // < kPendBlock: reserved per chunk
+            const unsigned long long pw = (unsigned long long)pb * kPendBlock + idx;
+            A.pend[pw] = ((unsigned long long)gp << kPendShift) | len;
+            return kRecPend | (uint32_t)pw;
+        }
+        if (!packed && len <= (size_t)kInline) pack_word(s, gp, len, wl, wh);
+        const uint64_t h = len <= (size_t)kInline ? short_hash(wl, wh, len) : hash_word(s, gp, len);
+        return resolve_here(len, gp, wl, wh, h);
+    };
+    // a pre-token of 2..16 bytes at stage position r (global gp): the LDS cache, else pending
     auto short_rec = [&](uint32_t r, size_t len, size_t gp) -> uint32_t {
         uint64_t wl, wh;
         pack_stage(kPre + (int)r, (int)len, wl, wh);
@@ -318,8 +391,7 @@ __global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan3(ScanArgs 
                 }
             }
         }
-        uint32_t rec = dict_find(D, wl, wh, (uint32_t)len, h);
-        if (rec == kRecNone) rec = table_rec(len, gp, wl, wh, h);
+        const uint32_t rec = pending(len, gp, wl, wh, true);
         if (A.use_cache) {
             for (int way = 0; way < 2; ++way) {   // cache it if a way is free
                 const unsigned sl = ls + way;
@@ -426,6 +498,13 @@ __global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan3(ScanArgs 
             s_rbase = b;
             A.rec_base[c] = b == ~0ULL ? 0 : b;
             A.rec_n[c] = b == ~0ULL ? 0 : total;
+            // room in the pending block for every pre-token of the chunk
+            if (s_pblk != -1 && (s_pblk == -2 || s_pused + total > kPendBlock)) {
+                if (s_pblk >= 0) A.block_used[s_pblk] = s_pused;
+                const unsigned nb = atomicAdd(A.pend_nblk, 1u);
+                s_pblk = nb < A.pend_blocks ? (int)nb : -1;
+                s_pused = 0;
+            }
         }
         __syncthreads();
         const unsigned long long rbase = s_rbase;
@@ -467,18 +546,14 @@ __global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan3(ScanArgs 
                         const size_t len = e - gp;
                         if (len == 1) {
                             rec = s_brec[StageText{}[r]];
-                            if (rec == kRecNone) {
-                                uint64_t wl, wh;
-                                pack_stage(kPre + (int)r, 1, wl, wh);
-                                rec = table_rec(1, gp, wl, wh, short_hash(wl, wh, 1));
-                            }
+                            if (rec == kRecNone) rec = pending(1, gp, 0, 0, false);
                         } else if (len <= (size_t)kInline) {
                             rec = short_rec(r, len, gp);
-                        } else if (len >= (1ULL << 24)) {
+                        } else if (len >= (1ULL << kPendShift)) {
                             atomicOr(A.status, 2u);
                             rec = 0;
                         } else {
-                            rec = table_rec(len, gp, 0, 0, hash_word(s, gp, len));
+                            rec = pending(len, gp, 0, 0, false);
                         }
                     }
                 }
@@ -504,6 +579,55 @@ __global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan3(ScanArgs 
             if (b) atomicAdd(A.fill, b);
         }
     }
+    __syncthreads();
+    if (tid == 0 && s_pblk >= 0) A.block_used[s_pblk] = s_pused;
+}
+
+// Every pending entry to its final record, in place: the word's bytes from the text, then the
+// dictionary, then the word table.  One entry per thread, no mask work: the lookups of many
+// entries are in flight at once.
+struct ResolveArgs {
+    const uint8_t* s;
+    unsigned long long* pend;
+    const uint32_t* block_used;
+    unsigned long long n_entries;     // blocks handed out x kPendBlock
+    unsigned long long* kv;
+    unsigned long long* pos;
+    size_t mask;
+    unsigned long long* fill;
+    unsigned* status;
+};
+
+__global__ void __launch_bounds__(256) k_enc_resolve(ResolveArgs A, EncDict D) {
+    const size_t cap = A.mask + 1;
+    unsigned long long inserted = 0;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.n_entries; i += stride) {
+        if ((i & (kPendBlock - 1)) >= A.block_used[i / kPendBlock]) continue;
+        const unsigned long long e = A.pend[i];
+        const size_t gp = (size_t)(e >> kPendShift), len = (size_t)(e & ((1ULL << kPendShift) - 1));
+        uint32_t rec = kRecNone;
+        uint64_t wl = 0, wh = 0, h;
+        if (len <= (size_t)kInline) {
+            pack_word(A.s, gp, len, wl, wh);
+            h = short_hash(wl, wh, len);
+            if (len >= 2) {
+                rec = dict_find(D, wl, wh, (uint32_t)len, h);
+                if (rec != kRecNone) rec = dict_rec(rec, cap);
+            }
+        } else {
+            h = hash_word(A.s, gp, len);
+        }
+        if (rec == kRecNone) {   // (a probe chain past kMaxProbe sets status 1: the host retries)
+            bool ins = false;
+            const size_t slot = table_add(A.s, A.s, gp, len, wl, wh, h, 0, A.kv, A.pos, A.mask, A.status, &ins);
+            inserted += ins;
+            rec = slot == ~(size_t)0 ? 0u : (uint32_t)slot;
+        }
+        A.pend[i] = rec;
+    }
+    inserted = wave_sum(inserted);
+    if ((threadIdx.x & 63) == 0 && inserted) atomicAdd(A.fill, inserted);
 }
 
 // ------------------------------------------------------------------ 3. unique words
@@ -541,20 +665,24 @@ struct EmitArgs {
     const uint32_t* pool;
     size_t cap;                            // word-table slots
     EncDict D;
+    size_t dict_slots;
+    const unsigned long long* pend;        // resolved pending entries
     const int64_t* sp_vid;
     unsigned* ticket;                      // chunks in the order workgroups take them
     unsigned long long* flags;             // per chunk: look-back state | id count
     unsigned* status;
 };
 
-// a record's ids in slot_info format (one load at most: a one-id word carries its id)
+// a record's ids in slot_info format (a one-id word carries its id)
 __device__ __forceinline__ unsigned long long rec_info(const EmitArgs& A, uint32_t rec) {
+    if ((rec & kRecKind) == kRecPend) rec = (uint32_t)A.pend[rec & kRecPayload];   // resolved in place
     const uint32_t kind = rec & kRecKind, pl = rec & kRecPayload;
     if (kind == kRecDirect) return kOneId | pl;
     if (kind == kRecSpecial) return kOneId | (uint32_t)A.sp_vid[pl];
-    if (kind == kRecDict) return A.D.ent[pl].info;
-    if (rec >= A.cap) { atomicOr(A.status, 32u); return 0; }   // a record naming no slot: a bug
-    return A.slot_info[rec];
+    if (rec < A.cap) return A.slot_info[rec];
+    if (kind == 0 && rec - A.cap < A.dict_slots) return A.D.ent[rec - A.cap].info;
+    atomicOr(A.status, 32u);   // a record naming nothing: a bug
+    return 0;
 }
 
 // the ids of one info through put(position, id), from position o; returns how many
@@ -835,9 +963,10 @@ struct bpe_tokenizer {
     // the other per-call device arrays, kept the same way (grow-only): per chunk, per word-table
     // slot, per unique word, the id pool, the u16 output of the bulk encoder
     struct Scratch {
-        bpe::DevBuf<uint32_t> rec_n, w_slot, w_len, pool;
+        bpe::DevBuf<uint32_t> rec_n, w_slot, w_len, pool, block_used;
         bpe::DevBuf<unsigned long long> rec_base, rec_fill, flags, fill, kv, pos, w_off, len64, idoff, slot_info;
-        bpe::DevBuf<unsigned> status, d_nw, ticket;
+        bpe::DevBuf<unsigned> status, d_nw, ticket, pend_nblk;
+        bpe::DevBuf<unsigned long long> pend;   // the scan's pending entries (resolved in place)
         bpe::DevBuf<bpe::Seg> segs;
         bpe::DevBuf<unsigned long long> sp_key, sp_sorted;   // special matches, (position << 16 | index)
         bpe::DevBuf<unsigned long long> sp_cnt, sp_off, cuts;   // the device segment builder's arrays
@@ -955,7 +1084,7 @@ void build_dictionary(bpe_tokenizer& T, const std::unordered_map<std::string, ui
             e.rec = kRecDirect | ids[0];
             e.info = kOneId | ids[0];
         } else {
-            e.rec = kRecDict | (uint32_t)sl;
+            e.rec = kDictMark | (uint32_t)sl;
             e.info = ids.empty() ? 0ULL : (((unsigned long long)ids.size() << 39) | kDictPool | dpool.size());
             dpool.insert(dpool.end(), ids.begin(), ids.end());
         }
@@ -1108,7 +1237,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
         for (;;) {
             S.sp_key.reserve(cap);
             BPE_HIP(hipMemsetAsync(S.status.p, 0, 4, s));
-            hipLaunchKernelGGL(k_find_specials, dim3(grid_for(n, 256)), dim3(256), 0, s, d_text, n, E,
+            hipLaunchKernelGGL(k_find_specials, dim3(grid_for((n + 15) / 16 + 1, 256)), dim3(256), 0, s, d_text, n, E,
                                T.first_mask.p, S.sp_key.p, S.status.p, cap);
             BPE_HIP(hipGetLastError());
             to_host(&cnt32, S.status.p, 4, s);
@@ -1192,7 +1321,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
     const size_t n_chunks = (n + kChunk - 1) / kChunk;
     BPE_REQUIRE(n_chunks < (1ull << 32), BPE_E_LIMIT, "text too long for one encode");
     const bool aligned = (reinterpret_cast<uintptr_t>(d_text) & 15u) == 0;
-    auto kern = aligned ? k_enc_scan3<true> : k_enc_scan3<false>;
+    auto kern = aligned ? k_enc_scan4<true> : k_enc_scan4<false>;
     int per_cu = 0, dev = 0, n_cu = 0;
     BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, kStage));
     BPE_HIP(hipGetDevice(&dev));
@@ -1206,6 +1335,13 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
     unsigned long long rec_cap = n < (1u << 26) ? n + 64 : n / 4 + (1u << 20);
     if (const char* e = std::getenv("BPE355_ENC_REC_CAP"))   // test knob: force the record retry
         rec_cap = std::max<unsigned long long>(1, std::strtoull(e, nullptr, 10));
+    // pending entries: ~0.07 per byte at the bench corpus (the LDS cache's misses); a block per
+    // workgroup at least twice over; when the pool is spent the scan resolves words itself
+    unsigned long long pend_cap = std::max<unsigned long long>(n / 8, 2ull * sgrid * kPendBlock);
+    if (const char* e = std::getenv("BPE355_ENC_PEND_CAP"))   // test knob: a small pool (0: none)
+        pend_cap = std::strtoull(e, nullptr, 10);
+    pend_cap = std::min<unsigned long long>(pend_cap, (unsigned long long)kRecPayload + 1 - kPendBlock);
+    const unsigned pend_blocks = (unsigned)(pend_cap / kPendBlock);
     DevBuf<unsigned long long>&kv = S.kv, &pos = S.pos;
     DevBuf<unsigned long long>&rec_base = S.rec_base, &rec_fill = S.rec_fill, &fill = S.fill;
     DevBuf<uint32_t>& rec_n = S.rec_n;
@@ -1215,9 +1351,13 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
     rec_fill.reserve(1);
     fill.reserve(1);
     status.reserve(1);
+    S.pend.reserve(std::max<unsigned long long>((unsigned long long)pend_blocks * kPendBlock, 1));
+    S.block_used.reserve(std::max(pend_blocks, 1u));
+    S.pend_nblk.reserve(1);
     const EncDict D = T.dict();
+    BPE_REQUIRE(T.dict_slots < kRecPayload / 2, BPE_E_LIMIT, "vocab too large for the encoder's dictionary");
     for (int attempt = 0;; ++attempt) {
-        BPE_REQUIRE(cap <= (size_t)kRecPayload, BPE_E_LIMIT, "too many distinct words for one encode");
+        BPE_REQUIRE(cap + T.dict_slots <= (size_t)kRecPayload, BPE_E_LIMIT, "too many distinct words for one encode");
         kv.reserve(2 * cap);
         pos.reserve(cap);
         T.recs_cache.reserve(rec_cap);
@@ -1225,11 +1365,26 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
         BPE_HIP(hipMemsetAsync(status.p, 0, 4, s));
         BPE_HIP(hipMemsetAsync(fill.p, 0, 8, s));
         BPE_HIP(hipMemsetAsync(rec_fill.p, 0, 8, s));
+        BPE_HIP(hipMemsetAsync(S.pend_nblk.p, 0, 4, s));
         ScanArgs A{d_text, n, n_chunks, d_segs.p, nseg, std::getenv("BPE355_NOCACHE") ? 0 : 1, kv.p, pos.p,
                    cap - 1, (unsigned long long)(cap / 2), fill.p, T.recs_cache.p, rec_cap, rec_fill.p,
-                   rec_base.p, rec_n.p, status.p};
+                   rec_base.p, rec_n.p, pend_blocks ? S.pend.p : nullptr, pend_blocks, S.pend_nblk.p,
+                   S.block_used.p, status.p};
         hipLaunchKernelGGL(kern, dim3(sgrid), dim3(256), kStage, s, A, D);
         BPE_HIP(hipGetLastError());
+        unsigned nblk = 0;
+        to_host(&nblk, S.pend_nblk.p, 4, s);
+        nblk = std::min(nblk, pend_blocks);
+        if (nblk) {   // the pending words, resolved in place
+            int r_cu = 0;
+            BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&r_cu, k_enc_resolve, 256, 0));
+            const unsigned long long ne = (unsigned long long)nblk * kPendBlock;
+            const unsigned rgrid = (unsigned)std::min<unsigned long long>(ceil_div(ne, 256),
+                                                                         (unsigned long long)std::max(1, r_cu) * std::max(1, n_cu) * 8);
+            ResolveArgs RA{d_text, S.pend.p, S.block_used.p, ne, kv.p, pos.p, cap - 1, fill.p, status.p};
+            hipLaunchKernelGGL(k_enc_resolve, dim3(rgrid), dim3(256), 0, s, RA, D);
+            BPE_HIP(hipGetLastError());
+        }
         unsigned st = 0;
         to_host(&st, status.p, 4, s);
         if (st & 2u) throw Error{BPE_E_LIMIT, "a pre-token is longer than 16 MiB"};
@@ -1295,8 +1450,8 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
     int e_cu = 0;
     BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&e_cu, ekern, 256, 0));
     const unsigned egrid = (unsigned)std::min<size_t>(n_chunks, (size_t)std::max(1, e_cu) * std::max(1, n_cu));
-    EmitArgs EA{T.recs_cache.p, rec_base.p, rec_n.p, n_chunks, slot_info.p, pool.p, cap, D, E.sp_vid,
-                ticket.p, flags.p, status.p};
+    EmitArgs EA{T.recs_cache.p, rec_base.p, rec_n.p, n_chunks, slot_info.p, pool.p, cap, D, T.dict_slots,
+                S.pend.p, E.sp_vid, ticket.p, flags.p, status.p};
     hipLaunchKernelGGL(ekern, dim3(egrid), dim3(256), 0, s, EA, d_out);
     BPE_HIP(hipGetLastError());
     unsigned long long last_flag = 0;
