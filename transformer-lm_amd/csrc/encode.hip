@@ -74,9 +74,35 @@ __device__ __forceinline__ bool bytes_eq(const uint8_t* x, const uint8_t* y, siz
     return true;
 }
 
+// bytes [gp, gp + len) of s (len <= 16) packed little-endian, with aligned 8-byte loads (three at
+// most) when the text runs on past them, else byte by byte
+__device__ __forceinline__ void load_word(const uint8_t* __restrict__ s, size_t n, size_t gp, size_t len,
+                                          uint64_t& lo, uint64_t& hi) {
+    if (gp + 24 > n) {
+        pack_word(s, gp, len, lo, hi);
+        return;
+    }
+    const uintptr_t addr = reinterpret_cast<uintptr_t>(s + gp);
+    const uint64_t* a = reinterpret_cast<const uint64_t*>(addr & ~(uintptr_t)7);
+    const unsigned sh = (unsigned)(addr & 7) * 8;
+    const uint64_t q0 = a[0], q1 = a[1];
+    const uint64_t q2 = (addr & 7) + len > 16 ? a[2] : 0;
+    lo = sh ? (q0 >> sh) | (q1 << (64 - sh)) : q0;
+    hi = sh ? (q1 >> sh) | (q2 << (64 - sh)) : q1;
+    if (len < 8) {
+        lo &= (1ULL << (8 * len)) - 1;
+        hi = 0;
+    } else if (len < 16) {
+        hi &= (1ULL << (8 * (len - 8))) - 1;
+    }
+}
+
 // ------------------------------------------------------------------ 1. special candidates
 // Matches are appended as position << 16 | special index (sorted on the device afterwards).
 constexpr int kSpShift = 16;
+
+constexpr int kSpLds = 64;   // specials whose first 16 bytes k_find_specials keeps in LDS
+constexpr unsigned kSpBuf = 2048;   // matches a workgroup of k_find_specials stages in LDS
 
 __global__ void __launch_bounds__(256) k_find_specials(const uint8_t* __restrict__ s, size_t n, EncTables E,
                                                        const unsigned* __restrict__ first_mask,
@@ -85,51 +111,112 @@ __global__ void __launch_bounds__(256) k_find_specials(const uint8_t* __restrict
     // Every special matching at i is recorded (sorted longest first, the host takes the first
     // that fits): when the longest one straddles a piece cut, re.split on that piece still
     // matches a shorter special that is its prefix (tokenizer.py:63-66).
-    // A thread takes 16 bytes (one aligned 16-byte load; the text is streamed once), marks the
-    // bytes that may start a special (first-byte bitmap) and compares only those.  Grid-stride,
-    // the trip count uniform over the workgroup (wave_append needs every lane of the wave).
+    // A thread takes 16-byte units (aligned loads, two in flight; the text is streamed once),
+    // marks the bytes that may start a special (first-byte bitmap) and compares only those: the
+    // 16 bytes at a candidate against the specials' first 16 (LDS), the rest byte by byte.
+    // Grid-stride, the trip count uniform over the workgroup (the candidate loop's __any).
     __shared__ unsigned s_fm[8];
+    __shared__ uint64_t s_lo[kSpLds], s_hi[kSpLds];
+    __shared__ uint32_t s_len[kSpLds];
+    // the workgroup's matches, flushed with one global reservation at the end (a device-scope
+    // atomic per wave that found one: millions of them on one word would serialise at ~88/us)
+    __shared__ unsigned long long s_keys[kSpBuf];
+    __shared__ unsigned s_nk, s_base;
+    if (threadIdx.x == 0) s_nk = 0;
     if (threadIdx.x < 8) s_fm[threadIdx.x] = first_mask[threadIdx.x];
+    const int nsl = E.n_sp < kSpLds ? E.n_sp : kSpLds;
+    if ((int)threadIdx.x < nsl) {
+        const uint32_t l = E.sp_len[threadIdx.x];
+        uint64_t lo = 0, hi = 0;
+        const uint8_t* p = E.sp_bytes + E.sp_off[threadIdx.x];
+        for (uint32_t j = 0; j < l && j < 16; ++j) {
+            if (j < 8) lo |= (uint64_t)p[j] << (8 * j);
+            else hi |= (uint64_t)p[j] << (8 * (j - 8));
+        }
+        s_lo[threadIdx.x] = lo;
+        s_hi[threadIdx.x] = hi;
+        s_len[threadIdx.x] = l;
+    }
     __syncthreads();
-    const uintptr_t a0 = reinterpret_cast<uintptr_t>(s) & ~(uintptr_t)15;
-    const size_t lead = reinterpret_cast<uintptr_t>(s) - a0;
+    const uint8_t* const a0 = s - (reinterpret_cast<uintptr_t>(s) & 15);   // (global address space kept)
+    const size_t lead = (size_t)(s - a0);
     const size_t nv = (n + lead + 15) / 16;   // 16-byte units covering [s, s + n)
-    for (size_t v0 = (size_t)blockIdx.x * blockDim.x; v0 < nv; v0 += (size_t)gridDim.x * blockDim.x) {
-        const size_t v = v0 + threadIdx.x;
-        uint32_t w[4] = {0, 0, 0, 0};
-        unsigned cm = 0;   // bytes of the unit that may start a special
-        if (v < nv) {
-            const long long p0 = (long long)(16 * v) - (long long)lead;   // text position of byte 0
-            if (p0 >= 0 && p0 + 16 <= (long long)n) {
-                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a0 + 16 * v));
-                w[0] = q.x; w[1] = q.y; w[2] = q.z; w[3] = q.w;
-            } else {
-                for (int j = 0; j < 16; ++j) {
-                    const long long p = p0 + j;
-                    if (p >= 0 && p < (long long)n) w[j >> 2] |= (uint32_t)s[p] << (8 * (j & 3));
-                }
-            }
+    const size_t S = (size_t)gridDim.x * blockDim.x;
+    auto unit = [&](size_t v, uint32_t (&w)[4]) -> unsigned {   // candidate bits of unit v
+        unsigned cm = 0;
+        const long long p0 = (long long)(16 * v) - (long long)lead;   // text position of byte 0
 #pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const long long p = p0 + j;
+            const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
+            if (p >= 0 && p < (long long)n && ((s_fm[b >> 5] >> (b & 31)) & 1u)) cm |= 1u << j;
+        }
+        return cm;
+    };
+    auto load = [&](size_t v, uint32_t (&w)[4]) {
+        w[0] = w[1] = w[2] = w[3] = 0;
+        if (v >= nv) return;
+        const long long p0 = (long long)(16 * v) - (long long)lead;
+        if (p0 >= 0 && p0 + 16 <= (long long)n) {
+            const uint4 q = *reinterpret_cast<const uint4*>(a0 + 16 * v);
+            w[0] = q.x; w[1] = q.y; w[2] = q.z; w[3] = q.w;
+        } else {
             for (int j = 0; j < 16; ++j) {
                 const long long p = p0 + j;
-                const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
-                if (p >= 0 && p < (long long)n && ((s_fm[b >> 5] >> (b & 31)) & 1u)) cm |= 1u << j;
+                if (p >= 0 && p < (long long)n) w[j >> 2] |= (uint32_t)s[p] << (8 * (j & 3));
             }
         }
-        if (!__any(cm != 0)) continue;
+    };
+    auto check = [&](size_t v, unsigned cm) {
         for (int j = 0; j < 16; ++j) {
             const bool cand = (cm >> j) & 1u;
             if (!__any(cand)) continue;
             const size_t i = 16 * v + j - lead;
+            uint64_t tl = 0, th = 0;
+            if (cand) load_word(s, n, i, n - i < 16 ? n - i : 16, tl, th);
             for (int k = 0; k < E.n_sp; ++k) {
-                const unsigned l = E.sp_len[k];
-                const bool hit = cand && i + l <= n && bytes_eq(s + i, E.sp_bytes + E.sp_off[k], l);
-                const unsigned idx = wave_append(hit, n_out);
-                if (hit && idx < cap) key_out[idx] = ((unsigned long long)i << kSpShift) | (unsigned)k;
+                bool hit = false;
+                if (cand) {
+                    const uint32_t l = k < kSpLds ? s_len[k] : E.sp_len[k];
+                    if (i + l <= n) {
+                        if (k < kSpLds) {
+                            const uint64_t mlo = l >= 8 ? ~0ULL : (1ULL << (8 * l)) - 1;
+                            const uint64_t mhi = l >= 16 ? ~0ULL : (l <= 8 ? 0ULL : (1ULL << (8 * (l - 8))) - 1);
+                            hit = ((tl ^ s_lo[k]) & mlo) == 0 && ((th ^ s_hi[k]) & mhi) == 0 &&
+                                  (l <= 16 || bytes_eq(s + i + 16, E.sp_bytes + E.sp_off[k] + 16, l - 16));
+                        } else {
+                            hit = bytes_eq(s + i, E.sp_bytes + E.sp_off[k], l);
+                        }
+                    }
+                }
+                if (hit) {
+                    const unsigned long long key = ((unsigned long long)i << kSpShift) | (unsigned)k;
+                    const unsigned li = atomicAdd(&s_nk, 1u);
+                    if (li < kSpBuf) {
+                        s_keys[li] = key;
+                    } else {   // the buffer is full: straight to the global list
+                        const unsigned idx = atomicAdd(n_out, 1u);
+                        if (idx < cap) key_out[idx] = key;
+                    }
+                }
             }
         }
+    };
+    for (size_t v0 = (size_t)blockIdx.x * blockDim.x; v0 < nv; v0 += 2 * S) {
+        const size_t va = v0 + threadIdx.x, vb = va + S;
+        uint32_t wa[4], wb[4];
+        load(va, wa);
+        load(vb, wb);
+        const unsigned ca = va < nv ? unit(va, wa) : 0u, cb = vb < nv ? unit(vb, wb) : 0u;
+        if (__any(ca != 0)) check(va, ca);
+        if (__any(cb != 0)) check(vb, cb);
     }
+    __syncthreads();
+    const unsigned nk = s_nk < kSpBuf ? s_nk : kSpBuf;
+    if (threadIdx.x == 0) s_base = nk ? atomicAdd(n_out, nk) : 0u;
+    __syncthreads();
+    for (unsigned q = threadIdx.x; q < nk; q += blockDim.x)
+        if (s_base + q < cap) key_out[s_base + q] = s_keys[q];
 }
 
 // ------------------------------------------------------------------ 1'. segments on the device
@@ -272,6 +359,54 @@ struct ClipWin {   // one block's window with the bytes before window position l
     }
 };
 
+// The encoder's word table, over the training table's arrays (kv: 16-byte entries, pos): the
+// encoder counts nothing, so an entry's second word holds the word's first 8 bytes and a probe
+// is one 16-byte load, with no read of the text to verify a key:
+//   words of <= 15 bytes: kv[2s] = kInl | len << 56 | bytes 8..14, kv[2s + 1] = bytes 0..7
+//     (claimed by a CAS on the first word, then the second stored: a reader that sees the first
+//     before the second may miss the word and insert it again further on -- a duplicate slot,
+//     which encodes to the same ids);
+//   longer words: kv[2s] = len << 40 | (offset + 1) of an occurrence, verified against the text.
+// pos[s] = an occurrence's offset (k_collect reads (offset, len) of every slot as before).
+constexpr int kEncInline = 15;
+
+__device__ __forceinline__ size_t enc_table_add(const uint8_t* __restrict__ s, size_t gp, size_t len, uint64_t wl,
+                                                uint64_t wh, uint64_t h, unsigned long long* __restrict__ kv,
+                                                unsigned long long* __restrict__ pos, size_t mask,
+                                                unsigned* __restrict__ status, bool* inserted) {
+    *inserted = false;
+    const bool inl = len <= (size_t)kEncInline;
+    const unsigned long long mine = inl ? kInl | ((unsigned long long)len << 56) | wh
+                                        : ((unsigned long long)len << 40) | (gp + 1);
+    size_t slot = h & mask;
+    for (int probe = 0; probe < kMaxProbe; ++probe) {
+        const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(kv + 2 * slot);
+        unsigned long long k = e.x, k0 = e.y;
+        if (k == 0) {
+            k = atomicCAS(&kv[2 * slot], 0ULL, mine);
+            if (k == 0) {   // claimed
+                if (inl) kv[2 * slot + 1] = wl;
+                pos[slot] = gp;
+                *inserted = true;
+                return slot;
+            }
+            k0 = kv[2 * slot + 1];
+        }
+        if (inl) {
+            if (k == mine && k0 == wl) return slot;
+        } else if (!(k & kInl) && (k >> 40) == len) {
+            const size_t q = (k & kOffMask) - 1;
+            bool eq = true;
+            for (size_t i = 0; i < len && eq; ++i) eq = s[q + i] == s[gp + i];
+            if (eq) return slot;
+        }
+        slot = (slot + 1) & mask;
+    }
+    atomicOr(status, 1u);
+    return ~(size_t)0;
+}
+
+
 struct ScanArgs {
     const uint8_t* s;
     size_t n, n_chunks;
@@ -284,6 +419,7 @@ struct ScanArgs {
     unsigned long long* fill;
     uint32_t* recs;                   // records, each chunk's run contiguous
     unsigned long long rec_cap;
+    unsigned long long rec_region;    // records a workgroup reserves at a time (>= kChunk)
     unsigned long long* rec_fill;
     unsigned long long* rec_base;     // per chunk: its run in recs
     uint32_t* rec_n;
@@ -331,7 +467,7 @@ __global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan4(ScanArgs 
     __shared__ int s_seg0, s_segn;   // first segment of the chunk window and how many are in LDS (-1: too many)
     __shared__ unsigned long long s_red[4];
     __shared__ uint32_t s_wsum[4];
-    __shared__ unsigned long long s_rbase;
+    __shared__ unsigned long long s_rbase, s_rnext, s_rend;   // the record region the workgroup holds
     __shared__ int s_stop, s_pblk;   // s_pblk: the pending block held (-2: none yet, -1: pool spent)
     __shared__ unsigned s_pused;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -343,6 +479,7 @@ __global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan4(ScanArgs 
     if (tid == 0) {
         s_pblk = A.pend ? -2 : -1;
         s_pused = 0;
+        s_rnext = s_rend = 0;
     }
     load_cls2(tid, blockDim.x);
     unsigned long long inserted = 0;
@@ -355,7 +492,7 @@ __global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan4(ScanArgs 
             if (rec != kRecNone) return dict_rec(rec, cap);
         }
         bool ins = false;
-        const size_t slot = table_add(s, s, gp, len, wl, wh, h, 0, A.kv, A.pos, A.mask, A.status, &ins);
+        const size_t slot = enc_table_add(s, gp, len, wl, wh, h, A.kv, A.pos, A.mask, A.status, &ins);
         inserted += ins;
         return slot == ~(size_t)0 ? 0u : (uint32_t)slot;
     };
@@ -490,11 +627,19 @@ __global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan4(ScanArgs 
         for (int w = 0; w < wave; ++w) toff += s_wsum[w];
         if (tid == 0) {
             const uint32_t total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
-            unsigned long long b = atomicAdd(A.rec_fill, (unsigned long long)total);
-            if (b + total > A.rec_cap) {   // the record buffer is too small: the host retries
-                atomicOr(A.status, 256u);
-                b = ~0ULL;
+            // the chunk's run in the workgroup's region; a new region (one global reservation per
+            // rec_region records) when it does not fit
+            unsigned long long b = s_rnext;
+            if (b + total > s_rend) {
+                b = atomicAdd(A.rec_fill, A.rec_region);
+                s_rend = b + A.rec_region;
+                if (s_rend > A.rec_cap) {   // the record buffer is too small: the host retries
+                    atomicOr(A.status, 256u);
+                    s_rend = 0;
+                    b = ~0ULL;
+                }
             }
+            if (b != ~0ULL) s_rnext = b + total;
             s_rbase = b;
             A.rec_base[c] = b == ~0ULL ? 0 : b;
             A.rec_n[c] = b == ~0ULL ? 0 : total;
@@ -588,6 +733,7 @@ __global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan4(ScanArgs 
 // entries are in flight at once.
 struct ResolveArgs {
     const uint8_t* s;
+    size_t n;
     unsigned long long* pend;
     const uint32_t* block_used;
     unsigned long long n_entries;     // blocks handed out x kPendBlock
@@ -609,7 +755,7 @@ __global__ void __launch_bounds__(256) k_enc_resolve(ResolveArgs A, EncDict D) {
         uint32_t rec = kRecNone;
         uint64_t wl = 0, wh = 0, h;
         if (len <= (size_t)kInline) {
-            pack_word(A.s, gp, len, wl, wh);
+            load_word(A.s, A.n, gp, len, wl, wh);
             h = short_hash(wl, wh, len);
             if (len >= 2) {
                 rec = dict_find(D, wl, wh, (uint32_t)len, h);
@@ -620,7 +766,7 @@ __global__ void __launch_bounds__(256) k_enc_resolve(ResolveArgs A, EncDict D) {
         }
         if (rec == kRecNone) {   // (a probe chain past kMaxProbe sets status 1: the host retries)
             bool ins = false;
-            const size_t slot = table_add(A.s, A.s, gp, len, wl, wh, h, 0, A.kv, A.pos, A.mask, A.status, &ins);
+            const size_t slot = enc_table_add(A.s, gp, len, wl, wh, h, A.kv, A.pos, A.mask, A.status, &ins);
             inserted += ins;
             rec = slot == ~(size_t)0 ? 0u : (uint32_t)slot;
         }
@@ -656,6 +802,27 @@ __device__ __forceinline__ uint32_t info_nids(unsigned long long info) {
     return (info & kOneId) ? 1u : (uint32_t)((info >> 39) & 0xffffffu);
 }
 
+// After k_encode_words: every resolved pending entry's record replaced by its ids' info (u64,
+// slot_info format), so the emit reads a pending word's ids with one gather instead of two
+// dependent ones.  One entry per thread, like the resolve.
+__global__ void __launch_bounds__(256) k_enc_finalize(unsigned long long* __restrict__ pend,
+                                                      const uint32_t* __restrict__ block_used,
+                                                      unsigned long long n_entries,
+                                                      const unsigned long long* __restrict__ slot_info, size_t cap,
+                                                      EncDict D, size_t dict_slots, unsigned* __restrict__ status) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_entries; i += stride) {
+        if ((i & (kPendBlock - 1)) >= block_used[i / kPendBlock]) continue;
+        const uint32_t rec = (uint32_t)pend[i];
+        unsigned long long info = 0;
+        if ((rec & kRecKind) == kRecDirect) info = kOneId | (rec & kRecPayload);
+        else if (rec < cap) info = slot_info[rec];
+        else if ((rec & kRecKind) == 0 && rec - cap < dict_slots) info = D.ent[rec - cap].info;
+        else atomicOr(status, 32u);   // a record naming nothing: a bug
+        pend[i] = info;
+    }
+}
+
 struct EmitArgs {
     const uint32_t* recs;
     const unsigned long long* rec_base;
@@ -666,7 +833,7 @@ struct EmitArgs {
     size_t cap;                            // word-table slots
     EncDict D;
     size_t dict_slots;
-    const unsigned long long* pend;        // resolved pending entries
+    const unsigned long long* pend;        // pending entries, finalized: each holds its word's ids' info
     const int64_t* sp_vid;
     unsigned* ticket;                      // chunks in the order workgroups take them
     unsigned long long* flags;             // per chunk: look-back state | id count
@@ -675,7 +842,7 @@ struct EmitArgs {
 
 // a record's ids in slot_info format (a one-id word carries its id)
 __device__ __forceinline__ unsigned long long rec_info(const EmitArgs& A, uint32_t rec) {
-    if ((rec & kRecKind) == kRecPend) rec = (uint32_t)A.pend[rec & kRecPayload];   // resolved in place
+    if ((rec & kRecKind) == kRecPend) return A.pend[rec & kRecPayload];   // finalized in place
     const uint32_t kind = rec & kRecKind, pl = rec & kRecPayload;
     if (kind == kRecDirect) return kOneId | pl;
     if (kind == kRecSpecial) return kOneId | (uint32_t)A.sp_vid[pl];
@@ -760,13 +927,16 @@ __device__ unsigned long long lookback(unsigned long long* flags, unsigned c, un
     return acc;
 }
 
-// One chunk per workgroup at a time: its records' ids counted (gathers issued together, kept in
+// Chunks by ticket (kEmitGroup consecutive ones each), one at a time per workgroup: its records' ids counted (gathers issued together, kept in
 // registers), its output offset by look-back, its ids assembled in LDS and stored with coalesced
 // 16-byte writes (a chunk averages ~5 K ids).  OutT uint32_t: the ids; uint16_t: np.uint16 as
 // encode.py saves them (encode.py:37), an id past 65535 reported in status (bit 128) instead of
 // wrapped.
 constexpr unsigned kEmitIds = 12288;   // ids staged per chunk (48 KB)
 constexpr int kEmitR = 16;             // records per thread held in registers: chunks of <= 4096
+// consecutive chunks a workgroup takes per ticket: one ticket per chunk would be ~0.7 M returning
+// atomics on one word, which serialise at ~88 per us (MI355X_MICROARCH.md, dequeue)
+constexpr unsigned kEmitGroup = 8;
 
 template <class OutT>
 __global__ void __launch_bounds__(256) k_enc_emit(EmitArgs A, OutT* __restrict__ out) {
@@ -789,8 +959,11 @@ __global__ void __launch_bounds__(256) k_enc_emit(EmitArgs A, OutT* __restrict__
     for (;;) {
         if (tid == 0) s_c = atomicAdd(A.ticket, 1u);
         __syncthreads();
-        const unsigned c = s_c;
-        if (c >= A.n_chunks) break;
+        const unsigned long long g0 = (unsigned long long)s_c * kEmitGroup;
+        __syncthreads();   // s_c is read by every thread before the next ticket is taken
+        if (g0 >= A.n_chunks) break;
+        const unsigned long long g1 = g0 + kEmitGroup < A.n_chunks ? g0 + kEmitGroup : A.n_chunks;
+        for (unsigned c = (unsigned)g0; c < (unsigned)g1; ++c) {
         const uint32_t m = A.rec_n[c];
         const uint32_t* __restrict__ r = A.recs + A.rec_base[c];
         if (m <= 256u * kEmitR) {
@@ -870,7 +1043,8 @@ __global__ void __launch_bounds__(256) k_enc_emit(EmitArgs A, OutT* __restrict__
                 run += rt;
             }
         }
-        __syncthreads();   // buf and s_c are reused by the next chunk
+        __syncthreads();   // buf is reused by the next chunk
+        }
     }
     if (kNarrow) {
         if (wide) s_wide = 1;
@@ -1237,7 +1411,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
         for (;;) {
             S.sp_key.reserve(cap);
             BPE_HIP(hipMemsetAsync(S.status.p, 0, 4, s));
-            hipLaunchKernelGGL(k_find_specials, dim3(grid_for((n + 15) / 16 + 1, 256)), dim3(256), 0, s, d_text, n, E,
+            hipLaunchKernelGGL(k_find_specials, dim3(std::min<unsigned>(grid_for((n + 15) / 16 + 1, 256), 4096)), dim3(256), 0, s, d_text, n, E,
                                T.first_mask.p, S.sp_key.p, S.status.p, cap);
             BPE_HIP(hipGetLastError());
             to_host(&cnt32, S.status.p, 4, s);
@@ -1333,8 +1507,16 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
     // text has ~0.15 pre-tokens per byte (at most one per byte: the retry's size)
     size_t cap = next_pow2(std::max<size_t>(1 << 16, n < (1u << 26) ? n / 16 : n / 1024));
     unsigned long long rec_cap = n < (1u << 26) ? n + 64 : n / 4 + (1u << 20);
+    // records are reserved a region per workgroup at a time: a region holds any chunk, and the
+    // regions left part-used (the last of every workgroup, a chunk-sized tail of the others) are
+    // slack the buffer carries
+    const unsigned long long rec_region =
+        std::min<unsigned long long>(1u << 18, std::max<unsigned long long>(kChunk, next_pow2(rec_cap / sgrid / 8)));
+    const unsigned long long rec_slack = (unsigned long long)sgrid * rec_region;
+    rec_cap += rec_slack + rec_cap / rec_region * kChunk;
     if (const char* e = std::getenv("BPE355_ENC_REC_CAP"))   // test knob: force the record retry
         rec_cap = std::max<unsigned long long>(1, std::strtoull(e, nullptr, 10));
+    const unsigned long long rec_cap_max = n + n / 8 + rec_slack + 64;   // one record per byte
     // pending entries: ~0.07 per byte at the bench corpus (the LDS cache's misses); a block per
     // workgroup at least twice over; when the pool is spent the scan resolves words itself
     unsigned long long pend_cap = std::max<unsigned long long>(n / 8, 2ull * sgrid * kPendBlock);
@@ -1355,6 +1537,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
     S.block_used.reserve(std::max(pend_blocks, 1u));
     S.pend_nblk.reserve(1);
     const EncDict D = T.dict();
+    unsigned long long pend_entries = 0;   // blocks handed out x kPendBlock (the last attempt's)
     BPE_REQUIRE(T.dict_slots < kRecPayload / 2, BPE_E_LIMIT, "vocab too large for the encoder's dictionary");
     for (int attempt = 0;; ++attempt) {
         BPE_REQUIRE(cap + T.dict_slots <= (size_t)kRecPayload, BPE_E_LIMIT, "too many distinct words for one encode");
@@ -1367,7 +1550,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
         BPE_HIP(hipMemsetAsync(rec_fill.p, 0, 8, s));
         BPE_HIP(hipMemsetAsync(S.pend_nblk.p, 0, 4, s));
         ScanArgs A{d_text, n, n_chunks, d_segs.p, nseg, std::getenv("BPE355_NOCACHE") ? 0 : 1, kv.p, pos.p,
-                   cap - 1, (unsigned long long)(cap / 2), fill.p, T.recs_cache.p, rec_cap, rec_fill.p,
+                   cap - 1, (unsigned long long)(cap / 2), fill.p, T.recs_cache.p, rec_cap, rec_region, rec_fill.p,
                    rec_base.p, rec_n.p, pend_blocks ? S.pend.p : nullptr, pend_blocks, S.pend_nblk.p,
                    S.block_used.p, status.p};
         hipLaunchKernelGGL(kern, dim3(sgrid), dim3(256), kStage, s, A, D);
@@ -1375,13 +1558,14 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
         unsigned nblk = 0;
         to_host(&nblk, S.pend_nblk.p, 4, s);
         nblk = std::min(nblk, pend_blocks);
+        pend_entries = (unsigned long long)nblk * kPendBlock;
         if (nblk) {   // the pending words, resolved in place
             int r_cu = 0;
             BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&r_cu, k_enc_resolve, 256, 0));
             const unsigned long long ne = (unsigned long long)nblk * kPendBlock;
             const unsigned rgrid = (unsigned)std::min<unsigned long long>(ceil_div(ne, 256),
                                                                          (unsigned long long)std::max(1, r_cu) * std::max(1, n_cu) * 8);
-            ResolveArgs RA{d_text, S.pend.p, S.block_used.p, ne, kv.p, pos.p, cap - 1, fill.p, status.p};
+            ResolveArgs RA{d_text, n, S.pend.p, S.block_used.p, ne, kv.p, pos.p, cap - 1, fill.p, status.p};
             hipLaunchKernelGGL(k_enc_resolve, dim3(rgrid), dim3(256), 0, s, RA, D);
             BPE_HIP(hipGetLastError());
         }
@@ -1395,8 +1579,8 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
             continue;
         }
         if (st & 256u) {   // more pre-tokens than guessed: one per byte at most
-            BPE_REQUIRE(rec_cap < n + 64, BPE_E_HIP, "internal error: encode records overflow");
-            rec_cap = n + 64;
+            BPE_REQUIRE(rec_cap < rec_cap_max, BPE_E_HIP, "internal error: encode records overflow");
+            rec_cap = rec_cap_max;
             continue;
         }
         break;
@@ -1413,6 +1597,16 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
                        w_off.p, w_len.p, d_nw.p);
     unsigned nw = 0;
     to_host(&nw, d_nw.p, 4, s);
+    if (std::getenv("BPE355_TRACE")) {
+        unsigned long long nrec = 0;
+        to_host(&nrec, rec_fill.p, 8, s);
+        std::vector<uint32_t> used(pend_entries / kPendBlock);
+        if (!used.empty()) to_host(used.data(), S.block_used.p, used.size() * 4, s);
+        unsigned long long npend = 0;
+        for (uint32_t u : used) npend += u;
+        std::fprintf(stderr, "[bpe355 encode] %zu bytes: %llu record slots reserved, %llu pending (%zu blocks), %u table words "
+                     "(%zu slots), dictionary %zu words\n", n, nrec, npend, used.size(), nw, cap, T.dict_words);
+    }
 
     // 3. encode each word of the table once
     DevBuf<unsigned long long>&len64 = S.len64, &idoff = S.idoff;
@@ -1437,6 +1631,15 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
     if (nw) {
         hipLaunchKernelGGL(k_encode_words, dim3(ceil_div(nw, 256)), dim3(256), 0, s, d_text, E, w_off.p,
                            w_len.p, idoff.p, w_slot.p, nw, pool.p, slot_info.p, status.p, n);
+        BPE_HIP(hipGetLastError());
+    }
+    if (pend_entries) {   // pending entries: record -> ids' info
+        int f_cu = 0;
+        BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&f_cu, k_enc_finalize, 256, 0));
+        const unsigned fgrid = (unsigned)std::min<unsigned long long>(ceil_div(pend_entries, 256),
+                                                                     (unsigned long long)std::max(1, f_cu) * std::max(1, n_cu) * 8);
+        hipLaunchKernelGGL(k_enc_finalize, dim3(fgrid), dim3(256), 0, s, S.pend.p, S.block_used.p, pend_entries,
+                           slot_info.p, cap, D, T.dict_slots, status.p);
         BPE_HIP(hipGetLastError());
     }
     // 4. ids: one pass over the records, chunk offsets by look-back
