@@ -27,3 +27,5 @@ if [ -f $ROOT/build/variants/enc_old/libbpe355.so ]; then
   BPE355_LIB=$ROOT/build/variants/enc_old/libbpe355.so timeout -k 10 300 python $ROOT/tools/enc_bench.py > $OUT/enc_old.log 2>&1
   echo "old encoder: $(tail -1 $OUT/enc_old.log)"
 fi
+BPE355_ENC_RESOLVE_CACHE=1 timeout -k 10 300 python $ROOT/tools/enc_bench.py > $OUT/enc_rescache.log 2>&1
+echo "resolve with LDS cache: $(tail -1 $OUT/enc_rescache.log)"

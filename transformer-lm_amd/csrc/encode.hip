@@ -776,18 +776,119 @@ __global__ void __launch_bounds__(256) k_enc_resolve(ResolveArgs A, EncDict D) {
     if ((threadIdx.x & 63) == 0 && inserted) atomicAdd(A.fill, inserted);
 }
 
+// The same with an LDS word cache: a workgroup takes the scan's blocks one at a time (a block
+// holds one scan workgroup's misses over ~16 chunks, where mid-frequency words recur beyond the
+// scan's small cache), and a word met again skips the dictionary and the table.
+constexpr int kResCache = 1024;
+__global__ void __launch_bounds__(256) k_enc_resolve_c(ResolveArgs A, EncDict D, unsigned n_blocks) {
+    __shared__ unsigned long long c_key[kResCache];
+    __shared__ uint64_t c_lo[kResCache], c_hi[kResCache];
+    __shared__ uint32_t c_rec[kResCache];
+    const size_t cap = A.mask + 1;
+    unsigned long long inserted = 0;
+    for (int i = threadIdx.x; i < kResCache; i += blockDim.x) c_key[i] = 0;
+    __syncthreads();
+    for (unsigned b = blockIdx.x; b < n_blocks; b += gridDim.x) {
+        const unsigned used = A.block_used[b];
+        const size_t base = (size_t)b * kPendBlock;
+        for (unsigned j = threadIdx.x; j < used; j += blockDim.x) {
+            const unsigned long long e = A.pend[base + j];
+            const size_t gp = (size_t)(e >> kPendShift), len = (size_t)(e & ((1ULL << kPendShift) - 1));
+            uint32_t rec = kRecNone;
+            uint64_t wl = 0, wh = 0, h;
+            unsigned ls = 0;
+            const bool cacheable = len >= 2 && len <= (size_t)kInline;
+            if (len <= (size_t)kInline) {
+                load_word(A.s, A.n, gp, len, wl, wh);
+                h = short_hash(wl, wh, len);
+                if (cacheable) {
+                    ls = (unsigned)(h >> 40) & (kResCache - 2);
+                    for (int way = 0; way < 2 && rec == kRecNone; ++way) {
+                        const unsigned sl = ls + way;
+                        const unsigned long long k = c_key[sl];
+                        if (k != 0 && k != kBusy && (k >> 40) == len) {
+                            __asm__ volatile("" ::: "memory");
+                            if (c_lo[sl] == wl && c_hi[sl] == wh) rec = c_rec[sl];
+                        }
+                    }
+                    if (rec != kRecNone) {
+                        A.pend[base + j] = rec;
+                        continue;
+                    }
+                    rec = dict_find(D, wl, wh, (uint32_t)len, h);
+                    if (rec != kRecNone) rec = dict_rec(rec, cap);
+                }
+            } else {
+                h = hash_word(A.s, gp, len);
+            }
+            if (rec == kRecNone) {   // (a probe chain past kMaxProbe sets status 1: the host retries)
+                bool ins = false;
+                const size_t slot = enc_table_add(A.s, gp, len, wl, wh, h, A.kv, A.pos, A.mask, A.status, &ins);
+                inserted += ins;
+                rec = slot == ~(size_t)0 ? 0u : (uint32_t)slot;
+            }
+            if (cacheable) {
+                for (int way = 0; way < 2; ++way) {   // cache it if a way is free
+                    const unsigned sl = ls + way;
+                    if (c_key[sl] == 0 && atomicCAS(&c_key[sl], 0ULL, kBusy) == 0) {
+                        c_lo[sl] = wl;
+                        c_hi[sl] = wh;
+                        c_rec[sl] = rec;
+                        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        atomicExch(&c_key[sl], ((unsigned long long)len << 40) | 1ULL);
+                        break;
+                    }
+                }
+            }
+            A.pend[base + j] = rec;
+        }
+        if (((b - blockIdx.x) / gridDim.x) % 4 == 3) {   // a fresh cache every 4 blocks
+            __syncthreads();
+            for (int i = threadIdx.x; i < kResCache; i += blockDim.x) c_key[i] = 0;
+            __syncthreads();
+        }
+    }
+    inserted = wave_sum(inserted);
+    if ((threadIdx.x & 63) == 0 && inserted) atomicAdd(A.fill, inserted);
+}
+
 // ------------------------------------------------------------------ 3. unique words
-__global__ void k_collect(const unsigned long long* __restrict__ kv, const unsigned long long* __restrict__ pos,
-                          size_t cap, uint32_t* __restrict__ w_slot, unsigned long long* __restrict__ w_off,
-                          uint32_t* __restrict__ w_len, unsigned* __restrict__ n_words) {
-    const size_t sidx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const unsigned long long k = sidx < cap ? kv[2 * sidx] : 0ULL;
-    const unsigned w = wave_append(k != 0, n_words);
-    if (!k) return;
-    w_slot[w] = (uint32_t)sidx;
-    const bool inl = (k >> 63) != 0;   // key format: stage.h
-    w_off[w] = inl ? pos[sidx] : (k & kOff40) - 1;
-    w_len[w] = inl ? (uint32_t)((k >> 56) & 0x7f) : (uint32_t)(k >> 40);
+// Every word-table slot in use -> (slot, offset, length).  A workgroup takes kCollectPer x 256
+// slots (coalesced) and reserves its words' positions with ONE global atomic: one per wave would
+// be ~0.26 M returning atomics on one word at a 16 M-slot table, ~3 ms at ~88 per us.
+constexpr unsigned kCollectPer = 8;
+__global__ void __launch_bounds__(256) k_collect(const unsigned long long* __restrict__ kv,
+                                                 const unsigned long long* __restrict__ pos, size_t cap,
+                                                 uint32_t* __restrict__ w_slot, unsigned long long* __restrict__ w_off,
+                                                 uint32_t* __restrict__ w_len, unsigned* __restrict__ n_words) {
+    __shared__ unsigned s_n, s_base;
+    if (threadIdx.x == 0) s_n = 0;
+    const size_t s0 = (size_t)blockIdx.x * 256 * kCollectPer + threadIdx.x;
+    unsigned long long key[kCollectPer];
+    unsigned mine = 0;
+#pragma unroll
+    for (unsigned u = 0; u < kCollectPer; ++u) {
+        const size_t sl = s0 + (size_t)u * 256;
+        key[u] = sl < cap ? kv[2 * sl] : 0ULL;
+        mine += key[u] != 0;
+    }
+    __syncthreads();   // s_n initialised
+    const unsigned at = mine ? atomicAdd(&s_n, mine) : 0u;   // LDS: this thread's first position
+    __syncthreads();
+    if (threadIdx.x == 0) s_base = s_n ? atomicAdd(n_words, s_n) : 0u;
+    __syncthreads();
+    unsigned w = s_base + at;
+#pragma unroll
+    for (unsigned u = 0; u < kCollectPer; ++u) {
+        const unsigned long long k = key[u];
+        if (!k) continue;
+        const size_t sl = s0 + (size_t)u * 256;
+        const bool inl = (k >> 63) != 0;   // key format: enc_table_add
+        w_slot[w] = (uint32_t)sl;
+        w_off[w] = inl ? pos[sl] : (k & kOff40) - 1;
+        w_len[w] = inl ? (uint32_t)((k >> 56) & 0x7f) : (uint32_t)(k >> 40);
+        ++w;
+    }
 }
 
 // ------------------------------------------------------------------ 5. ids, in one pass
@@ -1566,7 +1667,15 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
             const unsigned rgrid = (unsigned)std::min<unsigned long long>(ceil_div(ne, 256),
                                                                          (unsigned long long)std::max(1, r_cu) * std::max(1, n_cu) * 8);
             ResolveArgs RA{d_text, n, S.pend.p, S.block_used.p, ne, kv.p, pos.p, cap - 1, fill.p, status.p};
-            hipLaunchKernelGGL(k_enc_resolve, dim3(rgrid), dim3(256), 0, s, RA, D);
+            const char* rc_env = std::getenv("BPE355_ENC_RESOLVE_CACHE");   // A/B knob
+            if (rc_env && rc_env[0] == '1') {
+                int c_cu = 0;
+                BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&c_cu, k_enc_resolve_c, 256, 0));
+                const unsigned cgrid = std::min<unsigned>(nblk, (unsigned)(std::max(1, c_cu) * std::max(1, n_cu)));
+                hipLaunchKernelGGL(k_enc_resolve_c, dim3(cgrid), dim3(256), 0, s, RA, D, nblk);
+            } else {
+                hipLaunchKernelGGL(k_enc_resolve, dim3(rgrid), dim3(256), 0, s, RA, D);
+            }
             BPE_HIP(hipGetLastError());
         }
         unsigned st = 0;
@@ -1593,7 +1702,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
     w_len.reserve(cap);
     d_nw.reserve(1);
     BPE_HIP(hipMemsetAsync(d_nw.p, 0, 4, s));
-    hipLaunchKernelGGL(k_collect, dim3(ceil_div(cap, 256)), dim3(256), 0, s, kv.p, pos.p, cap, w_slot.p,
+    hipLaunchKernelGGL(k_collect, dim3(ceil_div(cap, 256 * kCollectPer)), dim3(256), 0, s, kv.p, pos.p, cap, w_slot.p,
                        w_off.p, w_len.p, d_nw.p);
     unsigned nw = 0;
     to_host(&nw, d_nw.p, 4, s);
