@@ -21,11 +21,9 @@ cd /tmp && export TMPDIR=/tmp
 BPE355_TRACE=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o enc -- python $ROOT/tools/enc_bench.py > $OUT/enc_prof.log 2>&1
 rc=$?; tail -2 $OUT/enc_prof.log
 [ $rc -eq 0 ] || exit $rc
-python $ROOT/tools/rocprof_summary.py $(ls $OUT/prof/*/*kernel_stats.csv $OUT/prof/*kernel_stats.csv 2>/dev/null | head -1) > $OUT/kernel_stats.txt 2>&1
+python $ROOT/tools/rocprof_summary.py $(find $OUT/prof -name "*.db" | head -1) > $OUT/kernel_stats.txt 2>&1
 grep -E "enc|find_spec|collect|emit" $OUT/kernel_stats.txt | head -20
-if [ -f $ROOT/build/variants/enc_old/libbpe355.so ]; then
-  BPE355_LIB=$ROOT/build/variants/enc_old/libbpe355.so timeout -k 10 300 python $ROOT/tools/enc_bench.py > $OUT/enc_old.log 2>&1
-  echo "old encoder: $(tail -1 $OUT/enc_old.log)"
-fi
-BPE355_ENC_RESOLVE_CACHE=1 timeout -k 10 300 python $ROOT/tools/enc_bench.py > $OUT/enc_rescache.log 2>&1
-echo "resolve with LDS cache: $(tail -1 $OUT/enc_rescache.log)"
+for knob in BPE355_ENC_RESOLVE_CACHE=1 BPE355_ENC_FINALIZE=0; do
+  env $knob timeout -k 10 300 python $ROOT/tools/enc_bench.py > $OUT/enc_${knob%%=*}.log 2>&1
+  echo "$knob: $(tail -1 $OUT/enc_${knob%%=*}.log)"
+done

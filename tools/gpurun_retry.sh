@@ -3,7 +3,7 @@
 # no box free); a command that ran (ok, failed, timed out) is never re-run.
 # usage: tools/gpurun_retry.sh TIMEOUT 'command'
 T=$1; shift
-for attempt in 1 2 3 4 5 6 7 8; do
+for attempt in $(seq 1 ${RETRIES:-8}); do
   out=$(/usr/local/graft/bin/gpurun --timeout $T -- "$@" 2>&1)
   rc=$?
   echo "$out" | tail -25

@@ -17,10 +17,12 @@
 //      predicate per 64-byte block, and write one u32 record per pre-token, each chunk's records
 //      one dense run: a direct id (one-byte words, one-id dictionary words, via an LDS word
 //      cache), a special, a dictionary entry, or the slot of a word-table entry (the long tail).
-//   3. k_collect + k_encode_words: the word table's words get their rank-ordered merges once.
-//   4. k_enc_emit: one pass over the records -- per chunk, ids counted (gathers issued together),
-//      the chunk's output offset by decoupled look-back, ids assembled in LDS and stored with
-//      coalesced writes.
+//   3. k_collect + k_encode_words: the word table's words get their rank-ordered merges once
+//      (after step 4's resolve has inserted them).
+//   4. k_enc_resolve: the scan's pending words (LDS-cache misses) -> dictionary / word table, in
+//      a kernel with registers to spare; k_enc_finalize: their records -> their ids' info.
+//   5. k_enc_emit<count>, an exclusive scan of the chunks' id counts, k_enc_emit<write>: per
+//      chunk, ids assembled in LDS and stored with coalesced writes.
 
 #include <algorithm>
 #include <atomic>
@@ -934,16 +936,20 @@ struct EmitArgs {
     size_t cap;                            // word-table slots
     EncDict D;
     size_t dict_slots;
-    const unsigned long long* pend;        // pending entries, finalized: each holds its word's ids' info
+    const unsigned long long* pend;        // pending entries: their records, or (finalized) their ids' info
+    int finalized;
     const int64_t* sp_vid;
-    unsigned* ticket;                      // chunks in the order workgroups take them
-    unsigned long long* flags;             // per chunk: look-back state | id count
+    unsigned long long* ctot;              // per chunk: its ids (the count pass)
+    const unsigned long long* coff;        // per chunk: its first id's position (exclusive scan)
     unsigned* status;
 };
 
 // a record's ids in slot_info format (a one-id word carries its id)
 __device__ __forceinline__ unsigned long long rec_info(const EmitArgs& A, uint32_t rec) {
-    if ((rec & kRecKind) == kRecPend) return A.pend[rec & kRecPayload];   // finalized in place
+    if ((rec & kRecKind) == kRecPend) {
+        if (A.finalized) return A.pend[rec & kRecPayload];   // k_enc_finalize: the ids' info
+        rec = (uint32_t)A.pend[rec & kRecPayload];            // k_enc_resolve: the word's record
+    }
     const uint32_t kind = rec & kRecKind, pl = rec & kRecPayload;
     if (kind == kRecDirect) return kOneId | pl;
     if (kind == kRecSpecial) return kOneId | (uint32_t)A.sp_vid[pl];
@@ -983,88 +989,27 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_ws, 
     return off;
 }
 
-// Decoupled look-back (single-pass prefix over chunks): chunk c publishes its id count as an
-// aggregate, then walks back over its predecessors 64 at a time, summing aggregates until one
-// that holds an inclusive prefix, and publishes its own inclusive prefix.  State and value share
-// one 64-bit word, read and written with agent-scope atomics (coherent across the XCDs' L2s).
-// Workgroups take chunks by ticket, so every predecessor is running or done: it publishes its
-// aggregate without waiting for anyone.  Called by all 64 lanes of one wave; returns the ids of
-// the chunks before c.
-constexpr unsigned long long kLbAgg = 1ULL << 62, kLbIncl = 2ULL << 62, kLbVal = (1ULL << 62) - 1;
-
-__device__ __forceinline__ unsigned long long lb_load(const unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void lb_store(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ unsigned long long lookback(unsigned long long* flags, unsigned c, unsigned long long T) {
-    const int lane = threadIdx.x & 63;
-    if (c == 0) {
-        if (lane == 0) lb_store(flags, kLbIncl | T);
-        return 0;
-    }
-    if (lane == 0) lb_store(flags + c, kLbAgg | T);
-    unsigned long long acc = 0;
-    long long j = (long long)c - 1;   // the window [j - 63, j], nearest predecessor in lane 0
-    for (;;) {
-        const long long q = j - lane;
-        unsigned long long v = q >= 0 ? lb_load(flags + q) : kLbIncl;
-        while (__any((v >> 62) == 0)) {   // every chunk of the window has published something
-            __builtin_amdgcn_s_sleep(2);
-            if ((v >> 62) == 0) v = lb_load(flags + q);
-        }
-        const unsigned long long incl = __ballot((v >> 62) == 2);
-        if (incl) {
-            const int f = __ffsll((long long)incl) - 1;   // the nearest inclusive prefix
-            acc += wave_sum(lane <= f ? (v & kLbVal) : 0ULL);
-            break;
-        }
-        acc += wave_sum(v & kLbVal);
-        j -= 64;
-    }
-    if (lane == 0) lb_store(flags + c, kLbIncl | (acc + T));
-    return acc;
-}
-
-// Chunks by ticket (kEmitGroup consecutive ones each), one at a time per workgroup: its records' ids counted (gathers issued together, kept in
-// registers), its output offset by look-back, its ids assembled in LDS and stored with coalesced
-// 16-byte writes (a chunk averages ~5 K ids).  OutT uint32_t: the ids; uint16_t: np.uint16 as
-// encode.py saves them (encode.py:37), an id past 65535 reported in status (bit 128) instead of
-// wrapped.
+// Two passes over the chunks, no dependence between workgroups: kCount sums each chunk's ids
+// (its records' infos gathered, all loads issued together) into ctot[c]; after an exclusive scan
+// of those (coff), the write pass gathers them again -- the chunk's pending entries were just
+// read and sit in a few KB of L2 -- assembles the ids in LDS and stores them with coalesced
+// 16-byte writes at coff[c] (a chunk averages ~5 K ids).  (A one-pass form with a decoupled
+// look-back over the chunks measured slower: its look-back chains)  OutT
+// uint32_t: the ids; uint16_t: np.uint16 as encode.py saves them (encode.py:37), an id past
+// 65535 reported in status (bit 128) instead of wrapped.
 constexpr unsigned kEmitIds = 12288;   // ids staged per chunk (48 KB)
 constexpr int kEmitR = 16;             // records per thread held in registers: chunks of <= 4096
-// consecutive chunks a workgroup takes per ticket: one ticket per chunk would be ~0.7 M returning
-// atomics on one word, which serialise at ~88 per us (MI355X_MICROARCH.md, dequeue)
-constexpr unsigned kEmitGroup = 8;
 
-template <class OutT>
+template <class OutT, bool kCount>
 __global__ void __launch_bounds__(256) k_enc_emit(EmitArgs A, OutT* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) uint32_t buf[kEmitIds];
+    __shared__ __attribute__((aligned(16))) uint32_t buf[kCount ? 4 : kEmitIds];
     __shared__ uint32_t s_ws[4];
-    __shared__ unsigned s_c, s_wide;
-    __shared__ unsigned long long s_pre;
+    __shared__ unsigned s_wide;
     const int tid = threadIdx.x;
     constexpr bool kNarrow = sizeof(OutT) == 2;
     bool wide = false;
     if (tid == 0) s_wide = 0;
-    auto prefix = [&](unsigned c, uint32_t T) -> unsigned long long {
-        if (tid < 64) {
-            const unsigned long long p = lookback(A.flags, c, T);
-            if (tid == 0) s_pre = p;
-        }
-        __syncthreads();
-        return s_pre;
-    };
-    for (;;) {
-        if (tid == 0) s_c = atomicAdd(A.ticket, 1u);
-        __syncthreads();
-        const unsigned long long g0 = (unsigned long long)s_c * kEmitGroup;
-        __syncthreads();   // s_c is read by every thread before the next ticket is taken
-        if (g0 >= A.n_chunks) break;
-        const unsigned long long g1 = g0 + kEmitGroup < A.n_chunks ? g0 + kEmitGroup : A.n_chunks;
-        for (unsigned c = (unsigned)g0; c < (unsigned)g1; ++c) {
+    for (size_t c = blockIdx.x; c < A.n_chunks; c += gridDim.x) {
         const uint32_t m = A.rec_n[c];
         const uint32_t* __restrict__ r = A.recs + A.rec_base[c];
         if (m <= 256u * kEmitR) {
@@ -1078,8 +1023,10 @@ __global__ void __launch_bounds__(256) k_enc_emit(EmitArgs A, OutT* __restrict__
             for (int i = 0; i < kEmitR; ++i) sum += lo + i < hi ? info_nids(info[i]) : 0u;
             uint32_t T;
             const uint32_t toff = block_excl_scan(sum, s_ws, &T);
-            const unsigned long long P = prefix(c, T);
-            if (T <= kEmitIds) {
+            if (kCount) {
+                if (tid == 0) A.ctot[c] = T;
+            } else if (T <= kEmitIds) {
+                const unsigned long long P = A.coff[c];
                 uint32_t o = toff;
 #pragma unroll
                 for (int i = 0; i < kEmitR; ++i)
@@ -1114,7 +1061,9 @@ __global__ void __launch_bounds__(256) k_enc_emit(EmitArgs A, OutT* __restrict__
                     out[P + q] = (OutT)buf[q];
                     wide |= buf[q] > 0xffffu;
                 }
+                __syncthreads();   // buf is reused by the next chunk
             } else {   // too many ids for LDS: straight to memory
+                const unsigned long long P = A.coff[c];
                 uint32_t o = toff;
 #pragma unroll
                 for (int i = 0; i < kEmitR; ++i)
@@ -1124,13 +1073,15 @@ __global__ void __launch_bounds__(256) k_enc_emit(EmitArgs A, OutT* __restrict__
                             wide |= kNarrow && v > 0xffffu;
                         });
             }
-        } else {   // many records: rounds of 256, counted first, then re-read and written
+        } else if (kCount) {   // many records: rounds of 256
             uint32_t sum = 0;
             for (uint32_t b = 0; b < m; b += 256)
                 if (b + tid < m) sum += info_nids(rec_info(A, r[b + tid]));
             uint32_t T;
             (void)block_excl_scan(sum, s_ws, &T);
-            const unsigned long long P = prefix(c, T);
+            if (tid == 0) A.ctot[c] = T;
+        } else {
+            const unsigned long long P = A.coff[c];
             uint32_t run = 0;
             for (uint32_t b = 0; b < m; b += 256) {
                 const unsigned long long inf = b + tid < m ? rec_info(A, r[b + tid]) : 0ULL;
@@ -1144,10 +1095,8 @@ __global__ void __launch_bounds__(256) k_enc_emit(EmitArgs A, OutT* __restrict__
                 run += rt;
             }
         }
-        __syncthreads();   // buf is reused by the next chunk
-        }
     }
-    if (kNarrow) {
+    if (kNarrow && !kCount) {
         if (wide) s_wide = 1;
         __syncthreads();
         if (tid == 0 && s_wide) atomicOr(A.status, 128u);
@@ -1239,8 +1188,9 @@ struct bpe_tokenizer {
     // slot, per unique word, the id pool, the u16 output of the bulk encoder
     struct Scratch {
         bpe::DevBuf<uint32_t> rec_n, w_slot, w_len, pool, block_used;
-        bpe::DevBuf<unsigned long long> rec_base, rec_fill, flags, fill, kv, pos, w_off, len64, idoff, slot_info;
-        bpe::DevBuf<unsigned> status, d_nw, ticket, pend_nblk;
+        bpe::DevBuf<unsigned long long> rec_base, rec_fill, fill, kv, pos, w_off, len64, idoff, slot_info;
+        bpe::DevBuf<unsigned> status, d_nw, pend_nblk;
+        bpe::DevBuf<unsigned long long> ctot, coff;   // per chunk: ids, first id's position
         bpe::DevBuf<unsigned long long> pend;   // the scan's pending entries (resolved in place)
         bpe::DevBuf<bpe::Seg> segs;
         bpe::DevBuf<unsigned long long> sp_key, sp_sorted;   // special matches, (position << 16 | index)
@@ -1742,7 +1692,10 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
                            w_len.p, idoff.p, w_slot.p, nw, pool.p, slot_info.p, status.p, n);
         BPE_HIP(hipGetLastError());
     }
-    if (pend_entries) {   // pending entries: record -> ids' info
+    // A/B knob BPE355_ENC_FINALIZE=0: the emit reads the resolved records instead
+    const char* fin_env = std::getenv("BPE355_ENC_FINALIZE");
+    const bool finalize = pend_entries && !(fin_env && fin_env[0] == '0');
+    if (finalize) {   // pending entries: record -> ids' info
         int f_cu = 0;
         BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&f_cu, k_enc_finalize, 256, 0));
         const unsigned fgrid = (unsigned)std::min<unsigned long long>(ceil_div(pend_entries, 256),
@@ -1751,32 +1704,40 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
                            slot_info.p, cap, D, T.dict_slots, status.p);
         BPE_HIP(hipGetLastError());
     }
-    // 4. ids: one pass over the records, chunk offsets by look-back
-    DevBuf<unsigned long long>& flags = S.flags;
-    DevBuf<unsigned>& ticket = S.ticket;
-    flags.reserve(n_chunks);
-    ticket.reserve(1);
-    BPE_HIP(hipMemsetAsync(flags.p, 0, n_chunks * 8, s));
-    BPE_HIP(hipMemsetAsync(ticket.p, 0, 4, s));
-    auto ekern = k_enc_emit<OutT>;
-    int e_cu = 0;
-    BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&e_cu, ekern, 256, 0));
-    const unsigned egrid = (unsigned)std::min<size_t>(n_chunks, (size_t)std::max(1, e_cu) * std::max(1, n_cu));
+    // 4. ids: the chunks' id counts, their exclusive scan, then the write pass
+    DevBuf<unsigned long long>&ctot = S.ctot, &coff = S.coff;
+    ctot.reserve(n_chunks);
+    coff.reserve(n_chunks);
     EmitArgs EA{T.recs_cache.p, rec_base.p, rec_n.p, n_chunks, slot_info.p, pool.p, cap, D, T.dict_slots,
-                S.pend.p, E.sp_vid, ticket.p, flags.p, status.p};
-    hipLaunchKernelGGL(ekern, dim3(egrid), dim3(256), 0, s, EA, d_out);
-    BPE_HIP(hipGetLastError());
-    unsigned long long last_flag = 0;
+                S.pend.p, finalize ? 1 : 0, E.sp_vid, ctot.p, coff.p, status.p};
+    {
+        auto ck = k_enc_emit<OutT, true>;
+        int c_cu = 0;
+        BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&c_cu, ck, 256, 0));
+        const unsigned cgrid = (unsigned)std::min<size_t>(n_chunks, (size_t)std::max(1, c_cu) * std::max(1, n_cu) * 2);
+        hipLaunchKernelGGL(ck, dim3(cgrid), dim3(256), 0, s, EA, d_out);
+        BPE_HIP(hipGetLastError());
+    }
+    exclusive_sum(ctot.p, coff.p, n_chunks, s, &S.tmp);
+    {
+        auto wk = k_enc_emit<OutT, false>;
+        int w_cu = 0;
+        BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&w_cu, wk, 256, 0));
+        const unsigned wgrid = (unsigned)std::min<size_t>(n_chunks, (size_t)std::max(1, w_cu) * std::max(1, n_cu) * 2);
+        hipLaunchKernelGGL(wk, dim3(wgrid), dim3(256), 0, s, EA, d_out);
+        BPE_HIP(hipGetLastError());
+    }
+    unsigned long long last[2] = {0, 0};
     unsigned st = 0;
-    to_host(&last_flag, flags.p + n_chunks - 1, 8, s);
+    to_host(&last[0], coff.p + n_chunks - 1, 8, s);
+    to_host(&last[1], ctot.p + n_chunks - 1, 8, s);
     to_host(&st, status.p, 4, s);
     if (st & 4u) throw Error{BPE_E_KEY, "a merged token is not in the vocab"};
     BPE_REQUIRE(!(st & 96u), BPE_E_HIP, "internal error: encode records inconsistent (status " +
                                           std::to_string(st) + ")");
-    BPE_REQUIRE((last_flag >> 62) == 2, BPE_E_HIP, "internal error: encode look-back incomplete");
     if (sizeof(OutT) == 2)
         BPE_REQUIRE(!(st & 128u), BPE_E_LIMIT, "a token id does not fit np.uint16 (vocab larger than 65536)");
-    const size_t total = last_flag & kLbVal;
+    const size_t total = last[0] + last[1];
     BPE_REQUIRE(total <= n, BPE_E_HIP, "encode produced more ids than input bytes");
     BPE_HIP(hipStreamSynchronize(s));
     return total;
