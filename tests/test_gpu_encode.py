@@ -117,7 +117,7 @@ def test_encode_several_devices_equals_one(ranks, monkeypatch):
     {"BPE355_ENC_PEND_CAP": "40000", "BPE355_STREAM_WG": "2"},   # the pool runs out part way
     {"BPE355_NOCACHE": "1"},                                     # no LDS cache: every word pending
     {"BPE355_ENC_REC_CAP": "1000"},                              # too few records: the retry
-    {"BPE355_ENC_RESOLVE_CACHE": "1"},                           # the resolve's LDS word cache
+    {"BPE355_ENC_RESOLVE_CACHE": "0"},                           # the resolve without its LDS cache
     {"BPE355_ENC_FINALIZE": "0"},                                # the emit reads resolved records
 ])
 def test_encode_resolution_paths(monkeypatch, knobs):

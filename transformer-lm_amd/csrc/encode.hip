@@ -287,28 +287,32 @@ __global__ void k_sp_emit(const unsigned long long* __restrict__ keys, size_t me
 }
 
 // ------------------------------------------------------------------ 2. the scan: one record per pre-token
-// Records.  Every pre-token becomes one u32; the top two bits say what it names:
-//   kRecDirect | id    a word of exactly one vocab id: one-byte words (the byte table) and the
-//                      dictionary's one-id words
-//   kRecSpecial | k    special token k (one id)
-//   kRecPend | pw      (scan output only) a word the scan left to k_enc_resolve: pending entry pw,
-//                      which the resolve overwrites with the word's final record
-//   slot               kind 0: a word-table slot (slot < cap: a word first met in this text,
-//                      encoded after the scan by k_encode_words), or cap + a dictionary slot (a
-//                      dictionary word of several ids, or none)
+// Records.  Every pre-token becomes one u32; its top bits say what it names:
+//   0 | pw                (scan output only) a word the scan left to k_enc_resolve: pending entry
+//                         pw (31 bits), which the resolve overwrites with the word's final record
+//   kRecDirect | id       11: a word of exactly one vocab id (< 2^30): one-byte words (the byte
+//                         table) and the dictionary's one-id words
+//   kRecSpecial | k       101: special token k
+//   kRecSlot | p          100: p < cap: a word-table slot (a word first met in this text, encoded
+//                         after the scan by k_encode_words); cap + s: dictionary slot s (a word of
+//                         several ids, or none)
 // The dictionary (built once per tokenizer, build_dictionary) holds every vocab entry of 2..16
 // bytes with its encoding: a pre-token's ids depend only on its bytes (tokenizer.py:124-136), so
 // a word found there needs no word-table entry.  The scan itself touches no global table: a word
 // its LDS cache does not hold becomes a pending entry (its position and length, 8 bytes), and a
 // separate kernel with registers to spare resolves all of them with many lookups in flight --
 // the dictionary (2 MB, L2-resident) first, then the word table.
-constexpr uint32_t kRecKind = 0xC0000000u;
+constexpr uint32_t kRecPendBit = 0x80000000u;   // clear: a pending entry
 constexpr uint32_t kRecDirect = 0xC0000000u;
-constexpr uint32_t kRecSpecial = 0x80000000u;
-constexpr uint32_t kRecPend = 0x40000000u;
-constexpr uint32_t kRecPayload = 0x3FFFFFFFu;   // ids, slots and pending indices are below this
+constexpr uint32_t kRecSpecial = 0xA0000000u;
+constexpr uint32_t kRecSlot = 0x80000000u;
+constexpr uint32_t kRecKind3 = 0xE0000000u;     // the kind of a special / slot record
+constexpr uint32_t kRecPayload = 0x3FFFFFFFu;   // direct ids are below this
+constexpr uint32_t kRecPayload29 = 0x1FFFFFFFu; // slots and special indices
+constexpr uint32_t kRecPendMax = 0x7FFFFFFFu;   // pending entries are below this
 constexpr uint32_t kRecNone = 0xFFFFFFFFu;      // byte table / dictionary lookup: no record
 constexpr uint32_t kDictMark = 0x40000000u;     // DictEnt.rec of a several-id word: kDictMark | slot
+__device__ __forceinline__ bool rec_is_direct(uint32_t r) { return (r & kRecDirect) == kRecDirect; }
 
 struct DictEnt {               // 32 bytes: one probe is one aligned 32-byte read
     uint64_t lo, hi;           // packed bytes
@@ -440,7 +444,7 @@ constexpr int kPendShift = 24;        // pending entry: position << 24 | length 
 
 // a dictionary record as the emit reads it: several-id words are cap + their dictionary slot
 __device__ __forceinline__ uint32_t dict_rec(uint32_t rec, size_t cap) {
-    return (rec & kRecKind) == kDictMark ? (uint32_t)(cap + (rec & kRecPayload)) : rec;
+    return (rec & kRecDirect) == kDictMark ? kRecSlot | (uint32_t)(cap + (rec & kRecPayload)) : rec;
 }
 
 // Persistent workgroups stream 16 KiB chunks through LDS (stage2.h).  Every thread turns its
@@ -496,7 +500,7 @@ __global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan4(ScanArgs 
         bool ins = false;
         const size_t slot = enc_table_add(s, gp, len, wl, wh, h, A.kv, A.pos, A.mask, A.status, &ins);
         inserted += ins;
-        return slot == ~(size_t)0 ? 0u : (uint32_t)slot;
+        return kRecSlot | (slot == ~(size_t)0 ? 0u : (uint32_t)slot);
     };
     // a word left to k_enc_resolve, or resolved here when the pool is spent
     auto pending = [&](size_t len, size_t gp, uint64_t wl, uint64_t wh, bool packed) -> uint32_t {
@@ -505,7 +509,7 @@ __global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan4(ScanArgs 
             const unsigned idx = atomicAdd(&s_pused, 1u);   // < kPendBlock: reserved per chunk
             const unsigned long long pw = (unsigned long long)pb * kPendBlock + idx;
             A.pend[pw] = ((unsigned long long)gp << kPendShift) | len;
-            return kRecPend | (uint32_t)pw;
+            return (uint32_t)pw;   // a pending record: bit 31 clear
         }
         if (!packed && len <= (size_t)kInline) pack_word(s, gp, len, wl, wh);
         const uint64_t h = len <= (size_t)kInline ? short_hash(wl, wh, len) : hash_word(s, gp, len);
@@ -688,7 +692,7 @@ __global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan4(ScanArgs 
                             if (lim != sg.end && e + 4 > lim) e = token_end(s, (size_t)sg.end, gp);
                         }
                     }
-                    if (e <= gp) { atomicOr(A.status, 16u); rec = 0; }
+                    if (e <= gp) { atomicOr(A.status, 16u); rec = kRecSlot; }
                     else {
                         const size_t len = e - gp;
                         if (len == 1) {
@@ -698,7 +702,7 @@ __global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan4(ScanArgs 
                             rec = short_rec(r, len, gp);
                         } else if (len >= (1ULL << kPendShift)) {
                             atomicOr(A.status, 2u);
-                            rec = 0;
+                            rec = kRecSlot;
                         } else {
                             rec = pending(len, gp, 0, 0, false);
                         }
@@ -770,7 +774,7 @@ __global__ void __launch_bounds__(256) k_enc_resolve(ResolveArgs A, EncDict D) {
             bool ins = false;
             const size_t slot = enc_table_add(A.s, gp, len, wl, wh, h, A.kv, A.pos, A.mask, A.status, &ins);
             inserted += ins;
-            rec = slot == ~(size_t)0 ? 0u : (uint32_t)slot;
+            rec = kRecSlot | (slot == ~(size_t)0 ? 0u : (uint32_t)slot);
         }
         A.pend[i] = rec;
     }
@@ -827,7 +831,7 @@ __global__ void __launch_bounds__(256) k_enc_resolve_c(ResolveArgs A, EncDict D,
                 bool ins = false;
                 const size_t slot = enc_table_add(A.s, gp, len, wl, wh, h, A.kv, A.pos, A.mask, A.status, &ins);
                 inserted += ins;
-                rec = slot == ~(size_t)0 ? 0u : (uint32_t)slot;
+                rec = kRecSlot | (slot == ~(size_t)0 ? 0u : (uint32_t)slot);
             }
             if (cacheable) {
                 for (int way = 0; way < 2; ++way) {   // cache it if a way is free
@@ -895,14 +899,22 @@ __global__ void __launch_bounds__(256) k_collect(const unsigned long long* __res
 
 // ------------------------------------------------------------------ 5. ids, in one pass
 // slot_info[slot] (k_encode_words) and a dictionary entry's info: a word's ids in one 8-byte
-// cell -- kOneId | id for a word of one id, nids << 39 | offset into an id pool for more (the
-// dictionary's pool when kDictPool is set), 0 for none (a pre-token equal to a special)
+// cell -- kOneId | id for a word of one id, kTwoIds | id1 << 31 | id0 for two (ids < 2^31),
+// nids << 38 | offset into an id pool for more (the dictionary's pool when kDictPool is set), 0
+// for none (a pre-token equal to a special)
 constexpr unsigned long long kOneId = 1ULL << 63;
-constexpr unsigned long long kDictPool = 1ULL << 38;
+constexpr unsigned long long kTwoIds = 1ULL << 62;
+constexpr unsigned long long kDictPool = 1ULL << 37;
 constexpr unsigned long long kPoolOff = kDictPool - 1;
 
+__host__ __device__ inline unsigned long long make_info(uint32_t nids, const uint32_t* ids, unsigned long long off) {
+    if (nids == 1) return kOneId | ids[0];
+    if (nids == 2 && ids[0] < 0x80000000u && ids[1] < 0x80000000u)
+        return kTwoIds | ((unsigned long long)ids[1] << 31) | ids[0];
+    return nids ? ((unsigned long long)nids << 38) | off : 0ULL;
+}
 __device__ __forceinline__ uint32_t info_nids(unsigned long long info) {
-    return (info & kOneId) ? 1u : (uint32_t)((info >> 39) & 0xffffffu);
+    return (info & kOneId) ? 1u : (info & kTwoIds) ? 2u : (uint32_t)((info >> 38) & 0xffffffu);
 }
 
 // After k_encode_words: every resolved pending entry's record replaced by its ids' info (u64,
@@ -917,10 +929,11 @@ __global__ void __launch_bounds__(256) k_enc_finalize(unsigned long long* __rest
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_entries; i += stride) {
         if ((i & (kPendBlock - 1)) >= block_used[i / kPendBlock]) continue;
         const uint32_t rec = (uint32_t)pend[i];
+        const uint32_t p = rec & kRecPayload29;
         unsigned long long info = 0;
-        if ((rec & kRecKind) == kRecDirect) info = kOneId | (rec & kRecPayload);
-        else if (rec < cap) info = slot_info[rec];
-        else if ((rec & kRecKind) == 0 && rec - cap < dict_slots) info = D.ent[rec - cap].info;
+        if (rec_is_direct(rec)) info = kOneId | (rec & kRecPayload);
+        else if ((rec & kRecKind3) == kRecSlot && p < cap) info = slot_info[p];
+        else if ((rec & kRecKind3) == kRecSlot && p - cap < dict_slots) info = D.ent[p - cap].info;
         else atomicOr(status, 32u);   // a record naming nothing: a bug
         pend[i] = info;
     }
@@ -946,15 +959,15 @@ struct EmitArgs {
 
 // a record's ids in slot_info format (a one-id word carries its id)
 __device__ __forceinline__ unsigned long long rec_info(const EmitArgs& A, uint32_t rec) {
-    if ((rec & kRecKind) == kRecPend) {
-        if (A.finalized) return A.pend[rec & kRecPayload];   // k_enc_finalize: the ids' info
-        rec = (uint32_t)A.pend[rec & kRecPayload];            // k_enc_resolve: the word's record
+    if (!(rec & kRecPendBit)) {
+        if (A.finalized) return A.pend[rec];   // k_enc_finalize: the ids' info
+        rec = (uint32_t)A.pend[rec];            // k_enc_resolve: the word's record
     }
-    const uint32_t kind = rec & kRecKind, pl = rec & kRecPayload;
-    if (kind == kRecDirect) return kOneId | pl;
-    if (kind == kRecSpecial) return kOneId | (uint32_t)A.sp_vid[pl];
-    if (rec < A.cap) return A.slot_info[rec];
-    if (kind == 0 && rec - A.cap < A.dict_slots) return A.D.ent[rec - A.cap].info;
+    if (rec_is_direct(rec)) return kOneId | (rec & kRecPayload);
+    const uint32_t p = rec & kRecPayload29;
+    if ((rec & kRecKind3) == kRecSpecial) return kOneId | (uint32_t)A.sp_vid[p];
+    if (p < A.cap) return A.slot_info[p];
+    if (p - A.cap < A.dict_slots) return A.D.ent[p - A.cap].info;
     atomicOr(A.status, 32u);   // a record naming nothing: a bug
     return 0;
 }
@@ -965,6 +978,11 @@ __device__ __forceinline__ uint32_t put_ids(const EmitArgs& A, unsigned long lon
     if (info & kOneId) {
         put(o, (uint32_t)info);
         return 1;
+    }
+    if (info & kTwoIds) {
+        put(o, (uint32_t)info & 0x7fffffffu);
+        put(o + 1, (uint32_t)(info >> 31) & 0x7fffffffu);
+        return 2;
     }
     const uint32_t nm = info_nids(info);
     const uint32_t* src = ((info & kDictPool) ? A.D.pool : A.pool) + (info & kPoolOff);
@@ -1150,7 +1168,7 @@ k_encode_words(const uint8_t* __restrict__ s, EncTables E, const unsigned long l
         if (v < 0) atomicOr(status, 4u);
         t[i] = (uint32_t)v;
     }
-    *info = m == 1 ? (kOneId | t[0]) : (((unsigned long long)m << 39) | w_idoff[w]);
+    *info = make_info(m, t, w_idoff[w]);
 }
 
 __global__ void k_word_len64(const uint32_t* __restrict__ w_len, unsigned n, unsigned long long* __restrict__ o) {
@@ -1284,9 +1302,12 @@ void build_dictionary(bpe_tokenizer& T, const std::unordered_map<std::string, ui
         const unsigned long long inf = info[i];
         std::vector<uint32_t> ids;
         if (inf & kOneId) ids.push_back((uint32_t)inf);
-        else if (inf) {
-            const uint32_t nm = (uint32_t)((inf >> 39) & 0xffffffu);
-            const size_t o = (size_t)(inf & ((1ULL << 39) - 1));
+        else if (inf & kTwoIds) {
+            ids.push_back((uint32_t)inf & 0x7fffffffu);
+            ids.push_back((uint32_t)(inf >> 31) & 0x7fffffffu);
+        } else if (inf) {
+            const uint32_t nm = (uint32_t)((inf >> 38) & 0xffffffu);
+            const size_t o = (size_t)(inf & kPoolOff);
             ids.assign(pool.begin() + o, pool.begin() + o + nm);
         }
         bool ok = true;
@@ -1310,8 +1331,8 @@ void build_dictionary(bpe_tokenizer& T, const std::unordered_map<std::string, ui
             e.info = kOneId | ids[0];
         } else {
             e.rec = kDictMark | (uint32_t)sl;
-            e.info = ids.empty() ? 0ULL : (((unsigned long long)ids.size() << 39) | kDictPool | dpool.size());
-            dpool.insert(dpool.end(), ids.begin(), ids.end());
+            e.info = make_info((uint32_t)ids.size(), ids.data(), kDictPool | dpool.size());
+            if (ids.size() > 2 || (ids.size() == 2 && !(e.info & kTwoIds))) dpool.insert(dpool.end(), ids.begin(), ids.end());
         }
         ++words;
     }
@@ -1573,7 +1594,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
     unsigned long long pend_cap = std::max<unsigned long long>(n / 8, 2ull * sgrid * kPendBlock);
     if (const char* e = std::getenv("BPE355_ENC_PEND_CAP"))   // test knob: a small pool (0: none)
         pend_cap = std::strtoull(e, nullptr, 10);
-    pend_cap = std::min<unsigned long long>(pend_cap, (unsigned long long)kRecPayload + 1 - kPendBlock);
+    pend_cap = std::min<unsigned long long>(pend_cap, (unsigned long long)kRecPendMax + 1 - kPendBlock);
     const unsigned pend_blocks = (unsigned)(pend_cap / kPendBlock);
     DevBuf<unsigned long long>&kv = S.kv, &pos = S.pos;
     DevBuf<unsigned long long>&rec_base = S.rec_base, &rec_fill = S.rec_fill, &fill = S.fill;
@@ -1589,9 +1610,9 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
     S.pend_nblk.reserve(1);
     const EncDict D = T.dict();
     unsigned long long pend_entries = 0;   // blocks handed out x kPendBlock (the last attempt's)
-    BPE_REQUIRE(T.dict_slots < kRecPayload / 2, BPE_E_LIMIT, "vocab too large for the encoder's dictionary");
+    BPE_REQUIRE(T.dict_slots < kRecPayload29 / 2, BPE_E_LIMIT, "vocab too large for the encoder's dictionary");
     for (int attempt = 0;; ++attempt) {
-        BPE_REQUIRE(cap + T.dict_slots <= (size_t)kRecPayload, BPE_E_LIMIT, "too many distinct words for one encode");
+        BPE_REQUIRE(cap + T.dict_slots <= (size_t)kRecPayload29, BPE_E_LIMIT, "too many distinct words for one encode");
         kv.reserve(2 * cap);
         pos.reserve(cap);
         T.recs_cache.reserve(rec_cap);
@@ -1617,8 +1638,10 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
             const unsigned rgrid = (unsigned)std::min<unsigned long long>(ceil_div(ne, 256),
                                                                          (unsigned long long)std::max(1, r_cu) * std::max(1, n_cu) * 8);
             ResolveArgs RA{d_text, n, S.pend.p, S.block_used.p, ne, kv.p, pos.p, cap - 1, fill.p, status.p};
-            const char* rc_env = std::getenv("BPE355_ENC_RESOLVE_CACHE");   // A/B knob
-            if (rc_env && rc_env[0] == '1') {
+            // the LDS-cached resolve (default: 195 vs 198 ms at the bench corpus, r04h); the knob's
+            // 0 runs the uncached one
+            const char* rc_env = std::getenv("BPE355_ENC_RESOLVE_CACHE");
+            if (!(rc_env && rc_env[0] == '0')) {
                 int c_cu = 0;
                 BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&c_cu, k_enc_resolve_c, 256, 0));
                 const unsigned cgrid = std::min<unsigned>(nblk, (unsigned)(std::max(1, c_cu) * std::max(1, n_cu)));
