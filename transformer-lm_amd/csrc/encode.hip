@@ -952,8 +952,8 @@ struct EmitArgs {
     const unsigned long long* pend;        // pending entries: their records, or (finalized) their ids' info
     int finalized;
     const int64_t* sp_vid;
-    unsigned long long* ctot;              // per chunk: its ids (the count pass)
-    const unsigned long long* coff;        // per chunk: its first id's position (exclusive scan)
+    unsigned long long* ctot;              // per chunk part: its ids (the count pass)
+    const unsigned long long* coff;        // per chunk part: its first id's position (exclusive scan)
     unsigned* status;
 };
 
@@ -1015,11 +1015,15 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_ws, 
 // look-back over the chunks measured slower: its look-back chains)  OutT
 // uint32_t: the ids; uint16_t: np.uint16 as encode.py saves them (encode.py:37), an id past
 // 65535 reported in status (bit 128) instead of wrapped.
-constexpr unsigned kEmitIds = 12288;   // ids staged per chunk (48 KB)
-constexpr int kEmitR = 16;             // records per thread held in registers: chunks of <= 4096
+// The passes work on PARTS of chunks (kEmitParts per chunk, the chunk's records split evenly):
+// half the registers and LDS of a whole chunk, so twice the workgroups per CU to hide the
+// gathers' latency (the write pass is latency-bound at 3 workgroups per CU).
+constexpr unsigned kEmitParts = 2;
+constexpr unsigned kEmitIds = 12288 / kEmitParts;   // ids staged per part
+constexpr int kEmitR = 16 / (int)kEmitParts;        // records per thread held in registers
 
 template <class OutT, bool kCount>
-__global__ void __launch_bounds__(256) k_enc_emit(EmitArgs A, OutT* __restrict__ out) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) k_enc_emit(EmitArgs A, OutT* __restrict__ out) {
     __shared__ __attribute__((aligned(16))) uint32_t buf[kCount ? 4 : kEmitIds];
     __shared__ uint32_t s_ws[4];
     __shared__ unsigned s_wide;
@@ -1027,9 +1031,13 @@ __global__ void __launch_bounds__(256) k_enc_emit(EmitArgs A, OutT* __restrict__
     constexpr bool kNarrow = sizeof(OutT) == 2;
     bool wide = false;
     if (tid == 0) s_wide = 0;
-    for (size_t c = blockIdx.x; c < A.n_chunks; c += gridDim.x) {
-        const uint32_t m = A.rec_n[c];
-        const uint32_t* __restrict__ r = A.recs + A.rec_base[c];
+    for (size_t c = blockIdx.x; c < A.n_chunks * kEmitParts; c += gridDim.x) {   // c: a part
+        const size_t ch = c / kEmitParts;
+        const unsigned part = (unsigned)(c % kEmitParts);
+        const uint32_t mc = A.rec_n[ch];
+        const uint32_t r0 = (uint32_t)((unsigned long long)mc * part / kEmitParts);
+        const uint32_t m = (uint32_t)((unsigned long long)mc * (part + 1) / kEmitParts) - r0;
+        const uint32_t* __restrict__ r = A.recs + A.rec_base[ch] + r0;
         if (m <= 256u * kEmitR) {
             const uint32_t R = (m + 255) >> 8;
             const uint32_t lo = tid * R, hi = lo + R < m ? lo + R : m;
@@ -1729,31 +1737,32 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
     }
     // 4. ids: the chunks' id counts, their exclusive scan, then the write pass
     DevBuf<unsigned long long>&ctot = S.ctot, &coff = S.coff;
-    ctot.reserve(n_chunks);
-    coff.reserve(n_chunks);
+    const size_t n_parts = n_chunks * kEmitParts;
+    ctot.reserve(n_parts);
+    coff.reserve(n_parts);
     EmitArgs EA{T.recs_cache.p, rec_base.p, rec_n.p, n_chunks, slot_info.p, pool.p, cap, D, T.dict_slots,
                 S.pend.p, finalize ? 1 : 0, E.sp_vid, ctot.p, coff.p, status.p};
     {
         auto ck = k_enc_emit<OutT, true>;
         int c_cu = 0;
         BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&c_cu, ck, 256, 0));
-        const unsigned cgrid = (unsigned)std::min<size_t>(n_chunks, (size_t)std::max(1, c_cu) * std::max(1, n_cu) * 2);
+        const unsigned cgrid = (unsigned)std::min<size_t>(n_parts, (size_t)std::max(1, c_cu) * std::max(1, n_cu) * 2);
         hipLaunchKernelGGL(ck, dim3(cgrid), dim3(256), 0, s, EA, d_out);
         BPE_HIP(hipGetLastError());
     }
-    exclusive_sum(ctot.p, coff.p, n_chunks, s, &S.tmp);
+    exclusive_sum(ctot.p, coff.p, n_parts, s, &S.tmp);
     {
         auto wk = k_enc_emit<OutT, false>;
         int w_cu = 0;
         BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&w_cu, wk, 256, 0));
-        const unsigned wgrid = (unsigned)std::min<size_t>(n_chunks, (size_t)std::max(1, w_cu) * std::max(1, n_cu) * 2);
+        const unsigned wgrid = (unsigned)std::min<size_t>(n_parts, (size_t)std::max(1, w_cu) * std::max(1, n_cu) * 2);
         hipLaunchKernelGGL(wk, dim3(wgrid), dim3(256), 0, s, EA, d_out);
         BPE_HIP(hipGetLastError());
     }
     unsigned long long last[2] = {0, 0};
     unsigned st = 0;
-    to_host(&last[0], coff.p + n_chunks - 1, 8, s);
-    to_host(&last[1], ctot.p + n_chunks - 1, 8, s);
+    to_host(&last[0], coff.p + n_parts - 1, 8, s);
+    to_host(&last[1], ctot.p + n_parts - 1, 8, s);
     to_host(&st, status.p, 4, s);
     if (st & 4u) throw Error{BPE_E_KEY, "a merged token is not in the vocab"};
     BPE_REQUIRE(!(st & 96u), BPE_E_HIP, "internal error: encode records inconsistent (status " +
