@@ -22,7 +22,7 @@ tok = Tokenizer(vocab, merges, ["<|endoftext|>"])
 knobs = {k: v for k, v in os.environ.items() if k.startswith("BPE355_")}
 for i in range(3):
     t0 = time.perf_counter()
-    ids = encode_file(tok, path)
+    ids = encode_file(tok, path, keep_device_buffers=True)
     dt = time.perf_counter() - t0
     print(f"{knobs} call {i}: {dt * 1e3:.0f} ms = {n / dt / 1e9:.2f} GB/s, ids {ids.size}, phases "
           f"{ {k: round(v) for k, v in last_phases_ms.items()} }", flush=True)

@@ -61,6 +61,28 @@ __device__ __noinline__ uint4 fetch_edge(const uint8_t* __restrict__ s, size_t n
     return make_uint4(d[0], d[1], d[2], d[3]);
 }
 
+// 16 bytes at p (any alignment) from the two aligned 16-byte words that cover them: every unit
+// of a window shares p's misalignment, so the word select is uniform; each aligned word is a
+// neighbour's too (an unaligned text, e.g. an encode region starting at a piece start, loads at
+// full width instead of byte by byte).  Both words lie in 16-byte units that hold a byte of
+// [p, p + 16), so within the allocation.
+__device__ __forceinline__ uint4 fetch_shifted(const uint8_t* p) {
+    const uintptr_t addr = reinterpret_cast<uintptr_t>(p);
+    const unsigned d = (unsigned)(addr & 15);
+    const uint4* a = reinterpret_cast<const uint4*>(addr - d);
+    const uint4 q0 = a[0];
+    if (d == 0) return q0;
+    const uint4 q1 = a[1];
+    const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+    const unsigned k = d >> 2, sh = (d & 3) * 8;
+    uint32_t o[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) o[i] = k == 0 ? w[i] : k == 1 ? w[i + 1] : k == 2 ? w[i + 2] : w[i + 3];
+    if (sh == 0) return make_uint4(o[0], o[1], o[2], o[3]);
+    return make_uint4((o[0] >> sh) | (o[1] << (32 - sh)), (o[1] >> sh) | (o[2] << (32 - sh)),
+                      (o[2] >> sh) | (o[3] << (32 - sh)), (o[3] >> sh) | (o[4] << (32 - sh)));
+}
+
 // the chunk window [base - kPre, base + kWin + kPost) of s[0, n): bytes before the text read '\n'
 // (tokstart.h), bytes past n read 0 (and are flagged past the end by vhi)
 template <bool kAligned>
@@ -72,6 +94,7 @@ __device__ __forceinline__ void fetch2(uint4 (&pre)[kSVec], const uint8_t* __res
         if (off >= kStage) continue;
         const long long g = (long long)base - kPre + off;
         if (kAligned && g >= 0 && (size_t)g + 16 <= n) pre[v] = *reinterpret_cast<const uint4*>(s + g);
+        else if (!kAligned && g >= 0 && (size_t)g + 16 <= n) pre[v] = fetch_shifted(s + g);
         else pre[v] = fetch_edge(s, n, g);
     }
 }
