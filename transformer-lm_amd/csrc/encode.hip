@@ -25,6 +25,7 @@
 //      chunk, ids assembled in LDS and stored with coalesced writes.
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -746,6 +747,7 @@ struct ResolveArgs {
     unsigned long long* kv;
     unsigned long long* pos;
     size_t mask;
+    unsigned long long max_fill;      // words the table takes (load 1/2) before the host retries
     unsigned long long* fill;
     unsigned* status;
 };
@@ -794,7 +796,26 @@ __global__ void __launch_bounds__(256) k_enc_resolve_c(ResolveArgs A, EncDict D,
     unsigned long long inserted = 0;
     for (int i = threadIdx.x; i < kResCache; i += blockDim.x) c_key[i] = 0;
     __syncthreads();
+    __shared__ unsigned long long s_ins;
+    __shared__ int s_full;
     for (unsigned b = blockIdx.x; b < n_blocks; b += gridDim.x) {
+        // the words this workgroup inserted so far go to the fill count; past the table's
+        // half-load the resolve stops (the host retries with a 4 x larger table)
+        const unsigned long long ins = wave_sum(inserted);
+        inserted = 0;
+        if (threadIdx.x == 0) { s_ins = 0; s_full = 0; }
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0 && ins) atomicAdd(&s_ins, ins);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned long long f = s_ins ? atomicAdd(A.fill, s_ins) + s_ins : *(volatile unsigned long long*)A.fill;
+            if (f > A.max_fill) {
+                s_full = 1;
+                atomicOr(A.status, 1u);
+            }
+        }
+        __syncthreads();
+        if (s_full) return;
         const unsigned used = A.block_used[b];
         const size_t base = (size_t)b * kPendBlock;
         for (unsigned j = threadIdx.x; j < used; j += blockDim.x) {
@@ -1585,7 +1606,11 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
         sgrid = std::max(1u, std::min(sgrid, (unsigned)std::atoi(e)));
     // first guesses: small texts have many more unique words per byte than large corpora; natural
     // text has ~0.15 pre-tokens per byte (at most one per byte: the retry's size)
-    size_t cap = next_pow2(std::max<size_t>(1 << 16, n < (1u << 26) ? n / 16 : n / 1024));
+    // word table: distinct words grow sublinearly with the text (~1.3 M in 64 MB and ~7.5 M in
+    // 11.9 GB of the OWT-like bench corpus, about n^0.35); 2.5 x that estimate keeps the load under
+    // ~0.4, and a table that fills past 1/2 anyway stops the resolve and is retried 4 x larger
+    const double est = 1.32e6 * std::pow(std::max(1.0, (double)n / (double)(1u << 26)), 0.35);
+    size_t cap = next_pow2(std::max<size_t>(1 << 16, n < (1u << 26) ? n / 16 : (size_t)(2.5 * est)));
     unsigned long long rec_cap = n < (1u << 26) ? n + 64 : n / 4 + (1u << 20);
     // records are reserved a region per workgroup at a time: a region holds any chunk, and the
     // regions left part-used (the last of every workgroup, a chunk-sized tail of the others) are
@@ -1645,7 +1670,8 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
             const unsigned long long ne = (unsigned long long)nblk * kPendBlock;
             const unsigned rgrid = (unsigned)std::min<unsigned long long>(ceil_div(ne, 256),
                                                                          (unsigned long long)std::max(1, r_cu) * std::max(1, n_cu) * 8);
-            ResolveArgs RA{d_text, n, S.pend.p, S.block_used.p, ne, kv.p, pos.p, cap - 1, fill.p, status.p};
+            ResolveArgs RA{d_text, n, S.pend.p, S.block_used.p, ne, kv.p, pos.p, cap - 1, (unsigned long long)(cap / 2),
+                           fill.p, status.p};
             // the LDS-cached resolve (default: 195 vs 198 ms at the bench corpus, r04h); the knob's
             // 0 runs the uncached one
             const char* rc_env = std::getenv("BPE355_ENC_RESOLVE_CACHE");
