@@ -1946,10 +1946,10 @@ size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint
     bool read_done = false;
     std::atomic<bool> stop{false};   // an error downstream: read no further
     std::exception_ptr read_err;
-    // reader and copier threads: fewer than the trainer's loader uses, so the encode's host side
-    // (segment table, launches, read-backs) keeps a core (measured at 11.9 GB: 4 threads each
-    // 593-648 ms per call, 8: 713-749, 16: 810-858)
-    const int io_n = (int)env_size("BPE355_ENC_IO_THREADS", 4);
+    // reader and copier threads, each (measured at 11.9 GB, r04: 8 threads 492-508 ms per call,
+    // 4 threads 1.96-2.0 s before the region encode got fast; r03, with a 430 ms encode phase: 4
+    // threads 593-648 ms, 8: 713-749, 16: 810-858)
+    const int io_n = (int)env_size("BPE355_ENC_IO_THREADS", 8);
     // experiment knob: BPE355_ENC_OVERLAP=0 reads the whole file before the first encode
     const char* ov = std::getenv("BPE355_ENC_OVERLAP");
     const bool overlap_read = !(ov && ov[0] == '0');
