@@ -23,7 +23,9 @@ rc=$?; tail -2 $OUT/enc_prof.log
 [ $rc -eq 0 ] || exit $rc
 python $ROOT/tools/rocprof_summary.py $(find $OUT/prof -name "*.db" | head -1) > $OUT/kernel_stats.txt 2>&1
 grep -E "enc|find_spec|collect|emit" $OUT/kernel_stats.txt | head -20
-for knob in BPE355_ENC_RESOLVE_CACHE=0; do
-  env $knob timeout -k 10 300 python $ROOT/tools/enc_bench.py > $OUT/enc_${knob%%=*}.log 2>&1
-  echo "$knob: $(tail -1 $OUT/enc_${knob%%=*}.log)"
+timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -d $OUT/pmc_hit -o hit -- python $ROOT/tools/enc_bench.py > $OUT/pmc_hit.log 2>&1
+rc=$?; tail -1 $OUT/pmc_hit.log; [ $rc -eq 0 ] || exit $rc
+for knob in ${KNOBS:-BPE355_ENC_FINALIZE=0}; do
+  env $knob timeout -k 10 300 python $ROOT/tools/enc_bench.py > $OUT/enc_${knob//=/_}.log 2>&1
+  echo "$knob: $(tail -1 $OUT/enc_${knob//=/_}.log)"
 done

@@ -13,14 +13,15 @@
 //   1. k_find_specials marks where a special starts (first-byte bitmap, then compare); the
 //      sorted matches become the segment table on the device (k_sp_*), or on the host when
 //      matches overlap.
-//   2. k_enc_scan3: persistent workgroups stage 16 KiB chunks in LDS, evaluate the token-start
+//   2. k_enc_scan4: persistent workgroups stage 16 KiB chunks in LDS, evaluate the token-start
 //      predicate per 64-byte block, and write one u32 record per pre-token, each chunk's records
 //      one dense run: a direct id (one-byte words, one-id dictionary words, via an LDS word
 //      cache), a special, a dictionary entry, or the slot of a word-table entry (the long tail).
 //   3. k_collect + k_encode_words: the word table's words get their rank-ordered merges once
 //      (after step 4's resolve has inserted them).
-//   4. k_enc_resolve: the scan's pending words (LDS-cache misses) -> dictionary / word table, in
-//      a kernel with registers to spare; k_enc_finalize: their records -> their ids' info.
+//   4. k_enc_resolve_c: the scan's pending words (LDS-cache misses) -> a dictionary word's ids'
+//      info, or a word-table slot, in a kernel with registers to spare; k_enc_finalize: the
+//      table words' slots -> their ids' info.
 //   5. k_enc_emit<count>, an exclusive scan of the chunks' id counts, k_enc_emit<write>: per
 //      chunk, ids assembled in LDS and stored with coalesced writes.
 
@@ -290,7 +291,8 @@ __global__ void k_sp_emit(const unsigned long long* __restrict__ keys, size_t me
 // ------------------------------------------------------------------ 2. the scan: one record per pre-token
 // Records.  Every pre-token becomes one u32; its top bits say what it names:
 //   0 | pw                (scan output only) a word the scan left to k_enc_resolve: pending entry
-//                         pw (31 bits), which the resolve overwrites with the word's final record
+//                         pw (31 bits), which the resolve overwrites with the word's ids' info
+//                         (a dictionary word) or its slot record (resolved_is_rec)
 //   kRecDirect | id       11: a word of exactly one vocab id (< 2^30): one-byte words (the byte
 //                         table) and the dictionary's one-id words
 //   kRecSpecial | k       101: special token k
@@ -314,6 +316,16 @@ constexpr uint32_t kRecPendMax = 0x7FFFFFFFu;   // pending entries are below thi
 constexpr uint32_t kRecNone = 0xFFFFFFFFu;      // byte table / dictionary lookup: no record
 constexpr uint32_t kDictMark = 0x40000000u;     // DictEnt.rec of a several-id word: kDictMark | slot
 __device__ __forceinline__ bool rec_is_direct(uint32_t r) { return (r & kRecDirect) == kRecDirect; }
+// A pending entry after the resolve holds either its word's ids' info (a dictionary word: the
+// info format of section 5, never in [2^31, 2^32)) or a record kRecSlot | slot (a word-table
+// word, whose ids exist only after k_encode_words; k_enc_finalize swaps it for the info).
+__device__ __forceinline__ bool resolved_is_rec(unsigned long long v) { return (v >> 31) == 1; }
+
+// ids' info (section 5): kOneId | id, kTwoIds | id1 << 31 | id0, nids << 38 | pool offset
+constexpr unsigned long long kOneId = 1ULL << 63;
+constexpr unsigned long long kTwoIds = 1ULL << 62;
+constexpr unsigned long long kDictPool = 1ULL << 37;
+constexpr unsigned long long kPoolOff = kDictPool - 1;
 
 struct DictEnt {               // 32 bytes: one probe is one aligned 32-byte read
     uint64_t lo, hi;           // packed bytes
@@ -326,14 +338,42 @@ struct EncDict {
     unsigned long long mask;   // slots - 1
     const uint32_t* pool;
     const uint32_t* byte_rec;  // 256 records of the one-byte words (kRecNone: through the table)
+    const uint32_t* filt;      // membership bits: a word whose bit is clear is not in the dictionary
 };
+// The dictionary's membership filter: one bit per hash value's bits 20..39 (128 KB, which stays
+// in every XCD's L2 where the 2 MB of entries do not: the resolve's table words, 63 % of the
+// pending words at the bench corpus, mostly skip the dictionary probe that would miss L2)
+constexpr int kFiltShift = 20;
+constexpr unsigned kFiltBits = 1u << 20;
+__host__ __device__ inline unsigned filt_index(uint64_t h) { return (unsigned)(h >> kFiltShift) & (kFiltBits - 1); }
+__device__ __forceinline__ bool filt_maybe(const EncDict& D, uint64_t h) {
+    const unsigned i = filt_index(h);
+    return (D.filt[i >> 5] >> (i & 31)) & 1u;
+}
 
 __device__ __forceinline__ uint32_t dict_find(const EncDict& D, uint64_t wl, uint64_t wh, uint32_t len, uint64_t h) {
+    if (!filt_maybe(D, h)) return kRecNone;
     size_t sl = h & D.mask;
     for (;;) {
         const DictEnt e = D.ent[sl];
         if (e.len == 0) return kRecNone;
         if (e.len == len && e.lo == wl && e.hi == wh) return e.rec;
+        sl = (sl + 1) & D.mask;
+    }
+}
+// the same, answering with the word's ids' info (the resolve stores it in the pending entry, so a
+// dictionary word needs nothing more after the resolve)
+__device__ __forceinline__ bool dict_find_info(const EncDict& D, uint64_t wl, uint64_t wh, uint32_t len, uint64_t h,
+                                               unsigned long long* info) {
+    if (!filt_maybe(D, h)) return false;
+    size_t sl = h & D.mask;
+    for (;;) {
+        const DictEnt e = D.ent[sl];
+        if (e.len == 0) return false;
+        if (e.len == len && e.lo == wl && e.hi == wh) {
+            *info = e.info;
+            return true;
+        }
         sl = (sl + 1) & D.mask;
     }
 }
@@ -750,36 +790,51 @@ struct ResolveArgs {
     unsigned long long max_fill;      // words the table takes (load 1/2) before the host retries
     unsigned long long* fill;
     unsigned* status;
+    unsigned long long* stats;        // BPE355_TRACE: LDS-cache hits, dictionary hits, table words; else null
 };
 
+// the resolve's counters (trace only): one atomic per wave and counter
+__device__ __forceinline__ void resolve_stats(unsigned long long* stats, unsigned long long c0, unsigned long long c1,
+                                              unsigned long long c2) {
+    if (!stats) return;
+    c0 = wave_sum(c0);
+    c1 = wave_sum(c1);
+    c2 = wave_sum(c2);
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&stats[0], c0);
+        atomicAdd(&stats[1], c1);
+        atomicAdd(&stats[2], c2);
+    }
+}
+
 __global__ void __launch_bounds__(256) k_enc_resolve(ResolveArgs A, EncDict D) {
-    const size_t cap = A.mask + 1;
-    unsigned long long inserted = 0;
+    unsigned long long inserted = 0, n_dict = 0, n_table = 0;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.n_entries; i += stride) {
         if ((i & (kPendBlock - 1)) >= A.block_used[i / kPendBlock]) continue;
         const unsigned long long e = A.pend[i];
         const size_t gp = (size_t)(e >> kPendShift), len = (size_t)(e & ((1ULL << kPendShift) - 1));
-        uint32_t rec = kRecNone;
+        unsigned long long val = 0;
+        bool found = false;
         uint64_t wl = 0, wh = 0, h;
         if (len <= (size_t)kInline) {
             load_word(A.s, A.n, gp, len, wl, wh);
             h = short_hash(wl, wh, len);
-            if (len >= 2) {
-                rec = dict_find(D, wl, wh, (uint32_t)len, h);
-                if (rec != kRecNone) rec = dict_rec(rec, cap);
-            }
+            if (len >= 2) found = dict_find_info(D, wl, wh, (uint32_t)len, h, &val);
         } else {
             h = hash_word(A.s, gp, len);
         }
-        if (rec == kRecNone) {   // (a probe chain past kMaxProbe sets status 1: the host retries)
+        n_dict += found;
+        if (!found) {   // (a probe chain past kMaxProbe sets status 1: the host retries)
             bool ins = false;
             const size_t slot = enc_table_add(A.s, gp, len, wl, wh, h, A.kv, A.pos, A.mask, A.status, &ins);
             inserted += ins;
-            rec = kRecSlot | (slot == ~(size_t)0 ? 0u : (uint32_t)slot);
+            ++n_table;
+            val = kRecSlot | (slot == ~(size_t)0 ? 0u : (uint32_t)slot);
         }
-        A.pend[i] = rec;
+        A.pend[i] = val;
     }
+    resolve_stats(A.stats, 0, n_dict, n_table);
     inserted = wave_sum(inserted);
     if ((threadIdx.x & 63) == 0 && inserted) atomicAdd(A.fill, inserted);
 }
@@ -791,9 +846,8 @@ constexpr int kResCache = 1024;
 __global__ void __launch_bounds__(256) k_enc_resolve_c(ResolveArgs A, EncDict D, unsigned n_blocks) {
     __shared__ unsigned long long c_key[kResCache];
     __shared__ uint64_t c_lo[kResCache], c_hi[kResCache];
-    __shared__ uint32_t c_rec[kResCache];
-    const size_t cap = A.mask + 1;
-    unsigned long long inserted = 0;
+    __shared__ uint32_t c_rec[kResCache];   // kRecDirect | id (a one-id dictionary word) or kRecSlot | slot
+    unsigned long long inserted = 0, n_hit = 0, n_dict = 0, n_table = 0;
     for (int i = threadIdx.x; i < kResCache; i += blockDim.x) c_key[i] = 0;
     __syncthreads();
     __shared__ unsigned long long s_ins;
@@ -821,7 +875,8 @@ __global__ void __launch_bounds__(256) k_enc_resolve_c(ResolveArgs A, EncDict D,
         for (unsigned j = threadIdx.x; j < used; j += blockDim.x) {
             const unsigned long long e = A.pend[base + j];
             const size_t gp = (size_t)(e >> kPendShift), len = (size_t)(e & ((1ULL << kPendShift) - 1));
-            uint32_t rec = kRecNone;
+            unsigned long long val = 0;   // the dictionary word's info, or the table word's record
+            bool found = false;
             uint64_t wl = 0, wh = 0, h;
             unsigned ls = 0;
             const bool cacheable = len >= 2 && len <= (size_t)kInline;
@@ -830,44 +885,53 @@ __global__ void __launch_bounds__(256) k_enc_resolve_c(ResolveArgs A, EncDict D,
                 h = short_hash(wl, wh, len);
                 if (cacheable) {
                     ls = (unsigned)(h >> 40) & (kResCache - 2);
-                    for (int way = 0; way < 2 && rec == kRecNone; ++way) {
+                    for (int way = 0; way < 2 && !found; ++way) {
                         const unsigned sl = ls + way;
                         const unsigned long long k = c_key[sl];
                         if (k != 0 && k != kBusy && (k >> 40) == len) {
                             __asm__ volatile("" ::: "memory");
-                            if (c_lo[sl] == wl && c_hi[sl] == wh) rec = c_rec[sl];
+                            if (c_lo[sl] == wl && c_hi[sl] == wh) {
+                                const uint32_t r = c_rec[sl];
+                                val = rec_is_direct(r) ? kOneId | (r & kRecPayload) : r;
+                                found = true;
+                            }
                         }
                     }
-                    if (rec != kRecNone) {
-                        A.pend[base + j] = rec;
+                    if (found) {
+                        ++n_hit;
+                        A.pend[base + j] = val;
                         continue;
                     }
-                    rec = dict_find(D, wl, wh, (uint32_t)len, h);
-                    if (rec != kRecNone) rec = dict_rec(rec, cap);
+                    found = dict_find_info(D, wl, wh, (uint32_t)len, h, &val);
+                    n_dict += found;
                 }
             } else {
                 h = hash_word(A.s, gp, len);
             }
-            if (rec == kRecNone) {   // (a probe chain past kMaxProbe sets status 1: the host retries)
+            if (!found) {   // (a probe chain past kMaxProbe sets status 1: the host retries)
                 bool ins = false;
                 const size_t slot = enc_table_add(A.s, gp, len, wl, wh, h, A.kv, A.pos, A.mask, A.status, &ins);
                 inserted += ins;
-                rec = kRecSlot | (slot == ~(size_t)0 ? 0u : (uint32_t)slot);
+                ++n_table;
+                val = kRecSlot | (slot == ~(size_t)0 ? 0u : (uint32_t)slot);
             }
-            if (cacheable) {
-                for (int way = 0; way < 2; ++way) {   // cache it if a way is free
+            // cache it if a way is free (a table word's slot or a one-id word's id; a dictionary
+            // word of several ids, rare, is not cached)
+            const bool one = (val & kOneId) && (uint32_t)val < kRecPayload;
+            if (cacheable && (one || resolved_is_rec(val))) {
+                for (int way = 0; way < 2; ++way) {
                     const unsigned sl = ls + way;
                     if (c_key[sl] == 0 && atomicCAS(&c_key[sl], 0ULL, kBusy) == 0) {
                         c_lo[sl] = wl;
                         c_hi[sl] = wh;
-                        c_rec[sl] = rec;
+                        c_rec[sl] = one ? kRecDirect | (uint32_t)val : (uint32_t)val;
                         __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                         atomicExch(&c_key[sl], ((unsigned long long)len << 40) | 1ULL);
                         break;
                     }
                 }
             }
-            A.pend[base + j] = rec;
+            A.pend[base + j] = val;
         }
         if (((b - blockIdx.x) / gridDim.x) % 4 == 3) {   // a fresh cache every 4 blocks
             __syncthreads();
@@ -875,6 +939,7 @@ __global__ void __launch_bounds__(256) k_enc_resolve_c(ResolveArgs A, EncDict D,
             __syncthreads();
         }
     }
+    resolve_stats(A.stats, n_hit, n_dict, n_table);
     inserted = wave_sum(inserted);
     if ((threadIdx.x & 63) == 0 && inserted) atomicAdd(A.fill, inserted);
 }
@@ -923,10 +988,6 @@ __global__ void __launch_bounds__(256) k_collect(const unsigned long long* __res
 // cell -- kOneId | id for a word of one id, kTwoIds | id1 << 31 | id0 for two (ids < 2^31),
 // nids << 38 | offset into an id pool for more (the dictionary's pool when kDictPool is set), 0
 // for none (a pre-token equal to a special)
-constexpr unsigned long long kOneId = 1ULL << 63;
-constexpr unsigned long long kTwoIds = 1ULL << 62;
-constexpr unsigned long long kDictPool = 1ULL << 37;
-constexpr unsigned long long kPoolOff = kDictPool - 1;
 
 __host__ __device__ inline unsigned long long make_info(uint32_t nids, const uint32_t* ids, unsigned long long off) {
     if (nids == 1) return kOneId | ids[0];
@@ -949,7 +1010,9 @@ __global__ void __launch_bounds__(256) k_enc_finalize(unsigned long long* __rest
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_entries; i += stride) {
         if ((i & (kPendBlock - 1)) >= block_used[i / kPendBlock]) continue;
-        const uint32_t rec = (uint32_t)pend[i];
+        const unsigned long long v = pend[i];
+        if (!resolved_is_rec(v)) continue;   // a dictionary word's info already
+        const uint32_t rec = (uint32_t)v;
         const uint32_t p = rec & kRecPayload29;
         unsigned long long info = 0;
         if (rec_is_direct(rec)) info = kOneId | (rec & kRecPayload);
@@ -981,8 +1044,9 @@ struct EmitArgs {
 // a record's ids in slot_info format (a one-id word carries its id)
 __device__ __forceinline__ unsigned long long rec_info(const EmitArgs& A, uint32_t rec) {
     if (!(rec & kRecPendBit)) {
-        if (A.finalized) return A.pend[rec];   // k_enc_finalize: the ids' info
-        rec = (uint32_t)A.pend[rec];            // k_enc_resolve: the word's record
+        const unsigned long long v = A.pend[rec];
+        if (A.finalized || !resolved_is_rec(v)) return v;   // the ids' info (finalize or the resolve)
+        rec = (uint32_t)v;                                  // k_enc_resolve: a table word's record
     }
     if (rec_is_direct(rec)) return kOneId | (rec & kRecPayload);
     const uint32_t p = rec & kRecPayload29;
@@ -1225,7 +1289,7 @@ struct bpe_tokenizer {
     // the encoder's dictionary (build_dictionary): every vocab entry of 2..16 bytes with its ids,
     // the one-byte words' records
     bpe::DevBuf<bpe::DictEnt> dict_ent;
-    bpe::DevBuf<uint32_t> dict_pool, byte_rec;
+    bpe::DevBuf<uint32_t> dict_pool, byte_rec, dict_filt;
     size_t dict_slots = 0, dict_words = 0;
     // the per-pre-token record buffer, kept for the next call: freeing and re-allocating tens of
     // GB per call costs up to seconds in the driver (measured 0.5 -> 2.8 s for an 11.9 GB
@@ -1238,6 +1302,7 @@ struct bpe_tokenizer {
         bpe::DevBuf<unsigned long long> rec_base, rec_fill, fill, kv, pos, w_off, len64, idoff, slot_info;
         bpe::DevBuf<unsigned> status, d_nw, pend_nblk;
         bpe::DevBuf<unsigned long long> ctot, coff;   // per chunk: ids, first id's position
+        bpe::DevBuf<unsigned long long> rstats;       // the resolve's counters (BPE355_TRACE)
         bpe::DevBuf<unsigned long long> pend;   // the scan's pending entries (resolved in place)
         bpe::DevBuf<bpe::Seg> segs;
         bpe::DevBuf<unsigned long long> sp_key, sp_sorted;   // special matches, (position << 16 | index)
@@ -1263,7 +1328,7 @@ struct bpe_tokenizer {
                               (int)specials.size()};
     }
     bpe::EncDict dict() const {
-        return bpe::EncDict{dict_ent.p, (unsigned long long)(dict_slots - 1), dict_pool.p, byte_rec.p};
+        return bpe::EncDict{dict_ent.p, (unsigned long long)(dict_slots - 1), dict_pool.p, byte_rec.p, dict_filt.p};
     }
 };
 
@@ -1379,6 +1444,14 @@ void build_dictionary(bpe_tokenizer& T, const std::unordered_map<std::string, ui
     if (!dpool.empty()) to_device(T.dict_pool.p, dpool.data(), dpool.size() * 4, T.stream);
     T.byte_rec.alloc(256);
     to_device(T.byte_rec.p, brec.data(), 256 * 4, T.stream);
+    std::vector<uint32_t> filt(kFiltBits / 32, 0u);
+    for (const DictEnt& e : ent)
+        if (e.len) {
+            const unsigned i = filt_index(short_hash(e.lo, e.hi, e.len));
+            filt[i >> 5] |= 1u << (i & 31);
+        }
+    T.dict_filt.alloc(filt.size());
+    to_device(T.dict_filt.p, filt.data(), filt.size() * 4, T.stream);
     BPE_HIP(hipStreamSynchronize(T.stream));
 }
 
@@ -1611,6 +1684,8 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
     // ~0.4, and a table that fills past 1/2 anyway stops the resolve and is retried 4 x larger
     const double est = 1.32e6 * std::pow(std::max(1.0, (double)n / (double)(1u << 26)), 0.35);
     size_t cap = next_pow2(std::max<size_t>(1 << 16, n < (1u << 26) ? n / 16 : (size_t)(2.5 * est)));
+    if (const char* e = std::getenv("BPE355_ENC_TABLE_SLOTS"))   // A/B knob: the first table's slots
+        cap = next_pow2(std::max<size_t>(1 << 16, std::strtoull(e, nullptr, 10)));
     unsigned long long rec_cap = n < (1u << 26) ? n + 64 : n / 4 + (1u << 20);
     // records are reserved a region per workgroup at a time: a region holds any chunk, and the
     // regions left part-used (the last of every workgroup, a chunk-sized tail of the others) are
@@ -1642,6 +1717,8 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
     S.block_used.reserve(std::max(pend_blocks, 1u));
     S.pend_nblk.reserve(1);
     const EncDict D = T.dict();
+    const bool tracing = std::getenv("BPE355_TRACE") != nullptr;
+    if (tracing) S.rstats.reserve(3);
     unsigned long long pend_entries = 0;   // blocks handed out x kPendBlock (the last attempt's)
     BPE_REQUIRE(T.dict_slots < kRecPayload29 / 2, BPE_E_LIMIT, "vocab too large for the encoder's dictionary");
     for (int attempt = 0;; ++attempt) {
@@ -1664,6 +1741,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
         to_host(&nblk, S.pend_nblk.p, 4, s);
         nblk = std::min(nblk, pend_blocks);
         pend_entries = (unsigned long long)nblk * kPendBlock;
+        if (tracing) BPE_HIP(hipMemsetAsync(S.rstats.p, 0, 3 * sizeof(unsigned long long), s));
         if (nblk) {   // the pending words, resolved in place
             int r_cu = 0;
             BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&r_cu, k_enc_resolve, 256, 0));
@@ -1671,7 +1749,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
             const unsigned rgrid = (unsigned)std::min<unsigned long long>(ceil_div(ne, 256),
                                                                          (unsigned long long)std::max(1, r_cu) * std::max(1, n_cu) * 8);
             ResolveArgs RA{d_text, n, S.pend.p, S.block_used.p, ne, kv.p, pos.p, cap - 1, (unsigned long long)(cap / 2),
-                           fill.p, status.p};
+                           fill.p, status.p, tracing ? S.rstats.p : nullptr};
             // the LDS-cached resolve (default: 195 vs 198 ms at the bench corpus, r04h); the knob's
             // 0 runs the uncached one
             const char* rc_env = std::getenv("BPE355_ENC_RESOLVE_CACHE");
@@ -1713,9 +1791,12 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
                        w_off.p, w_len.p, d_nw.p);
     unsigned nw = 0;
     to_host(&nw, d_nw.p, 4, s);
-    if (std::getenv("BPE355_TRACE")) {
-        unsigned long long nrec = 0;
+    if (tracing) {
+        unsigned long long nrec = 0, rs[3];
         to_host(&nrec, rec_fill.p, 8, s);
+        to_host(rs, S.rstats.p, sizeof rs, s);
+        std::fprintf(stderr, "[bpe355 encode] resolve: %llu LDS-cache hits, %llu dictionary words, %llu table words\n",
+                     rs[0], rs[1], rs[2]);
         std::vector<uint32_t> used(pend_entries / kPendBlock);
         if (!used.empty()) to_host(used.data(), S.block_used.p, used.size() * 4, s);
         unsigned long long npend = 0;
@@ -1929,9 +2010,12 @@ size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint
     const hipStream_t s = T.stream;
     const size_t n = src.size;
     if (n == 0) return 0;
+    const auto t_call = clk::now();
     const size_t read_slab = std::max<size_t>(1, env_size("BPE355_READ_SLAB", kReadSlab) >> 16) << 16;
     const size_t max_region = env_size("BPE355_ENC_REGION", kMaxRegion);
-    // per-region lines (range, ids, pieces, ms) appended to the file BPE355_ENC_TRACE names
+    // per-region lines (range, ids, pieces, ms; then the call's clock in ms at: the slab seen, its
+    // validation + counting done, the encode done) appended to the file BPE355_ENC_TRACE names,
+    // and one line per slab read and per copy (start, end)
     const char* trace_path = std::getenv("BPE355_ENC_TRACE");
     FILE* const trace = trace_path ? std::fopen(trace_path, "a") : nullptr;
     struct Closer { FILE* f; ~Closer() { if (f) std::fclose(f); } } trace_closer{trace};
@@ -1963,7 +2047,12 @@ size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint
                 const size_t len = std::min(read_slab, n - off);
                 if (fail_at && off + len >= fail_at)
                     throw Error{BPE_E_IO, "read failed (injected by BPE355_TEST_READ_FAIL_AT)"};
+                const double r0 = since(t_call);
                 stage_to_device(src, off, len, text + off, dev, io_n);
+                if (trace) {
+                    std::lock_guard<std::mutex> g(m);
+                    std::fprintf(trace, "read %zu %zu at %.1f %.1f\n", off, off + len, r0, since(t_call));
+                }
                 std::lock_guard<std::mutex> g(m);
                 loaded = off + len;
                 cv.notify_all();
@@ -1995,6 +2084,11 @@ size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint
                 copy_err = std::current_exception();
             }
             ph[3] += since(t0);
+            if (trace) {
+                std::lock_guard<std::mutex> g(m);
+                std::fprintf(trace, "copy %zu ids at %.1f %.1f\n", cnt, std::chrono::duration<double, std::milli>(t0 - t_call).count(),
+                             since(t_call));
+            }
         });
     };
     auto finish_threads = [&] {
@@ -2026,6 +2120,7 @@ size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint
             }
             seen = L;
             const auto t1 = clk::now();
+            const double t_seen = since(t_call);
             const size_t vend = V.prefix(L);
             const size_t cend = L == n ? n : L / 65536 * 65536;
             if (cend > counted) {
@@ -2036,6 +2131,7 @@ size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint
             bool cr = false;
             V.finish(&err, &cr);
             ph[1] += since(t1);
+            const double t_valid = since(t_call);
             if (err != ~0ULL)
                 throw Error{BPE_E_UTF8, "'utf-8' codec can't decode byte at position " + std::to_string(err)};
             if (cr) { serial = true; break; }
@@ -2061,8 +2157,9 @@ size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint
                 const double ems = since(t2);
                 ph[2] += ems;
                 if (trace) {
-                    std::fprintf(trace, "region %zu %zu ids %zu pieces %zu ms %.1f loaded %zu\n", enc_done, e_end, kk,
-                                 cuts.size() + 1, ems, seen);
+                    std::lock_guard<std::mutex> g(m);
+                    std::fprintf(trace, "region %zu %zu ids %zu pieces %zu ms %.1f loaded %zu at %.1f %.1f %.1f\n", enc_done,
+                                 e_end, kk, cuts.size() + 1, ems, seen, t_seen, t_valid, since(t_call));
                     std::fflush(trace);
                 }
                 BPE_REQUIRE(k_done + kk <= cap, BPE_E_ARG, "ids_out holds " + std::to_string(cap) +
