@@ -119,6 +119,7 @@ def test_encode_several_devices_equals_one(ranks, monkeypatch):
     {"BPE355_ENC_REC_CAP": "1000"},                              # too few records: the retry
     {"BPE355_ENC_RESOLVE_CACHE": "0"},                           # the resolve without its LDS cache
     {"BPE355_ENC_FINALIZE": "0"},                                # the emit reads resolved records
+    {"BPE355_ENC_FINALIZE": "2"},                                # the count pass stores the infos
 ])
 def test_encode_resolution_paths(monkeypatch, knobs):
     """the encoder's record paths against the oracle: pending entries resolved by k_enc_resolve,

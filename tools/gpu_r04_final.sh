@@ -25,7 +25,7 @@ python3 tools/rocprof_summary.py $(find $OUT/prof -name "*.db" | head -1) > $OUT
 head -16 $OUT/kernel_stats.txt
 BPE355_STATS_OUT=$OUT/c4_exchange.json timeout -k 10 400 python -u -m pytest tests/test_gpu_c4.py::test_c4_eight_ranks_words_full_owt -x -q --timeout 380 --timeout-method thread > $OUT/c4.log 2>&1 || { echo "c4 failed"; tail -20 $OUT/c4.log; exit 1; }
 cat $OUT/c4_exchange.json
-BPE355_PROBE=1 timeout -k 10 200 python -u bench.py --steps 1 --warmup 0 --no-encode --no-cpu-baseline --no-timing --no-device-resident --keep-corpus > $OUT/probe.log 2> $OUT/probe_err.log || { echo "probe failed"; tail -5 $OUT/probe_err.log; exit 1; }
+BPE355_PROBE=1 BPE355_LIB=build/variants/probe/libbpe355.so timeout -k 10 200 python -u bench.py --steps 1 --warmup 0 --no-encode --no-cpu-baseline --no-timing --no-device-resident --keep-corpus > $OUT/probe.log 2> $OUT/probe_err.log || { echo "probe failed"; tail -5 $OUT/probe_err.log; exit 1; }
 grep probe $OUT/probe_err.log | head -3
 rm -f /tmp/bpe355_bench_*
 echo done

@@ -167,6 +167,22 @@ struct DmaStreams {
     }
     hipStream_t pick(int t) const { return s[(size_t)t % s.size()]; }
 };
+
+// The copy streams of one direction on one device, created on first use and kept for the
+// process (never destroyed: streams outlive the calls that use them, and a stream torn down at
+// exit can outlive the runtime).  encode_file stages a slab and copies a region out per call of
+// stage_to_device / device_to_host; streams made and destroyed per call cost a round trip each,
+// and the two directions keep separate streams so that host-to-device and device-to-host copies
+// run side by side.
+const DmaStreams& cached_dma(int device, int dir) {
+    static std::mutex m;
+    static std::vector<DmaStreams*> made;   // index (device, dir)
+    std::lock_guard<std::mutex> g(m);
+    const size_t i = (size_t)device * 2 + (size_t)dir;
+    if (made.size() <= i) made.resize(i + 1, nullptr);
+    if (!made[i]) made[i] = new DmaStreams(device, dma_streams());
+    return *made[i];
+}
 }  // namespace
 
 // ------------------------------------------------------------------ sources
@@ -263,7 +279,7 @@ void stage_to_device(const Source& src, size_t off, size_t len, uint8_t* d_dst, 
     const int t_n = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads, chunks));
     std::atomic<size_t> next{0};
     std::vector<std::exception_ptr> errs(t_n);
-    DmaStreams dma(device, dma_streams());
+    const DmaStreams& dma = cached_dma(device, 0);
     auto work = [&](int t) {
         const hipStream_t s = dma.pick(t);
         void* buf[2] = {nullptr, nullptr};
@@ -314,7 +330,7 @@ void device_to_host(const uint8_t* d_src, size_t len, uint8_t* h_dst, int device
     const int t_n = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads, chunks));
     std::atomic<size_t> next{0};
     std::vector<std::exception_ptr> errs(t_n);
-    DmaStreams dma(device, dma_streams());
+    const DmaStreams& dma = cached_dma(device, 1);
     auto work = [&](int t) {
         const hipStream_t s = dma.pick(t);
         void* buf[2] = {nullptr, nullptr};

@@ -1033,8 +1033,9 @@ struct EmitArgs {
     size_t cap;                            // word-table slots
     EncDict D;
     size_t dict_slots;
-    const unsigned long long* pend;        // pending entries: their records, or (finalized) their ids' info
+    unsigned long long* pend;              // pending entries: their records, or (finalized) their ids' info
     int finalized;
+    int writeback;                         // the count pass stores the infos it resolves (no finalize pass)
     const int64_t* sp_vid;
     unsigned long long* ctot;              // per chunk part: its ids (the count pass)
     const unsigned long long* coff;        // per chunk part: its first id's position (exclusive scan)
@@ -1042,19 +1043,25 @@ struct EmitArgs {
 };
 
 // a record's ids in slot_info format (a one-id word carries its id)
-__device__ __forceinline__ unsigned long long rec_info(const EmitArgs& A, uint32_t rec) {
+__device__ __forceinline__ unsigned long long rec_info(const EmitArgs& A, uint32_t rec, bool wb = false) {
+    uint32_t pw = ~0u;
     if (!(rec & kRecPendBit)) {
         const unsigned long long v = A.pend[rec];
         if (A.finalized || !resolved_is_rec(v)) return v;   // the ids' info (finalize or the resolve)
+        pw = rec;
         rec = (uint32_t)v;                                  // k_enc_resolve: a table word's record
     }
-    if (rec_is_direct(rec)) return kOneId | (rec & kRecPayload);
+    unsigned long long info = 0;
     const uint32_t p = rec & kRecPayload29;
-    if ((rec & kRecKind3) == kRecSpecial) return kOneId | (uint32_t)A.sp_vid[p];
-    if (p < A.cap) return A.slot_info[p];
-    if (p - A.cap < A.dict_slots) return A.D.ent[p - A.cap].info;
-    atomicOr(A.status, 32u);   // a record naming nothing: a bug
-    return 0;
+    if (rec_is_direct(rec)) info = kOneId | (rec & kRecPayload);
+    else if ((rec & kRecKind3) == kRecSpecial) info = kOneId | (uint32_t)A.sp_vid[p];
+    else if (p < A.cap) info = A.slot_info[p];
+    else if (p - A.cap < A.dict_slots) info = A.D.ent[p - A.cap].info;
+    else atomicOr(A.status, 32u);   // a record naming nothing: a bug
+    // the count pass of the no-finalize mode: the pending entry takes its info (every record
+    // naming it stores the same value), so the write pass reads it directly
+    if (wb && pw != ~0u) A.pend[pw] = info;
+    return info;
 }
 
 // the ids of one info through put(position, id), from position o; returns how many
@@ -1128,7 +1135,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) k
             const uint32_t lo = tid * R, hi = lo + R < m ? lo + R : m;
             unsigned long long info[kEmitR];
 #pragma unroll
-            for (int i = 0; i < kEmitR; ++i) info[i] = lo + i < hi ? rec_info(A, r[lo + i]) : 0ULL;
+            for (int i = 0; i < kEmitR; ++i) info[i] = lo + i < hi ? rec_info(A, r[lo + i], kCount && A.writeback) : 0ULL;
             uint32_t sum = 0;
 #pragma unroll
             for (int i = 0; i < kEmitR; ++i) sum += lo + i < hi ? info_nids(info[i]) : 0u;
@@ -1187,7 +1194,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) k
         } else if (kCount) {   // many records: rounds of 256
             uint32_t sum = 0;
             for (uint32_t b = 0; b < m; b += 256)
-                if (b + tid < m) sum += info_nids(rec_info(A, r[b + tid]));
+                if (b + tid < m) sum += info_nids(rec_info(A, r[b + tid], A.writeback));
             uint32_t T;
             (void)block_excl_scan(sum, s_ws, &T);
             if (tid == 0) A.ctot[c] = T;
@@ -1303,6 +1310,7 @@ struct bpe_tokenizer {
         bpe::DevBuf<unsigned> status, d_nw, pend_nblk;
         bpe::DevBuf<unsigned long long> ctot, coff;   // per chunk: ids, first id's position
         bpe::DevBuf<unsigned long long> rstats;       // the resolve's counters (BPE355_TRACE)
+        bpe::PieceScratch piece;                      // encode_file's piece-start search
         bpe::DevBuf<unsigned long long> pend;   // the scan's pending entries (resolved in place)
         bpe::DevBuf<bpe::Seg> segs;
         bpe::DevBuf<unsigned long long> sp_key, sp_sorted;   // special matches, (position << 16 | index)
@@ -1830,9 +1838,12 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
                            w_len.p, idoff.p, w_slot.p, nw, pool.p, slot_info.p, status.p, n);
         BPE_HIP(hipGetLastError());
     }
-    // A/B knob BPE355_ENC_FINALIZE=0: the emit reads the resolved records instead
+    // A/B knob BPE355_ENC_FINALIZE: 0 the emit reads the resolved records instead, 2 the emit's
+    // count pass resolves them and stores the infos for the write pass
     const char* fin_env = std::getenv("BPE355_ENC_FINALIZE");
-    const bool finalize = pend_entries && !(fin_env && fin_env[0] == '0');
+    const int fin_mode = fin_env ? std::atoi(fin_env) : 1;
+    const bool finalize = pend_entries && fin_mode == 1;
+    const bool writeback = pend_entries && fin_mode == 2;
     if (finalize) {   // pending entries: record -> ids' info
         int f_cu = 0;
         BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&f_cu, k_enc_finalize, 256, 0));
@@ -1848,7 +1859,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
     ctot.reserve(n_parts);
     coff.reserve(n_parts);
     EmitArgs EA{T.recs_cache.p, rec_base.p, rec_n.p, n_chunks, slot_info.p, pool.p, cap, D, T.dict_slots,
-                S.pend.p, finalize ? 1 : 0, E.sp_vid, ctot.p, coff.p, status.p};
+                S.pend.p, finalize ? 1 : 0, writeback ? 1 : 0, E.sp_vid, ctot.p, coff.p, status.p};
     {
         auto ck = k_enc_emit<OutT, true>;
         int c_cu = 0;
@@ -1858,6 +1869,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
         BPE_HIP(hipGetLastError());
     }
     exclusive_sum(ctot.p, coff.p, n_parts, s, &S.tmp);
+    if (writeback) EA.finalized = 1;   // every pending entry holds its info now
     {
         auto wk = k_enc_emit<OutT, false>;
         int w_cu = 0;
@@ -2124,7 +2136,7 @@ size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint
             const size_t vend = V.prefix(L);
             const size_t cend = L == n ? n : L / 65536 * 65536;
             if (cend > counted) {
-                chars += piece_starts_range(text + counted, cend - counted, K, chars, counted, s, starts);
+                chars += piece_starts_range(text + counted, cend - counted, K, chars, counted, s, starts, &S.piece);
                 counted = cend;
             }
             unsigned long long err = 0;

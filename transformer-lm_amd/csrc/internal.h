@@ -41,9 +41,15 @@ const uint8_t* prepare_text(const uint8_t* d_in, size_t n, DevBuf<uint8_t>& scra
 // pieces f.read(k) returns begin (reference encode.py:31-33).
 std::vector<uint64_t> utf8_piece_starts(const uint8_t* d_text, size_t n, size_t k, hipStream_t stream);
 // The same over a range of a longer text whose first character is character c_base: appends the
-// starts found (plus `offset`) to out, returns the range's character count.
+// starts found (plus `offset`) to out, returns the range's character count.  scratch (optional)
+// keeps the device arrays across calls: a freed device buffer synchronises the whole device, which
+// in the overlapped encode_file would wait for the copies other threads have in flight.
+struct PieceScratch {
+    DevBuf<unsigned long long> cnt, first, marks;
+    DevBuf<uint8_t> tmp;
+};
 uint64_t piece_starts_range(const uint8_t* d_text, size_t n, size_t k, uint64_t c_base, uint64_t offset,
-                            hipStream_t stream, std::vector<uint64_t>& out);
+                            hipStream_t stream, std::vector<uint64_t>& out, PieceScratch* scratch = nullptr);
 
 // ---------------------------------------------------------------- unique-word count
 struct WordCounts {

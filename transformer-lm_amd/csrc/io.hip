@@ -133,13 +133,17 @@ int guarded_io(F&& f) {
 }  // namespace
 
 uint64_t piece_starts_range(const uint8_t* d_text, size_t n, size_t k, uint64_t c_base, uint64_t offset,
-                            hipStream_t s, std::vector<uint64_t>& out) {
+                            hipStream_t s, std::vector<uint64_t>& out, PieceScratch* scratch) {
     if (n == 0) return 0;
     const size_t blocks = (n + kCharBlock - 1) / kCharBlock;
-    DevBuf<unsigned long long> cnt(blocks), first(blocks);
+    PieceScratch local;
+    PieceScratch& S = scratch ? *scratch : local;
+    S.cnt.reserve(blocks);
+    S.first.reserve(blocks);
+    DevBuf<unsigned long long>&cnt = S.cnt, &first = S.first;
     hipLaunchKernelGGL(k_char_count, dim3(blocks), dim3(kCharThreads), 0, s, d_text, n, cnt.p);
     BPE_HIP(hipGetLastError());
-    exclusive_sum(cnt.p, first.p, blocks, s);
+    exclusive_sum(cnt.p, first.p, blocks, s, &S.tmp);
     unsigned long long last[2];
     to_host(&last[0], first.p + blocks - 1, 8, s);
     to_host(&last[1], cnt.p + blocks - 1, 8, s);
@@ -148,7 +152,8 @@ uint64_t piece_starts_range(const uint8_t* d_text, size_t n, size_t k, uint64_t 
     const unsigned long long mark0 = (c_base + k - 1) / k, mark1 = (c_base + chars + k - 1) / k;
     if (mark1 > mark0) {
         const size_t m = (size_t)(mark1 - mark0);
-        DevBuf<unsigned long long> marks(m);
+        S.marks.reserve(m);
+        DevBuf<unsigned long long>& marks = S.marks;
         hipLaunchKernelGGL(k_char_marks, dim3(blocks), dim3(kCharThreads), 0, s, d_text, n, first.p, cnt.p,
                            (unsigned long long)k, (unsigned long long)c_base, mark0, marks.p);
         BPE_HIP(hipGetLastError());

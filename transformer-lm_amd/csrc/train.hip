@@ -977,10 +977,11 @@ struct DeltaSinkN {
 // next trip's select start, 17-19 inside select's rule, 20/21 the last merge/apply workgroup's index
 constexpr int kProbeTrip = 8;
 constexpr int kProbeSlots = 32;   // 24-28: inside k_select's first phase
-// BPE355_PROBE_CODE=0 compiles the stamps out (code-size experiment; the default keeps them,
-// behind the run-time BPE355_PROBE switch)
+// The stamps are compiled in only with -DBPE355_PROBE_CODE=1 (tools/build_variant.sh probe; then
+// the run-time BPE355_PROBE switch turns them on).  Compiled in but off, their code and registers
+// cost 4-6 ms of the 260 ms merge phase (r04r A/B, two reps, profiles/r04/r_*).
 #ifndef BPE355_PROBE_CODE
-#define BPE355_PROBE_CODE 1
+#define BPE355_PROBE_CODE 0
 #endif
 __device__ __forceinline__ void probe_stamp(const RoundState* st, int trip, int k) {
     if (BPE355_PROBE_CODE && st->probe && (trip % kProbeTrip) == 0)
@@ -2971,7 +2972,10 @@ void MergeLoop<TokT>::run() {
     hs_.halt = HALT_REBUILD;
     hs_.max_len = std::max(max_len_, 1u);
     hs_.max_batch = max_batch_;
-    if (batched_ && std::getenv("BPE355_PROBE")) {
+    if (batched_ && std::getenv("BPE355_PROBE") && !BPE355_PROBE_CODE)
+        std::fprintf(stderr, "[bpe355 probe] BPE355_PROBE needs a library built with -DBPE355_PROBE_CODE=1 "
+                             "(tools/build_variant.sh): no stamps in this one\n");
+    if (batched_ && std::getenv("BPE355_PROBE") && BPE355_PROBE_CODE) {
         probe_.alloc((size_t)kProbeSlots * (n_rounds_ / kProbeTrip + 2));
         BPE_HIP(hipMemsetAsync(probe_.p, 0, probe_.bytes(), s_));
         hs_.probe = probe_.p;
