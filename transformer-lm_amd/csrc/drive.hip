@@ -68,6 +68,70 @@ PinnedPool& pool() {
     return *p;
 }
 
+// Device-to-host staging written by a kernel (device_to_host): coherent, device-mapped pinned
+// buffers, each with its device address.  HIP serves a device-to-host hipMemcpyAsync with a copy
+// KERNEL (__amd_rocclr_copyBuffer, 1399 launches of ~470 us in profiles/r04/n_*), whose
+// workgroups take CUs from the encode running beside it in encode_file (1 GiB region encodes went
+// from 21.6 to 43 ms while a region's ids were copied out, r04s).  A copy kernel of our own with
+// a small grid moves the same bytes over the bus from a few CUs.
+struct MappedBuf {
+    void* host = nullptr;
+    void* dev = nullptr;
+};
+struct MappedPool {
+    std::mutex m;
+    std::vector<MappedBuf> free_;
+    MappedBuf get() {
+        {
+            std::lock_guard<std::mutex> g(m);
+            if (!free_.empty()) {
+                const MappedBuf b = free_.back();
+                free_.pop_back();
+                return b;
+            }
+        }
+        MappedBuf b;
+        BPE_HIP(hipHostMalloc(&b.host, kStageChunk, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
+        const hipError_t e = hipHostGetDevicePointer(&b.dev, b.host, 0);
+        if (e != hipSuccess) {
+            (void)hipHostFree(b.host);
+            BPE_HIP(e);
+        }
+        return b;
+    }
+    void put(const MappedBuf& b) {
+        std::lock_guard<std::mutex> g(m);
+        free_.push_back(b);
+    }
+};
+MappedPool& mapped_pool() {
+    static MappedPool* p = new MappedPool;   // never freed: lives as long as the process
+    return *p;
+}
+
+// device bytes -> a mapped host buffer: 16-byte loads and stores when both ends allow
+__global__ void __launch_bounds__(256) k_to_host(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, size_t n) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if ((((uintptr_t)src | (uintptr_t)dst) & 15u) == 0) {
+        const size_t n16 = n / 16;
+        for (size_t i = t; i < n16; i += stride)
+            reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+        for (size_t i = n16 * 16 + t; i < n; i += stride) dst[i] = src[i];
+    } else {
+        for (size_t i = t; i < n; i += stride) dst[i] = src[i];
+    }
+}
+// workgroups per device-to-host chunk copy (BPE355_D2H_WG; 0: hipMemcpyAsync instead)
+int d2h_wg() {
+    static const int w = [] {
+        int n = 16;
+        if (const char* e = std::getenv("BPE355_D2H_WG")) n = std::atoi(e);
+        return std::max(0, std::min(n, 1024));
+    }();
+    return w;
+}
+
 // Device buffers for the corpus, kept across training calls (per device, checked out by one
 // call at a time): a fresh multi-GB allocation per call costs tens of ms (the driver clears it).
 struct CorpusBuf {
@@ -333,9 +397,11 @@ void device_to_host(const uint8_t* d_src, size_t len, uint8_t* h_dst, int device
     const DmaStreams& dma = cached_dma(device, 1);
     auto work = [&](int t) {
         const hipStream_t s = dma.pick(t);
+        const int wg = d2h_wg();
         void* buf[2] = {nullptr, nullptr};
+        MappedBuf mb[2];
         hipEvent_t ev[2] = {nullptr, nullptr};
-        size_t pend[2] = {~(size_t)0, ~(size_t)0};   // chunk whose DMA into buf[k] is in flight
+        size_t pend[2] = {~(size_t)0, ~(size_t)0};   // chunk whose copy into buf[k] is in flight
         auto drain = [&](int k) {
             if (pend[k] == ~(size_t)0) return;
             BPE_HIP(hipEventSynchronize(ev[k]));
@@ -346,7 +412,12 @@ void device_to_host(const uint8_t* d_src, size_t len, uint8_t* h_dst, int device
         try {
             BPE_HIP(hipSetDevice(device));
             for (int k = 0; k < 2; ++k) {
-                buf[k] = pool().get();
+                if (wg) {
+                    mb[k] = mapped_pool().get();
+                    buf[k] = mb[k].host;
+                } else {
+                    buf[k] = pool().get();
+                }
                 BPE_HIP(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
             }
             for (int k = 0;; k ^= 1) {
@@ -354,7 +425,12 @@ void device_to_host(const uint8_t* d_src, size_t len, uint8_t* h_dst, int device
                 const size_t i = next.fetch_add(1);
                 if (i >= chunks) break;
                 const size_t lo = i * kStageChunk, n = std::min(kStageChunk, len - lo);
-                BPE_HIP(hipMemcpyAsync(buf[k], d_src + lo, n, hipMemcpyDeviceToHost, s));
+                if (wg) {
+                    hipLaunchKernelGGL(k_to_host, dim3(wg), dim3(256), 0, s, d_src + lo, static_cast<uint8_t*>(mb[k].dev), n);
+                    BPE_HIP(hipGetLastError());
+                } else {
+                    BPE_HIP(hipMemcpyAsync(buf[k], d_src + lo, n, hipMemcpyDeviceToHost, s));
+                }
                 BPE_HIP(hipEventRecord(ev[k], s));
                 pend[k] = i;
             }
@@ -368,7 +444,10 @@ void device_to_host(const uint8_t* d_src, size_t len, uint8_t* h_dst, int device
         for (int k = 0; k < 2; ++k) {   // no DMA into a buffer that goes back to the pool
             if (pend[k] != ~(size_t)0) (void)hipEventSynchronize(ev[k]);
             if (ev[k]) (void)hipEventDestroy(ev[k]);
-            if (buf[k]) pool().put(buf[k]);
+            if (buf[k]) {
+                if (wg) mapped_pool().put(mb[k]);
+                else pool().put(buf[k]);
+            }
         }
     };
     std::vector<std::thread> th;

@@ -950,7 +950,11 @@ struct BatchState {
     unsigned long long k1_why[6];   // single-merge trips: P1 a == b / P1 not fresh / no list / P2 fails / tie / end
 };
 constexpr unsigned kListCap = 256;   // the candidate list k_select ranks (one thread per entry)
-constexpr unsigned kApplyGrid = 512;   // k_apply_batch workgroups (k_select reads one partial each)
+// k_apply_batch workgroups (k_select reads one partial each; build knob BPE355_APPLY_GRID)
+#ifndef BPE355_APPLY_GRID
+#define BPE355_APPLY_GRID 512
+#endif
+constexpr unsigned kApplyGrid = BPE355_APPLY_GRID;
 
 struct SelKey {   // a listed candidate as k_select's ranking reads it
     long long cnt;
@@ -1046,7 +1050,9 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
                                                         uint32_t* __restrict__ m_new, uint32_t* __restrict__ m_mode,
                                                         long long* __restrict__ m_cnt, int* __restrict__ trip_info,
                                                         int trip_slot) {
-    static_assert(kApplyGrid <= 64 * kSelListWave, "one partial per thread of the partial waves");
+    // each thread of the partial waves reduces kPartPer partials
+    constexpr int kPartPer = (int)((kApplyGrid + 64 * kSelListWave - 1) / (64 * kSelListWave));
+    static_assert(kPartPer >= 1 && kPartPer <= 4, "partials per thread of the partial waves");
     __shared__ Cand s_wave[kSelListWave];
     __shared__ Cand s_all[kListCap];
     __shared__ SelKey s_topkey[kListCap];          // the entries with fewer than kTopM larger counts,
@@ -1065,8 +1071,12 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
             st->probe[kProbeSlots * (size_t)((ptrip - 1) / kProbeTrip) + 16] = __builtin_amdgcn_s_memrealtime();
     }
     // ---- every independent load first
-    Partial q{};
-    if (wv < kSelListWave) q = part[tid];   // the buffer holds kApplyBatchBlocks entries
+    Partial q[kPartPer] = {};
+    if (wv < kSelListWave) {   // the buffer holds kApplyBatchBlocks entries
+#pragma unroll
+        for (int u = 0; u < kPartPer; ++u)
+            if (tid + u * 64 * kSelListWave < (int)kApplyGrid) q[u] = part[tid + u * 64 * kSelListWave];
+    }
     Partial lq{};
     const int li = tid - 64 * kSelListWave;   // list entry of this thread (>= 0: list waves)
     if (li >= 0) lq = list[li];
@@ -1097,7 +1107,14 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     if (tid == 0) probe_stamp(st, ptrip, 1);
     if (wv < kSelListWave) {   // P1: the exact best over the partials
         Cand best = cand_none();
-        if (tid < nparts) best = Cand{q.cnt, q.ka, q.kb, q.slot, q.a, q.b};
+#pragma unroll
+        for (int u = 0; u < kPartPer; ++u) {
+            const int idx = tid + u * 64 * kSelListWave;
+            if (idx < nparts) {
+                const Cand c{q[u].cnt, q[u].ka, q[u].kb, q[u].slot, q[u].a, q[u].b};
+                if (cand_better(c, best, K.pool, K.off, K.len)) best = c;
+            }
+        }
         for (int o = 32; o > 0; o >>= 1) {
             const Cand oc = shfl_xor_cand(best, o);
             if (cand_better(oc, best, K.pool, K.off, K.len)) best = oc;
