@@ -122,10 +122,12 @@ __global__ void __launch_bounds__(256) k_to_host(const uint8_t* __restrict__ src
         for (size_t i = t; i < n; i += stride) dst[i] = src[i];
     }
 }
-// workgroups per device-to-host chunk copy (BPE355_D2H_WG; 0: hipMemcpyAsync instead)
+// workgroups per device-to-host chunk copy by k_to_host (BPE355_D2H_WG); 0, the default:
+// hipMemcpyAsync.  16 workgroups moved encode_file's ids at ~18 GB/s against HIP's ~34 (r04u:
+// 581-670 vs 383-421 ms per 11.9 GB call), so the knob stays for A/B only.
 int d2h_wg() {
     static const int w = [] {
-        int n = 16;
+        int n = 0;
         if (const char* e = std::getenv("BPE355_D2H_WG")) n = std::atoi(e);
         return std::max(0, std::min(n, 1024));
     }();

@@ -321,10 +321,15 @@ __device__ __forceinline__ bool rec_is_direct(uint32_t r) { return (r & kRecDire
 // word, whose ids exist only after k_encode_words; k_enc_finalize swaps it for the info).
 __device__ __forceinline__ bool resolved_is_rec(unsigned long long v) { return (v >> 31) == 1; }
 
-// ids' info (section 5): kOneId | id, kTwoIds | id1 << 31 | id0, nids << 38 | pool offset
+// ids' info (section 5): kOneId | id, kTwoIds | id1 << 31 | id0, kThreeIds (ids < 2^20),
+// kFourIds (ids < 2^15), else nids << 36 | pool offset
 constexpr unsigned long long kOneId = 1ULL << 63;
 constexpr unsigned long long kTwoIds = 1ULL << 62;
-constexpr unsigned long long kDictPool = 1ULL << 37;
+constexpr unsigned long long kThreeIds = 1ULL << 61;
+constexpr unsigned long long kFourIds = 1ULL << 60;
+constexpr unsigned long long kInlineIds = kOneId | kTwoIds | kThreeIds | kFourIds;
+constexpr int kNidsShift = 36;
+constexpr unsigned long long kDictPool = 1ULL << 35;
 constexpr unsigned long long kPoolOff = kDictPool - 1;
 
 struct DictEnt {               // 32 bytes: one probe is one aligned 32-byte read
@@ -986,17 +991,41 @@ __global__ void __launch_bounds__(256) k_collect(const unsigned long long* __res
 // ------------------------------------------------------------------ 5. ids, in one pass
 // slot_info[slot] (k_encode_words) and a dictionary entry's info: a word's ids in one 8-byte
 // cell -- kOneId | id for a word of one id, kTwoIds | id1 << 31 | id0 for two (ids < 2^31),
-// nids << 38 | offset into an id pool for more (the dictionary's pool when kDictPool is set), 0
+// kThreeIds | id2 << 40 | id1 << 20 | id0 for three (ids < 2^20), kFourIds | id3 << 45 | id2 << 30 |
+// id1 << 15 | id0 for four (ids < 2^15: vocabularies up to 32768, the bench's 32000), so most
+// occurrences need no read of the id pool when their ids are written; else nids << 36 | offset
+// into an id pool (the dictionary's pool when kDictPool is set), 0
 // for none (a pre-token equal to a special)
 
 __host__ __device__ inline unsigned long long make_info(uint32_t nids, const uint32_t* ids, unsigned long long off) {
     if (nids == 1) return kOneId | ids[0];
     if (nids == 2 && ids[0] < 0x80000000u && ids[1] < 0x80000000u)
         return kTwoIds | ((unsigned long long)ids[1] << 31) | ids[0];
-    return nids ? ((unsigned long long)nids << 38) | off : 0ULL;
+    if (nids == 3 && (ids[0] | ids[1] | ids[2]) < (1u << 20))
+        return kThreeIds | ((unsigned long long)ids[2] << 40) | ((unsigned long long)ids[1] << 20) | ids[0];
+    if (nids == 4 && (ids[0] | ids[1] | ids[2] | ids[3]) < (1u << 15))
+        return kFourIds | ((unsigned long long)ids[3] << 45) | ((unsigned long long)ids[2] << 30) |
+               ((unsigned long long)ids[1] << 15) | ids[0];
+    return nids ? ((unsigned long long)nids << kNidsShift) | off : 0ULL;
 }
-__device__ __forceinline__ uint32_t info_nids(unsigned long long info) {
-    return (info & kOneId) ? 1u : (info & kTwoIds) ? 2u : (uint32_t)((info >> 38) & 0xffffffu);
+__host__ __device__ inline uint32_t info_nids(unsigned long long info) {
+    return (info & kOneId) ? 1u : (info & kTwoIds) ? 2u : (info & kThreeIds) ? 3u : (info & kFourIds) ? 4u
+                                                        : (uint32_t)((info >> kNidsShift) & 0xffffffu);
+}
+// an inline info's ids (1..4 of them; the pool format is not inline)
+__host__ __device__ inline uint32_t info_inline_ids(unsigned long long info, uint32_t* ids) {
+    if (info & kOneId) { ids[0] = (uint32_t)info; return 1; }
+    if (info & kTwoIds) {
+        ids[0] = (uint32_t)info & 0x7fffffffu;
+        ids[1] = (uint32_t)(info >> 31) & 0x7fffffffu;
+        return 2;
+    }
+    if (info & kThreeIds) {
+        for (int j = 0; j < 3; ++j) ids[j] = (uint32_t)(info >> (20 * j)) & 0xfffffu;
+        return 3;
+    }
+    for (int j = 0; j < 4; ++j) ids[j] = (uint32_t)(info >> (15 * j)) & 0x7fffu;
+    return 4;
 }
 
 // After k_encode_words: every resolved pending entry's record replaced by its ids' info (u64,
@@ -1067,14 +1096,13 @@ __device__ __forceinline__ unsigned long long rec_info(const EmitArgs& A, uint32
 // the ids of one info through put(position, id), from position o; returns how many
 template <class Put>
 __device__ __forceinline__ uint32_t put_ids(const EmitArgs& A, unsigned long long info, uint32_t o, const Put& put) {
-    if (info & kOneId) {
-        put(o, (uint32_t)info);
-        return 1;
-    }
-    if (info & kTwoIds) {
-        put(o, (uint32_t)info & 0x7fffffffu);
-        put(o + 1, (uint32_t)(info >> 31) & 0x7fffffffu);
-        return 2;
+    if (info & kInlineIds) {
+        uint32_t ids[4];
+        const uint32_t nm = info_inline_ids(info, ids);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+            if (j < nm) put(o + j, ids[j]);
+        return nm;
     }
     const uint32_t nm = info_nids(info);
     const uint32_t* src = ((info & kDictPool) ? A.D.pool : A.pool) + (info & kPoolOff);
@@ -1403,12 +1431,11 @@ void build_dictionary(bpe_tokenizer& T, const std::unordered_map<std::string, ui
     for (size_t i = 0; i < nc; ++i) {
         const unsigned long long inf = info[i];
         std::vector<uint32_t> ids;
-        if (inf & kOneId) ids.push_back((uint32_t)inf);
-        else if (inf & kTwoIds) {
-            ids.push_back((uint32_t)inf & 0x7fffffffu);
-            ids.push_back((uint32_t)(inf >> 31) & 0x7fffffffu);
+        if (inf & kInlineIds) {
+            uint32_t x[4];
+            ids.assign(x, x + info_inline_ids(inf, x));
         } else if (inf) {
-            const uint32_t nm = (uint32_t)((inf >> 38) & 0xffffffu);
+            const uint32_t nm = info_nids(inf);
             const size_t o = (size_t)(inf & kPoolOff);
             ids.assign(pool.begin() + o, pool.begin() + o + nm);
         }
@@ -1434,7 +1461,7 @@ void build_dictionary(bpe_tokenizer& T, const std::unordered_map<std::string, ui
         } else {
             e.rec = kDictMark | (uint32_t)sl;
             e.info = make_info((uint32_t)ids.size(), ids.data(), kDictPool | dpool.size());
-            if (ids.size() > 2 || (ids.size() == 2 && !(e.info & kTwoIds))) dpool.insert(dpool.end(), ids.begin(), ids.end());
+            if (!ids.empty() && !(e.info & kInlineIds)) dpool.insert(dpool.end(), ids.begin(), ids.end());
         }
         ++words;
     }
@@ -2006,7 +2033,8 @@ int guarded_enc(F&& f) {
 // it has been read.  phase_ms: busy time of the reader, of validation + counting, of the encodes
 // and of the copier (they overlap).
 constexpr size_t kReadSlab = 1ull << 30;        // a multiple of the counting block (64 KiB)
-constexpr size_t kMaxRegion = 3ull << 30;       // bytes one encode takes at most (the copy tail)
+constexpr size_t kMaxRegion = 3ull << 30;       // bytes one encode takes at most
+constexpr size_t kLastRegion = 256ull << 20;    // bytes of the last region (the copy tail)
 
 size_t env_size(const char* name, size_t dflt) {   // test knobs: small slabs and regions
     const char* e = std::getenv(name);
@@ -2025,6 +2053,7 @@ size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint
     const auto t_call = clk::now();
     const size_t read_slab = std::max<size_t>(1, env_size("BPE355_READ_SLAB", kReadSlab) >> 16) << 16;
     const size_t max_region = env_size("BPE355_ENC_REGION", kMaxRegion);
+    const size_t last_region = std::min(max_region, env_size("BPE355_ENC_LAST_REGION", kLastRegion));
     // per-region lines (range, ids, pieces, ms; then the call's clock in ms at: the slab seen, its
     // validation + counting done, the encode done) appended to the file BPE355_ENC_TRACE names,
     // and one line per slab read and per copy (start, end)
@@ -2151,9 +2180,15 @@ size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint
             // kMaxRegion at a time, each region ending at a piece start (or the end)
             const size_t ready = std::min(vend, counted);
             auto region_end = [&](size_t from) -> size_t {
-                if (ready == n && n - from <= max_region) return n;
+                // once the whole text is in, the last region is kept short (at most last_region
+                // bytes): its ids' copy is the one step nothing overlaps
+                size_t span = max_region;
+                if (ready == n) {
+                    if (n - from <= last_region) return n;
+                    span = std::min(max_region, n - from - last_region);
+                }
                 size_t lim = from;
-                for (size_t i = next_piece; i < starts.size() && starts[i] <= std::min(ready, from + max_region); ++i)
+                for (size_t i = next_piece; i < starts.size() && starts[i] <= std::min(ready, from + span); ++i)
                     lim = starts[i];
                 if (lim == from && ready == n)   // a piece longer than kMaxRegion: whole
                     lim = next_piece < starts.size() ? starts[next_piece] : n;

@@ -987,6 +987,12 @@ constexpr int kProbeSlots = 32;   // 24-28: inside k_select's first phase
 #ifndef BPE355_PROBE_CODE
 #define BPE355_PROBE_CODE 0
 #endif
+// The select's diagnostic counters (list overflows, head misses, the k histogram and why trips
+// took one merge; printed under BPE355_TRACE) are compiled in only with -DBPE355_STATS_CODE=1.
+// n_rounds_batched comes from the trips' records on the host either way.
+#ifndef BPE355_STATS_CODE
+#define BPE355_STATS_CODE 0
+#endif
 __device__ __forceinline__ void probe_stamp(const RoundState* st, int trip, int k) {
     if (BPE355_PROBE_CODE && st->probe && (trip % kProbeTrip) == 0)
         st->probe[kProbeSlots * (size_t)(trip / kProbeTrip) + k] = __builtin_amdgcn_s_memrealtime();
@@ -1241,7 +1247,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
              pair_used + 2ull * (unsigned)(ntok + kMaxBatch) * kMaxBatch > pair_limit ||
              pool_used + (unsigned long long)kMaxBatch * max_len > pool_cap)
         stop = HALT_HOST;
-    if (lane == 0 && !halt) {   // no-return atomics: nothing waits on them
+    if (BPE355_STATS_CODE && lane == 0 && !halt) {   // no-return atomics: nothing waits on them
         if (ln > kListCap) atomicAdd(&bs->n_overflow, 1ull);
         else if (!list_ok) atomicAdd(&bs->n_headmiss, 1ull);
         else if (nf < kTopM) atomicAdd(&bs->n_short, 1ull);
@@ -1353,7 +1359,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     }
     if (lane == 0) probe_stamp(st, ptrip, 19);
     const bool fr0 = __builtin_amdgcn_readlane((int)fr, 0);
-    if (k == 1 && lane == 0) {
+    if (BPE355_STATS_CODE && k == 1 && lane == 0) {
         const int why = p1.a == p1.b ? 0 : !fr0 ? 1 : nf == 1 ? 2 : k_rule == 1 ? 3 : 4;
         atomicAdd(&bs->k1_why[why], 1ull);
     }
@@ -1427,11 +1433,13 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
             bs->T2 = nt < T ? T : (nt > top ? top : nt);
             bs->list_n = 0;   // the apply of this trip fills it again
         }
-        if (k > 1) {
-            atomicAdd(&bs->rounds_batched, (unsigned long long)k);
-            atomicAdd(&bs->trips_batched, 1ull);
+        if (BPE355_STATS_CODE) {
+            if (k > 1) {
+                atomicAdd(&bs->rounds_batched, (unsigned long long)k);
+                atomicAdd(&bs->trips_batched, 1ull);
+            }
+            atomicAdd(&bs->k_hist[k], 1ull);
         }
-        atomicAdd(&bs->k_hist[k], 1ull);
         if (trip_info) {   // for the host: first round, members, scan mode, list entries
             trip_info[4 * trip_slot] = round; trip_info[4 * trip_slot + 1] = k;
             trip_info[4 * trip_slot + 2] = full; trip_info[4 * trip_slot + 3] = (int)tot_list;
@@ -2554,7 +2562,7 @@ class MergeLoop {
     // batched rounds (single rank): several exact merges per trip (k_select)
     bool batched_ = false;
     int max_batch_ = kMaxBatch;
-    long long trips_launched_ = 0, trips_run_ = 0;
+    long long trips_launched_ = 0, trips_run_ = 0, rounds_batched_ = 0;
     DevBuf<BatchState> bs_;
     DevBuf<Batch> batch_;
     DevBuf<uint32_t> tags_;      // per slot word: the last batch that claimed it
@@ -3174,8 +3182,8 @@ void MergeLoop<TokT>::run() {
         BatchState b{};
         BPE_HIP(hipMemcpy(&b, bs_.p, sizeof(b), hipMemcpyDeviceToHost));
         out_.stats.n_trips = trips_run_;
-        out_.stats.n_rounds_batched = (int64_t)b.rounds_batched;
-        if (std::getenv("BPE355_TRACE")) {
+        out_.stats.n_rounds_batched = rounds_batched_;
+        if (BPE355_STATS_CODE && std::getenv("BPE355_TRACE")) {
             std::fprintf(stderr, "[bpe355] trips: list overflow %llu, head miss %llu, short %llu; k:", b.n_overflow,
                          b.n_headmiss, b.n_short);
             for (int i = 0; i <= kMaxBatch; ++i) std::fprintf(stderr, " %llu", b.k_hist[i]);
@@ -3423,7 +3431,10 @@ void MergeLoop<TokT>::finish_block(int slot, bool timing, std::vector<hipEvent_t
     BPE_HIP(hipEventSynchronize(blk_ev_[slot]));
     hs_ = snap_st_[slot];
     const int* ti = snap_ti_ + (size_t)slot * 4 * kTrips;
-    for (int t = 0; t < trips_; ++t) trips_run_ += ti[4 * t + 1] > 0;
+    for (int t = 0; t < trips_; ++t) {
+        trips_run_ += ti[4 * t + 1] > 0;
+        rounds_batched_ += ti[4 * t + 1] > 1 ? ti[4 * t + 1] : 0;
+    }
     {   // size the merge grid of the blocks launched from now on by this block's largest trip:
         // the members' list entries at one per thread, twice over for growth; a full scan (or
         // a single member without a list) wants the whole layout.  Any grid is correct.
