@@ -9,10 +9,12 @@ OUT=$ROOT/gpurun_out/$TAG
 mkdir -p $OUT
 cd $ROOT
 PYT="python -u -m pytest -x -q --timeout 400 --timeout-method thread"
-BPE355_LIB=build/variants/scan3/libbpe355.so timeout -k 10 400 $PYT tests/test_gpu_encode.py > $OUT/pytest_scan3.log 2>&1
-rc=$?; tail -1 $OUT/pytest_scan3.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" $OUT/pytest_scan3.log | head -30; exit $rc; }
+for v in scan3 scan3c; do
+  BPE355_LIB=build/variants/$v/libbpe355.so timeout -k 10 400 $PYT tests/test_gpu_encode.py > $OUT/pytest_$v.log 2>&1
+  rc=$?; tail -1 $OUT/pytest_$v.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" $OUT/pytest_$v.log | head -30; exit $rc; }
+done
 for rep in 1 2; do
-  for v in cur scan3; do
+  for v in cur scan3 scan3c; do
     BPE355_LIB=build/variants/$v/libbpe355.so timeout -k 10 300 python tools/enc_bench.py > $OUT/enc_$v.$rep.log 2>&1 || { tail -5 $OUT/enc_$v.$rep.log; exit 1; }
     echo "$v: $(tail -1 $OUT/enc_$v.$rep.log)"
   done

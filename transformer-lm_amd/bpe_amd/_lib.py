@@ -218,9 +218,12 @@ def take_result(res: ctypes.c_void_p):
         n = L.bpe_result_flat(res, which, ctypes.byref(lens), ctypes.byref(data), ctypes.byref(nb))
         if n == 0:
             return []
-        off = list(itertools.accumulate(lens[:n], initial=0))
+        # lengths through a memoryview (one C call) and a list comprehension of slices: the
+        # fastest of the forms timed for ~64 K merge parts + 32 K vocab entries
+        lv = memoryview((ctypes.c_uint32 * n).from_address(ctypes.addressof(lens.contents))).cast("B").cast("I")
+        off = list(itertools.accumulate(lv.tolist(), initial=0))
         buf = ctypes.string_at(data, nb.value)
-        return list(map(buf.__getitem__, map(slice, off[:-1], off[1:])))
+        return [buf[a:b] for a, b in zip(off, off[1:])]
     try:
         m = flat(0)
         v = flat(1)

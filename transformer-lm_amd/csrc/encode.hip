@@ -383,7 +383,12 @@ __device__ __forceinline__ bool dict_find_info(const EncDict& D, uint64_t wl, ui
     }
 }
 
-constexpr int kEncCache = 512;    // LDS word cache (2-way): word -> record
+// LDS word cache of the scan (2-way): word -> record (build knob BPE355_ENC_CACHE, a power of 2)
+#ifndef BPE355_ENC_CACHE
+#define BPE355_ENC_CACHE 512
+#endif
+constexpr int kEncCache = BPE355_ENC_CACHE;
+static_assert((kEncCache & (kEncCache - 1)) == 0, "the scan's cache size is a power of two");
 constexpr int kEncEpoch = 4;
 constexpr unsigned kEncKeep = 2;
 constexpr int kSegLds = 64;
