@@ -275,6 +275,28 @@ def test_encode_file_overlapped_regions(tmp_path, monkeypatch, slab, region, k):
     assert set(last_phases_ms) == {"read", "decode", "encode", "copy"}
 
 
+@pytest.mark.parametrize("knobs", [{"BPE355_D2H_WG": "7"}, {"BPE355_ENC_LAST_REGION": "30000"},
+                                   {"BPE355_D2H_WG": "64", "BPE355_ENC_LAST_REGION": "1"}])
+def test_encode_file_copy_kernel_and_last_region(tmp_path, monkeypatch, knobs):
+    """the ids copied out by the workgroup copy kernel (BPE355_D2H_WG, instead of HIP's copy) and
+    a short last region once the whole file is in (BPE355_ENC_LAST_REGION): the same ids"""
+    from bpe_amd import Tokenizer
+    from bpe_amd.encode import encode_file
+    vocab, merges = gpt2_files.load_gpt2(["<|endoftext|>"])
+    tok = Tokenizer(dict(vocab), list(merges), ["<|endoftext|>"])
+    text = _mixed_text(12, 60000).replace("\r", "")
+    data = text.encode("utf-8")
+    src = tmp_path / "t.txt"
+    src.write_bytes(data)
+    want = _encode_chunks(tok, data, _piece_starts(text, 997))
+    monkeypatch.setenv("BPE355_READ_SLAB", "65536")
+    monkeypatch.setenv("BPE355_ENC_REGION", "100000")
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    got = encode_file(tok, src, chars_per_piece=997)
+    assert got.dtype == np.uint16 and got.tolist() == want
+
+
 def test_encode_file_late_carriage_return_and_bad_utf8(tmp_path, monkeypatch):
     """a carriage return first seen after regions were already encoded: the whole text is redone
     with universal newlines; an ill-formed byte late in the file raises UnicodeDecodeError at its

@@ -125,13 +125,10 @@ __global__ void __launch_bounds__(256) k_to_host(const uint8_t* __restrict__ src
 // workgroups per device-to-host chunk copy by k_to_host (BPE355_D2H_WG); 0, the default:
 // hipMemcpyAsync.  16 workgroups moved encode_file's ids at ~18 GB/s against HIP's ~34 (r04u:
 // 581-670 vs 383-421 ms per 11.9 GB call), so the knob stays for A/B only.
-int d2h_wg() {
-    static const int w = [] {
-        int n = 0;
-        if (const char* e = std::getenv("BPE355_D2H_WG")) n = std::atoi(e);
-        return std::max(0, std::min(n, 1024));
-    }();
-    return w;
+int d2h_wg() {   // read per call, so a test can switch it
+    int n = 0;
+    if (const char* e = std::getenv("BPE355_D2H_WG")) n = std::atoi(e);
+    return std::max(0, std::min(n, 1024));
 }
 
 // Device buffers for the corpus, kept across training calls (per device, checked out by one
