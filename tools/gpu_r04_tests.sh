@@ -9,3 +9,8 @@ timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeou
 tail -1 $OUT/pytest_gpu.log
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; tail -30 $OUT/smoke.log; exit 1; }
 tail -1 $OUT/smoke.log
+for k in BPE355_D2H_PRIO=1 BPE355_D2H_PRIO=0 BPE355_D2H_PRIO=1 BPE355_D2H_PRIO=0; do
+  env $k timeout -k 10 300 python -u tools/enc_file_bench.py > $OUT/k_${k//=/_}.log 2>&1 || { tail -5 $OUT/k_${k//=/_}.log; exit 1; }
+  grep call $OUT/k_${k//=/_}.log
+done
+rm -f /tmp/bpe355_encfile.txt

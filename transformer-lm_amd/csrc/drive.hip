@@ -206,14 +206,20 @@ namespace {
 // few deep queues keep the copy engines busier than one queue per thread
 struct DmaStreams {
     std::vector<hipStream_t> s;
-    DmaStreams(int device, int n) {   // on `device`; the calling thread's current device is kept
+    // on `device` (the calling thread's current device is kept); low_priority: the least stream
+    // priority the device offers
+    DmaStreams(int device, int n, bool low_priority = false) {
         int cur = 0;
         BPE_HIP(hipGetDevice(&cur));
         BPE_HIP(hipSetDevice(device));
         s.resize(n, nullptr);
+        int least = 0, greatest = 0;
+        if (low_priority) BPE_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
         hipError_t e = hipSuccess;
         for (auto& x : s)
-            if (e == hipSuccess) e = hipStreamCreateWithFlags(&x, hipStreamNonBlocking);
+            if (e == hipSuccess)
+                e = low_priority ? hipStreamCreateWithPriority(&x, hipStreamNonBlocking, least)
+                                 : hipStreamCreateWithFlags(&x, hipStreamNonBlocking);
         BPE_HIP(hipSetDevice(cur));
         if (e != hipSuccess) {
             for (auto& x : s)
@@ -243,7 +249,11 @@ const DmaStreams& cached_dma(int device, int dir) {
     std::lock_guard<std::mutex> g(m);
     const size_t i = (size_t)device * 2 + (size_t)dir;
     if (made.size() <= i) made.resize(i + 1, nullptr);
-    if (!made[i]) made[i] = new DmaStreams(device, dma_streams());
+    // device-to-host copies run at the least priority: HIP serves them with a copy kernel, whose
+    // workgroups should yield the CUs to the encode beside it (BPE355_D2H_PRIO=0: normal priority)
+    const char* pe = std::getenv("BPE355_D2H_PRIO");
+    const bool low = dir == 1 && !(pe && pe[0] == '0');
+    if (!made[i]) made[i] = new DmaStreams(device, dma_streams(), low);
     return *made[i];
 }
 }  // namespace
