@@ -33,6 +33,10 @@
 #include "stage2.h"
 #include "tokstart.h"
 
+#ifndef BPE355_COUNT_EARLY_PREFETCH
+#define BPE355_COUNT_EARLY_PREFETCH 0
+#endif
+
 namespace bpe {
 
 namespace {
@@ -125,6 +129,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
             break;
         }
         const size_t base = (chunk0 + c) * kChunk;
+        // build knob BPE355_COUNT_EARLY_PREFETCH: the next chunk's loads before the mask phase
+        if (BPE355_COUNT_EARLY_PREFETCH && c + gridDim.x < n_chunks)
+            fetch2<kAligned>(pre, s, n, (chunk0 + c + gridDim.x) * kChunk, tid);
 
         // ---- token-start masks: word w covers chunk bytes [64 w, 64 w + 64)
         auto mask_word = [&](int w) -> uint64_t {
@@ -142,7 +149,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
         };
         s_mask[tid] = mask_word(tid);
         // the next chunk's loads fly during the token phase (not the register-heavy mask phase)
-        if (c + gridDim.x < n_chunks) fetch2<kAligned>(pre, s, n, (chunk0 + c + gridDim.x) * kChunk, tid);
+        if (!BPE355_COUNT_EARLY_PREFETCH && c + gridDim.x < n_chunks)
+            fetch2<kAligned>(pre, s, n, (chunk0 + c + gridDim.x) * kChunk, tid);
         __syncthreads();
 
         // ---- the pre-tokens that start in this thread's 64 bytes

@@ -512,6 +512,9 @@ __device__ __forceinline__ uint32_t dict_rec(uint32_t rec, size_t cap) {
 #ifndef BPE355_ENC_SCAN_WG
 #define BPE355_ENC_SCAN_WG 4
 #endif
+#ifndef BPE355_ENC_EARLY_PREFETCH
+#define BPE355_ENC_EARLY_PREFETCH 0
+#endif
 template <bool kAligned>
 __global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan4(ScanArgs A, EncDict D) {
     __shared__ uint64_t s_mask[kWords];
@@ -628,6 +631,9 @@ __global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan4(ScanArgs 
             if (tid == 0) atomicOr(A.status, 1u);
             break;
         }
+        // the next chunk's loads: before the mask phase (build knob BPE355_ENC_EARLY_PREFETCH), so
+        // that they land during its VALU work instead of stalling the token phase's first wait
+        if (BPE355_ENC_EARLY_PREFETCH && c + gridDim.x < A.n_chunks) fetch2<kAligned>(pre, s, n, (c + gridDim.x) * kChunk, tid);
         const int seg0 = s_seg0, segn = s_segn;
         auto seg_at = [&](int i) -> Seg { return segn >= 0 ? s_seg[i - seg0] : A.segs[i]; };
         const int seg_end = segn >= 0 ? seg0 + segn : A.nseg;
@@ -678,7 +684,7 @@ __global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan4(ScanArgs 
             if (lane >= o) x += y;
         }
         if (lane == 63) s_wsum[wave] = x;
-        if (c + gridDim.x < A.n_chunks) fetch2<kAligned>(pre, s, n, (c + gridDim.x) * kChunk, tid);
+        if (!BPE355_ENC_EARLY_PREFETCH && c + gridDim.x < A.n_chunks) fetch2<kAligned>(pre, s, n, (c + gridDim.x) * kChunk, tid);
         __syncthreads();
         uint32_t toff = x - cnt;
         for (int w = 0; w < wave; ++w) toff += s_wsum[w];
