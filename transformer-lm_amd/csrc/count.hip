@@ -33,8 +33,10 @@
 #include "stage2.h"
 #include "tokstart.h"
 
+// the next chunk's loads issued before the mask phase (1, the default: 14 spilled VGPRs instead of
+// 20, k_count2 58.2 vs 59.0 ms in two paired runs, profiles/r04/y_*) or after it (0)
 #ifndef BPE355_COUNT_EARLY_PREFETCH
-#define BPE355_COUNT_EARLY_PREFETCH 0
+#define BPE355_COUNT_EARLY_PREFETCH 1
 #endif
 
 namespace bpe {
@@ -148,7 +150,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
             return m;
         };
         s_mask[tid] = mask_word(tid);
-        // the next chunk's loads fly during the token phase (not the register-heavy mask phase)
+        // (knob 0: the next chunk's loads fly during the token phase only)
         if (!BPE355_COUNT_EARLY_PREFETCH && c + gridDim.x < n_chunks)
             fetch2<kAligned>(pre, s, n, (chunk0 + c + gridDim.x) * kChunk, tid);
         __syncthreads();

@@ -512,6 +512,8 @@ __device__ __forceinline__ uint32_t dict_rec(uint32_t rec, size_t cap) {
 #ifndef BPE355_ENC_SCAN_WG
 #define BPE355_ENC_SCAN_WG 4
 #endif
+// the scan's next-chunk loads before the mask phase: 35 spilled VGPRs instead of 63, but no faster
+// (168.6-169.4 vs 168.6-168.7 ms per encode, profiles/r04/y_*), so off
 #ifndef BPE355_ENC_EARLY_PREFETCH
 #define BPE355_ENC_EARLY_PREFETCH 0
 #endif
