@@ -33,6 +33,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <exception>
 #include <memory>
 #include <mutex>
@@ -2048,6 +2049,7 @@ int guarded_enc(F&& f) {
 constexpr size_t kReadSlab = 1ull << 30;        // a multiple of the counting block (64 KiB)
 constexpr size_t kMaxRegion = 3ull << 30;       // bytes one encode takes at most
 constexpr size_t kLastRegion = 256ull << 20;    // bytes of the last region (the copy tail)
+constexpr size_t kMinRegion = 64ull << 20;      // bytes a region takes at least while the file arrives
 
 size_t env_size(const char* name, size_t dflt) {   // test knobs: small slabs and regions
     const char* e = std::getenv(name);
@@ -2067,6 +2069,7 @@ size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint
     const size_t read_slab = std::max<size_t>(1, env_size("BPE355_READ_SLAB", kReadSlab) >> 16) << 16;
     const size_t max_region = env_size("BPE355_ENC_REGION", kMaxRegion);
     const size_t last_region = std::min(max_region, env_size("BPE355_ENC_LAST_REGION", kLastRegion));
+    const size_t min_region = std::min(max_region, env_size("BPE355_ENC_MIN_REGION", kMinRegion));
     // per-region lines (range, ids, pieces, ms; then the call's clock in ms at: the slab seen, its
     // validation + counting done, the encode done) appended to the file BPE355_ENC_TRACE names,
     // and one line per slab read and per copy (start, end)
@@ -2088,6 +2091,8 @@ size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint
     // 4 threads 1.96-2.0 s before the region encode got fast; r03, with a 430 ms encode phase: 4
     // threads 593-648 ms, 8: 713-749, 16: 810-858)
     const int io_n = (int)env_size("BPE355_ENC_IO_THREADS", 8);
+    // host threads of each region's copy-out (the reader's io_n unless BPE355_ENC_COPY_THREADS)
+    const int copy_n = (int)env_size("BPE355_ENC_COPY_THREADS", (size_t)io_n);
     // experiment knob: BPE355_ENC_OVERLAP=0 reads the whole file before the first encode
     const char* ov = std::getenv("BPE355_ENC_OVERLAP");
     const bool overlap_read = !(ov && ov[0] == '0');
@@ -2120,30 +2125,58 @@ size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint
         ph[0] = since(t0);
         cv.notify_all();
     });
-    // copier: one region at a time
-    std::thread copier;
+    // copier: a queue of regions copied out in order by one thread (each copy fans out over io_n
+    // threads), so the encoder never waits for one region's copy before it starts the next
+    // (r04za timeline: waiting for the previous copy held the encoder 13-40 ms per region)
+    std::mutex qm;
+    std::condition_variable qcv;
+    std::deque<std::pair<size_t, size_t>> cq;
+    bool cq_closed = false;
     std::exception_ptr copy_err;
-    auto copy_wait = [&] {
-        if (copier.joinable()) copier.join();
-        if (copy_err) std::rethrow_exception(copy_err);
-    };
-    auto copy_start = [&](size_t at, size_t cnt) {
-        copy_wait();
-        copier = std::thread([&, at, cnt] {
+    std::thread copier([&] {
+        for (;;) {
+            std::pair<size_t, size_t> job;
+            {
+                std::unique_lock<std::mutex> g(qm);
+                qcv.wait(g, [&] { return !cq.empty() || cq_closed; });
+                if (cq.empty()) return;
+                job = cq.front();
+                cq.pop_front();
+            }
+            if (copy_err || stop.load()) continue;   // after an error: drain without copying
             const auto t0 = clk::now();
             try {
-                device_to_host(reinterpret_cast<const uint8_t*>(S.ids16.p + at), 2 * cnt,
-                               reinterpret_cast<uint8_t*>(ids_out + at), dev, io_n);
+                device_to_host(reinterpret_cast<const uint8_t*>(S.ids16.p + job.first), 2 * job.second,
+                               reinterpret_cast<uint8_t*>(ids_out + job.first), dev, copy_n);
             } catch (...) {
                 copy_err = std::current_exception();
             }
             ph[3] += since(t0);
             if (trace) {
                 std::lock_guard<std::mutex> g(m);
-                std::fprintf(trace, "copy %zu ids at %.1f %.1f\n", cnt, std::chrono::duration<double, std::milli>(t0 - t_call).count(),
-                             since(t_call));
+                std::fprintf(trace, "copy %zu ids at %.1f %.1f\n", job.second,
+                             std::chrono::duration<double, std::milli>(t0 - t_call).count(), since(t_call));
             }
-        });
+        }
+    });
+    auto copy_close = [&] {
+        {
+            std::lock_guard<std::mutex> g(qm);
+            cq_closed = true;
+        }
+        qcv.notify_all();
+        if (copier.joinable()) copier.join();
+    };
+    auto copy_wait = [&] {   // every queued copy done (then no more can be queued)
+        copy_close();
+        if (copy_err) std::rethrow_exception(copy_err);
+    };
+    auto copy_start = [&](size_t at, size_t cnt) {
+        {
+            std::lock_guard<std::mutex> g(qm);
+            cq.emplace_back(at, cnt);
+        }
+        qcv.notify_one();
     };
     auto finish_threads = [&] {
         stop.store(true);
@@ -2152,7 +2185,7 @@ size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint
             cv.wait(g, [&] { return read_done; });
         }
         if (reader.joinable()) reader.join();
-        if (copier.joinable()) copier.join();
+        copy_close();
     };
 
     size_t k_done = 0;
@@ -2205,6 +2238,9 @@ size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint
                     lim = starts[i];
                 if (lim == from && ready == n)   // a piece longer than kMaxRegion: whole
                     lim = next_piece < starts.size() ? starts[next_piece] : n;
+                // while the file is still arriving, a short leftover (the piece cut by a slab end)
+                // waits for the next slab instead of costing an encode call of its own
+                if (ready < n && lim - from < min_region) return from;
                 return lim;
             };
             for (size_t e_end = region_end(enc_done); e_end > enc_done; e_end = region_end(enc_done)) {
