@@ -2091,8 +2091,10 @@ size_t encode_file_pipelined(bpe_tokenizer& T, const Source& src, size_t K, uint
     // 4 threads 1.96-2.0 s before the region encode got fast; r03, with a 430 ms encode phase: 4
     // threads 593-648 ms, 8: 713-749, 16: 810-858)
     const int io_n = (int)env_size("BPE355_ENC_IO_THREADS", 8);
-    // host threads of each region's copy-out (the reader's io_n unless BPE355_ENC_COPY_THREADS)
-    const int copy_n = (int)env_size("BPE355_ENC_COPY_THREADS", (size_t)io_n);
+    // host threads of each region's copy-out (BPE355_ENC_COPY_THREADS): 4 leave the host cores the
+    // encoder's own thread needs while 8 readers run (r04zc, 11.9 GB: 4 threads 358-365 ms per warm
+    // call, 8 376-451, 2 442-446)
+    const int copy_n = (int)env_size("BPE355_ENC_COPY_THREADS", 4);
     // experiment knob: BPE355_ENC_OVERLAP=0 reads the whole file before the first encode
     const char* ov = std::getenv("BPE355_ENC_OVERLAP");
     const bool overlap_read = !(ov && ov[0] == '0');
