@@ -120,8 +120,6 @@ def test_encode_several_devices_equals_one(ranks, monkeypatch):
     {"BPE355_ENC_RESOLVE_CACHE": "0"},                           # the resolve without its LDS cache
     {"BPE355_ENC_FINALIZE": "0"},                                # the emit reads resolved records
     {"BPE355_ENC_FINALIZE": "2"},                                # the count pass stores the infos
-    {"BPE355_ENC_RESOLVE_ILP": "1"},                             # two entries per resolve thread
-    {"BPE355_ENC_RESOLVE_ILP": "1", "BPE355_ENC_PEND_CAP": "40000", "BPE355_STREAM_WG": "2"},
 ])
 def test_encode_resolution_paths(monkeypatch, knobs):
     """the encoder's record paths against the oracle: pending entries resolved by k_enc_resolve,

@@ -963,145 +963,6 @@ __global__ void __launch_bounds__(256) k_enc_resolve_c(ResolveArgs A, EncDict D,
     if ((threadIdx.x & 63) == 0 && inserted) atomicAdd(A.fill, inserted);
 }
 
-// The same with two entries per thread per step (j and j + 256 of a block): each stage's loads
-// (the entries, their words' bytes, the filter words, the first dictionary and table probes) are
-// issued for both before either is waited on, twice the misses in flight per wave.
-// BPE355_ENC_RESOLVE_ILP=1 selects it.
-constexpr int kResU = 2;
-__global__ void __launch_bounds__(256) k_enc_resolve_c2(ResolveArgs A, EncDict D, unsigned n_blocks) {
-    __shared__ unsigned long long c_key[kResCache];
-    __shared__ uint64_t c_lo[kResCache], c_hi[kResCache];
-    __shared__ uint32_t c_rec[kResCache];
-    unsigned long long inserted = 0, n_hit = 0, n_dict = 0, n_table = 0;
-    for (int i = threadIdx.x; i < kResCache; i += blockDim.x) c_key[i] = 0;
-    __syncthreads();
-    __shared__ unsigned long long s_ins;
-    __shared__ int s_full;
-    for (unsigned b = blockIdx.x; b < n_blocks; b += gridDim.x) {
-        const unsigned long long ins = wave_sum(inserted);
-        inserted = 0;
-        if (threadIdx.x == 0) { s_ins = 0; s_full = 0; }
-        __syncthreads();
-        if ((threadIdx.x & 63) == 0 && ins) atomicAdd(&s_ins, ins);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const unsigned long long f = s_ins ? atomicAdd(A.fill, s_ins) + s_ins : *(volatile unsigned long long*)A.fill;
-            if (f > A.max_fill) {
-                s_full = 1;
-                atomicOr(A.status, 1u);
-            }
-        }
-        __syncthreads();
-        if (s_full) return;
-        const unsigned used = A.block_used[b];
-        const size_t base = (size_t)b * kPendBlock;
-        for (unsigned j0 = threadIdx.x; j0 < used; j0 += kResU * blockDim.x) {
-            size_t gp[kResU], len[kResU];
-            bool have[kResU], found[kResU], cacheable[kResU];
-            uint64_t wl[kResU], wh[kResU], h[kResU];
-            unsigned long long val[kResU];
-            unsigned ls[kResU];
-#pragma unroll
-            for (int u = 0; u < kResU; ++u) {   // the entries
-                const unsigned j = j0 + u * blockDim.x;
-                have[u] = j < used;
-                const unsigned long long e = have[u] ? A.pend[base + j] : 0ULL;
-                gp[u] = (size_t)(e >> kPendShift);
-                len[u] = (size_t)(e & ((1ULL << kPendShift) - 1));
-                found[u] = false;
-                val[u] = 0;
-                wl[u] = wh[u] = 0;
-                ls[u] = 0;
-                cacheable[u] = have[u] && len[u] >= 2 && len[u] <= (size_t)kInline;
-            }
-#pragma unroll
-            for (int u = 0; u < kResU; ++u) {   // their bytes and hashes, then the LDS cache
-                if (!have[u]) continue;
-                if (len[u] <= (size_t)kInline) {
-                    load_word(A.s, A.n, gp[u], len[u], wl[u], wh[u]);
-                    h[u] = short_hash(wl[u], wh[u], len[u]);
-                } else {
-                    h[u] = hash_word(A.s, gp[u], len[u]);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kResU; ++u) {
-                if (!cacheable[u]) continue;
-                ls[u] = (unsigned)(h[u] >> 40) & (kResCache - 2);
-                for (int way = 0; way < 2 && !found[u]; ++way) {
-                    const unsigned sl = ls[u] + way;
-                    const unsigned long long k = c_key[sl];
-                    if (k != 0 && k != kBusy && (k >> 40) == len[u]) {
-                        __asm__ volatile("" ::: "memory");
-                        if (c_lo[sl] == wl[u] && c_hi[sl] == wh[u]) {
-                            const uint32_t r = c_rec[sl];
-                            val[u] = rec_is_direct(r) ? kOneId | (r & kRecPayload) : r;
-                            found[u] = true;
-                            ++n_hit;
-                        }
-                    }
-                }
-            }
-            bool maybe[kResU];
-#pragma unroll
-            for (int u = 0; u < kResU; ++u)   // the filter words of both
-                maybe[u] = cacheable[u] && !found[u] && filt_maybe(D, h[u]);
-#pragma unroll
-            for (int u = 0; u < kResU; ++u) {   // the dictionary
-                if (!maybe[u]) continue;
-                size_t sl = h[u] & D.mask;
-                for (;;) {
-                    const DictEnt e = D.ent[sl];
-                    if (e.len == 0) break;
-                    if (e.len == len[u] && e.lo == wl[u] && e.hi == wh[u]) {
-                        val[u] = e.info;
-                        found[u] = true;
-                        ++n_dict;
-                        break;
-                    }
-                    sl = (sl + 1) & D.mask;
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kResU; ++u) {   // the word table
-                if (!have[u] || found[u]) continue;
-                bool ins_ = false;
-                const size_t slot = enc_table_add(A.s, gp[u], len[u], wl[u], wh[u], h[u], A.kv, A.pos, A.mask, A.status, &ins_);
-                inserted += ins_;
-                ++n_table;
-                val[u] = kRecSlot | (slot == ~(size_t)0 ? 0u : (uint32_t)slot);
-            }
-#pragma unroll
-            for (int u = 0; u < kResU; ++u) {
-                if (!have[u]) continue;
-                const bool one = (val[u] & kOneId) && (uint32_t)val[u] < kRecPayload;
-                if (cacheable[u] && (one || resolved_is_rec(val[u]))) {
-                    for (int way = 0; way < 2; ++way) {
-                        const unsigned sl = ls[u] + way;
-                        if (c_key[sl] == 0 && atomicCAS(&c_key[sl], 0ULL, kBusy) == 0) {
-                            c_lo[sl] = wl[u];
-                            c_hi[sl] = wh[u];
-                            c_rec[sl] = one ? kRecDirect | (uint32_t)val[u] : (uint32_t)val[u];
-                            __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                            atomicExch(&c_key[sl], ((unsigned long long)len[u] << 40) | 1ULL);
-                            break;
-                        }
-                    }
-                }
-                A.pend[base + j0 + u * blockDim.x] = val[u];
-            }
-        }
-        if (((b - blockIdx.x) / gridDim.x) % 4 == 3) {   // a fresh cache every 4 blocks
-            __syncthreads();
-            for (int i = threadIdx.x; i < kResCache; i += blockDim.x) c_key[i] = 0;
-            __syncthreads();
-        }
-    }
-    resolve_stats(A.stats, n_hit, n_dict, n_table);
-    inserted = wave_sum(inserted);
-    if ((threadIdx.x & 63) == 0 && inserted) atomicAdd(A.fill, inserted);
-}
-
 // ------------------------------------------------------------------ 3. unique words
 // Every word-table slot in use -> (slot, offset, length).  A workgroup takes kCollectPer x 256
 // slots (coalesced) and reserves its words' positions with ONE global atomic: one per wave would
@@ -1941,13 +1802,7 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
             // the LDS-cached resolve (default: 195 vs 198 ms at the bench corpus, r04h); the knob's
             // 0 runs the uncached one
             const char* rc_env = std::getenv("BPE355_ENC_RESOLVE_CACHE");
-            const char* ilp_env = std::getenv("BPE355_ENC_RESOLVE_ILP");
-            if (!(rc_env && rc_env[0] == '0') && ilp_env && ilp_env[0] == '1') {
-                int c_cu = 0;
-                BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&c_cu, k_enc_resolve_c2, 256, 0));
-                const unsigned cgrid = std::min<unsigned>(nblk, (unsigned)(std::max(1, c_cu) * std::max(1, n_cu)));
-                hipLaunchKernelGGL(k_enc_resolve_c2, dim3(cgrid), dim3(256), 0, s, RA, D, nblk);
-            } else if (!(rc_env && rc_env[0] == '0')) {
+            if (!(rc_env && rc_env[0] == '0')) {
                 int c_cu = 0;
                 BPE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&c_cu, k_enc_resolve_c, 256, 0));
                 const unsigned cgrid = std::min<unsigned>(nblk, (unsigned)(std::max(1, c_cu) * std::max(1, n_cu)));
