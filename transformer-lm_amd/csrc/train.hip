@@ -1044,7 +1044,12 @@ __device__ __forceinline__ void cand_meta(const Cand& c, const ToksDev& K, const
 // look up its entries' metadata and rank them.  All global loads are issued before the first
 // barrier, so the kernel costs about one memory round trip plus the dedupe lookups' chain, then
 // the ranking, the rule and the record (wave 0).
-constexpr int kSelListWave = 8;   // first wave of the list
+// waves of k_select that reduce the apply's partials (kPartPer each per thread); the list's waves
+// follow them (build knob BPE355_SEL_PART_WAVES)
+#ifndef BPE355_SEL_PART_WAVES
+#define BPE355_SEL_PART_WAVES 8
+#endif
+constexpr int kSelListWave = BPE355_SEL_PART_WAVES;   // first wave of the list
 constexpr unsigned kListTarget = 48;   // keys the next list should hold (T2 control)
 constexpr bool kSelMetaAll = true;     // metadata of every listed key before the ranking
 constexpr int kSelThreads = 64 * kSelListWave + (int)kListCap;
