@@ -1045,9 +1045,11 @@ __device__ __forceinline__ void cand_meta(const Cand& c, const ToksDev& K, const
 // barrier, so the kernel costs about one memory round trip plus the dedupe lookups' chain, then
 // the ranking, the rule and the record (wave 0).
 // waves of k_select that reduce the apply's partials (kPartPer each per thread); the list's waves
-// follow them (build knob BPE355_SEL_PART_WAVES)
+// follow them (build knob BPE355_SEL_PART_WAVES).  4 waves with two partials per thread: a 512-
+// thread select, 252.2-253.7 ms of HBM-resident merges against 255.0-268.0 with 8 waves and
+// 258.3-260.6 with 2 (two paired reps, profiles/r04/zh_*)
 #ifndef BPE355_SEL_PART_WAVES
-#define BPE355_SEL_PART_WAVES 8
+#define BPE355_SEL_PART_WAVES 4
 #endif
 constexpr int kSelListWave = BPE355_SEL_PART_WAVES;   // first wave of the list
 constexpr unsigned kListTarget = 48;   // keys the next list should hold (T2 control)
