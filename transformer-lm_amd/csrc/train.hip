@@ -949,7 +949,13 @@ struct BatchState {
     unsigned long long n_overflow, n_headmiss, n_short, k_hist[kMaxBatch + 1];   // diagnostics
     unsigned long long k1_why[6];   // single-merge trips: P1 a == b / P1 not fresh / no list / P2 fails / tie / end
 };
-constexpr unsigned kListCap = 256;   // the candidate list k_select ranks (one thread per entry)
+// the candidate list k_select ranks, one thread per entry (build knob BPE355_LIST_CAP, a multiple
+// of 64; a trip whose list overflows it takes P1 alone and raises T2)
+#ifndef BPE355_LIST_CAP
+#define BPE355_LIST_CAP 256
+#endif
+constexpr unsigned kListCap = BPE355_LIST_CAP;
+static_assert(kListCap % 64 == 0 && kListCap >= 64, "whole waves of list threads");
 // k_apply_batch workgroups (k_select reads one partial each; build knob BPE355_APPLY_GRID)
 #ifndef BPE355_APPLY_GRID
 #define BPE355_APPLY_GRID 512
