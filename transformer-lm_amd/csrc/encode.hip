@@ -390,7 +390,10 @@ __device__ __forceinline__ bool dict_find_info(const EncDict& D, uint64_t wl, ui
 #endif
 constexpr int kEncCache = BPE355_ENC_CACHE;
 static_assert((kEncCache & (kEncCache - 1)) == 0, "the scan's cache size is a power of two");
-constexpr int kEncEpoch = 4;
+#ifndef BPE355_ENC_EPOCH
+#define BPE355_ENC_EPOCH 4
+#endif
+constexpr int kEncEpoch = BPE355_ENC_EPOCH;   // chunks between the scan cache's evictions
 constexpr unsigned kEncKeep = 2;
 constexpr int kSegLds = 64;
 

@@ -1058,7 +1058,10 @@ __device__ __forceinline__ void cand_meta(const Cand& c, const ToksDev& K, const
 #define BPE355_SEL_PART_WAVES 4
 #endif
 constexpr int kSelListWave = BPE355_SEL_PART_WAVES;   // first wave of the list
-constexpr unsigned kListTarget = 48;   // keys the next list should hold (T2 control)
+#ifndef BPE355_LIST_TARGET
+#define BPE355_LIST_TARGET 48
+#endif
+constexpr unsigned kListTarget = BPE355_LIST_TARGET;   // keys the next list should hold (T2 control)
 constexpr bool kSelMetaAll = true;     // metadata of every listed key before the ranking
 constexpr int kSelThreads = 64 * kSelListWave + (int)kListCap;
 __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__ st, BatchState* __restrict__ bs,
