@@ -87,6 +87,28 @@ def write_corpus(L, path: pathlib.Path, n: int, seed: int, flavour: int):
     os.replace(tmp, path)
 
 
+def golden_parity(n, seed, flavour, vocab_size, vocab, merges):
+    """The step's result against the committed scale golden of the same corpus, if there is one
+    (tests/golden/scale/train_*.json.gz: the C oracle's merges and vocab sha256 for (n, seed,
+    flavour, vocab), made by tests/golden/make_scale_golden.py; test data, not the oracle)."""
+    import gzip
+    import hashlib
+    import struct
+    for p in sorted((ROOT / "tests" / "golden" / "scale").glob("train_*.json.gz")):
+        g = json.load(gzip.open(p, "rt"))
+        if (g["n"], g["seed"], g["flavour"], g["vocab"]) != (n, seed, flavour, vocab_size):
+            continue
+        h = hashlib.sha256()
+        for i in range(len(vocab)):
+            h.update(struct.pack("<I", len(vocab[i])) + vocab[i])
+        want = [(bytes.fromhex(a), bytes.fromhex(b)) for a, b in g["merges"]]
+        ok_m, ok_v = merges == want, h.hexdigest() == g["vocab_sha256"]
+        return {"parity": ok_m and ok_v, "golden": f"tests/golden/scale/{p.name}", "merges_equal": ok_m,
+                "vocab_sha256_equal": ok_v}
+    return {"parity": None, "golden": None,
+            "note": f"no scale golden for n={n} seed={seed} flavour={flavour} vocab={vocab_size}"}
+
+
 def cpu_baselines(args, path, vocab, merges, L):
     """The CPU legs (oracle/cpu_bench.py) in a child process that never touches the GPU: the
     pure-Python port on corpus.en in full and on 16 / 64 MB samples (one core each), the
@@ -188,10 +210,10 @@ def main():
               file=sys.stderr, flush=True)
     barrier()
 
-    def train_file():
+    def train_file():   # steps repeat, so the corpus buffer and the counter's scratch are kept
         if multiproc:
-            return train_bpe(path, args.vocab, [EOT], comm=comm, split_file=True)
-        return train_bpe(path, args.vocab, [EOT])
+            return train_bpe(path, args.vocab, [EOT], comm=comm, split_file=True, keep_device_buffers=True)
+        return train_bpe(path, args.vocab, [EOT], keep_device_buffers=True)
 
     # ---------------------------------------------------------------- end to end: file -> merges
     stats = []
@@ -220,8 +242,8 @@ def main():
         for d in rounds:
             v = json.loads((d / "traffic.json").read_text()).get(kernel)
             if v is not None:
-                return v
-        return None
+                return v, f"profiles/{d.name}/traffic.json (committed PMC passes, not measured in this run)"
+        return None, None
 
     def merge_roofline(st, note):
         """the dominant kernel by device time, k_merge_batch (the merge-apply rewrite of a trip):
@@ -235,8 +257,9 @@ def main():
         us = a["merge_kernel_ms"] * 1e3 / a["merge_kernel_launches"]
         bpl = a["merge_kernel_bytes"] / a["merge_kernel_launches"]
         achieved = bpl / (us * 1e-6) / 1e9
+        tr, tsrc = traffic_of("k_merge_batch")
         return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_of("k_merge_batch"),
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr, "traffic_source": tsrc,
                 "kernel": "k_merge_batch", "launches_per_step": int(a["n_trips"]),
                 "timed_launches": int(sum(x["merge_kernel_launches"] for x in st)),
                 "avg_launch_us": round(us, 3), "bytes_per_launch": round(bpl), "note": note}
@@ -249,9 +272,10 @@ def main():
             return None
         kms, kb = a["count_kernel_ms"], a["count_kernel_bytes"]
         achieved = kb / (kms / 1e3) / 1e9
-        traffic = traffic_of("k_count2")
+        traffic, tsrc = traffic_of("k_count2")
         return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_source": tsrc,
                 "kernel": "k_count2", "launches_per_step": per_step_launches,
                 "timed_launches": len(st) * (per_step_launches or 1), "avg_launch_us": round(kms * 1e3, 3),
                 "bytes_per_launch": kb, "note": note}
@@ -277,7 +301,8 @@ def main():
     dstats = []
     if corpus is not None and not args.no_device_resident:
         def train_dev():
-            return train_bpe_device(corpus.data_ptr(), slab, args.vocab, [EOT], comm=comm)
+            return train_bpe_device(corpus.data_ptr(), slab, args.vocab, [EOT], comm=comm,
+                                    keep_device_buffers=True)
         for _ in range(args.warmup):
             v2, m2 = train_dev()
         L.bpe_set_timing(0 if args.no_timing else 1)
@@ -410,6 +435,8 @@ def main():
                                    "special <|endoftext|> (BASELINE configs[2])",
                        "corpus_bytes": n, "vocab_size": args.vocab, "merges": rounds,
                        "seed": args.seed, "flavour": args.flavour, "parallelism": par},
+            # the timed steps' result against the committed scale golden of this corpus
+            "parity": golden_parity(n, args.seed, args.flavour, args.vocab, vocab, merges),
             "merges_per_s": round(rounds / (avg["t_merge_ms"] / 1e3), 1) if avg["t_merge_ms"] else None,
             "device_resident": device_resident,
             "merge_loop": merge_loop,

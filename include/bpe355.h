@@ -47,7 +47,7 @@ enum {
     BPE_E_ARG = -5,      /* invalid argument */
     BPE_E_NOMEM = -6,    /* device or host allocation failed */
     BPE_E_RCCL = -7,     /* collective failure */
-    BPE_E_LIMIT = -8     /* input exceeds a documented limit (pretoken > 16 MiB, corpus > 1 TiB) */
+    BPE_E_LIMIT = -8     /* input exceeds a documented limit (pre-token >= 8 MiB, corpus > 1 TiB) */
 };
 
 typedef struct bpe_result bpe_result;
@@ -164,6 +164,17 @@ typedef struct {
 int bpe_result_stats(const bpe_result* r, bpe_train_stats* out);
 void bpe_result_free(bpe_result* r);
 
+/* Hands back the device memory the trainer keeps between calls so that a repeated train_bpe
+ * does not pay for fresh allocations: the corpus buffer (drive.hip), the counter's record pool
+ * and aggregation bins (count.hip; about 2 x 2 bytes per corpus byte) and the cached copy
+ * streams, for `device` (< 0: every device).  The reference keeps nothing after train_bpe returns
+ * (train.py:231) and its caller trains an LM on the same GPU next (train.py:230-232), so the
+ * Python train_bpe calls this after every call unless keep_device_buffers=True.  Buffers held by
+ * a call in flight are not touched; it must not run while another call of this library copies
+ * a file on that device.  Tokenizer buffers: bpe_tok_release_buffers.  *freed_bytes (may be
+ * NULL): device bytes handed back. */
+int bpe_release_device_memory(int device, size_t* freed_bytes);
+
 /* Enable per-launch event timing of the hot kernels (bench / profiling); default off. */
 void bpe_set_timing(int enable);
 
@@ -177,7 +188,11 @@ int bpe_tok_create(const uint8_t* vocab_blob, size_t vocab_n, const uint8_t* mer
                    size_t merges_n, const char* const* specials, int n_specials,
                    bpe_tokenizer** out);
 int64_t bpe_tok_special_id(const bpe_tokenizer* tok, int i);
-/* encode(text): UTF-8 bytes in host memory -> ids.  cap >= n always suffices. */
+/* encode(text): UTF-8 bytes in host memory -> ids.  cap >= n always suffices.
+ * Limits of one call (BPE_E_LIMIT): a pre-token under 8 MiB; at most 2^28 word-table slots,
+ * i.e. about 134 M distinct pre-tokens at the table's half load (an 11.9 GB OWT-like text has
+ * 7.5 M).  A text past that is encoded in pieces cut at safe points (bpe_tok_encode_gpus cuts
+ * them that way on one device too), whose concatenated ids are the whole text's. */
 int bpe_tok_encode(bpe_tokenizer* tok, const uint8_t* utf8, size_t n, uint32_t* ids_out,
                    size_t cap, size_t* n_out);
 /* same, device-resident text and output (d_out holds >= n ids) */

@@ -32,9 +32,11 @@ def count_pretokens(text: str, specials) -> dict:
 
 
 def train(text: str, vocab_size: int, specials=(), deadline: float | None = None,
-          round_cap_s: float | None = None):
+          round_cap_s: float | None = None, progress: list | None = None, progress_every: int = 1000):
     """Returns (vocab, merges, info).  info["complete"] is False if the deadline (absolute) or the
-    cap on the merge rounds' wall time (from the end of the count) stopped it."""
+    cap on the merge rounds' wall time (from the end of the count) stopped it.  `progress`, when
+    given, receives (rounds done, seconds since the start, live pairs) every `progress_every`
+    rounds (tools/cpu_port_full.py uses it to check the bench's flat-rate extrapolation)."""
     t0 = time.perf_counter()
     vocab_list: list = []
     present = set()
@@ -102,6 +104,8 @@ def train(text: str, vocab_size: int, specials=(), deadline: float | None = None
         where.pop((a, b), None)
         merges.append((a, b))
         done += 1
+        if progress is not None and done % progress_every == 0:
+            progress.append((done, time.perf_counter() - t0, len(pairs)))
     info = {"complete": done == max(0, rounds) or not pairs, "rounds_done": done,
             "rounds_total": max(0, rounds), "t_count_s": t_count,
             "t_merge_s": time.perf_counter() - t0 - t_count, "t_build_s": t_build, "n_words": len(words)}

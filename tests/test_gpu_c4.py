@@ -114,18 +114,32 @@ def test_c4_eight_ranks_words_full_owt(inproc):
                        **{k: st[k] for k in keep}}, f, indent=1)
 
 
-def test_c4_two_ranks_rounds_1g(inproc):
-    """the SURVEY's per-round protocol (one sum all-reduce of the delta cells per merge round,
-    replicated pair tables and argmax on every rank) on the 1 GB C3 prefix at vocab 32k; the
-    driver also requires both ranks to have chosen the same merges"""
+@pytest.mark.parametrize("ranks", [2, 8])
+def test_c4_ranks_rounds_1g(inproc, ranks):
+    """the SURVEY's per-round protocol (one sum all-reduce of the delta cells per merge
+    round, replicated pair tables and argmax on every rank; reference train.py:183-228) on the
+    1 GB C3 prefix at vocab 32k, at 2 and 8 ranks; the driver also requires every rank to have
+    chosen the same merges"""
     o = _load("train", "C3_1G")
     buf = np.empty(o["n"], dtype=np.uint8)
     assert _lib.lib().bpe_synth_corpus_host(buf.ctypes.data, o["n"], o["seed"], o["flavour"], 0, 16) == 0
     inproc.setenv("BPE355_EXCHANGE", "rounds")
-    bpe_amd.set_num_gpus(2)
+    bpe_amd.set_num_gpus(ranks)
     vocab, merges = bpe_amd.train_bpe_bytes(buf.tobytes(), o["vocab"], o["specials"])
-    assert last_train_stats()["n_gpus"] == 2
-    _check(o, vocab, merges, "C3_1G rounds x2")
+    st = last_train_stats()
+    assert st["n_gpus"] == ranks
+    _check(o, vocab, merges, f"C3_1G rounds x{ranks}")
+    out = os.environ.get("BPE355_STATS_OUT")
+    if out:   # DESIGN.md section 5: the per-round mode's merge loop beside the words mode
+        p = pathlib.Path(out)
+        p = p.with_name(f"{p.stem}_rounds{ranks}{p.suffix}")
+        keep = ("t_total_ms", "t_count_ms", "t_words_ms", "t_merge_ms", "n_rounds_device", "n_gpus")
+        with open(p, "w") as f:
+            json.dump({"test": f"test_c4_ranks_rounds_1g[{ranks}]",
+                       "ranks": f"{ranks} in-process ranks sharing one GPU; per-round all-reduce through "
+                                "host memory (the in-process communicator)",
+                       "us_per_round": round(st["t_merge_ms"] * 1e3 / max(1, st["n_rounds_device"]), 2),
+                       **{k: st[k] for k in keep}}, f, indent=1)
 
 
 def test_c5_encode_eight_devices(inproc):

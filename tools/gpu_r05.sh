@@ -1,0 +1,53 @@
+#!/bin/bash
+# Round-5 GPU call.  usage: tools/gpu_r05.sh TAG [tests|quick|bench|prof|c4] ...
+#   quick: the tests this round added or changed; tests: the whole -m gpu suite + smoke;
+#   bench: the default bench line (CPU baselines included); prof: rocprofv3 kernel summary of the
+#   HBM-resident bench; c4: the 8-rank words exchange stats + rounds-mode stats.
+set -o pipefail
+TAG=${1:-r05}
+shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+for step in "$@"; do
+  case $step in
+  quick)
+    timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_release.py tests/test_gpu_limits.py "tests/test_gpu_c4.py::test_c4_ranks_rounds_1g" tests/test_gpu_train.py tests/test_gpu_encode.py > $OUT/pytest_quick.log 2>&1 || { echo "quick tests failed"; tail -40 $OUT/pytest_quick.log; exit 1; }
+    tail -1 $OUT/pytest_quick.log ;;
+  scale)
+    timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_scale.py > $OUT/pytest_scale.log 2>&1 || { echo "scale tests failed"; tail -40 $OUT/pytest_scale.log; exit 1; }
+    tail -1 $OUT/pytest_scale.log ;;
+  tests)
+    timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }
+    tail -1 $OUT/pytest_gpu.log
+    timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; tail -30 $OUT/smoke.log; exit 1; }
+    tail -1 $OUT/smoke.log ;;
+  bench)
+    timeout -k 10 600 python -u bench.py --keep-corpus > $OUT/bench.log 2>&1 || { echo "bench failed"; tail -30 $OUT/bench.log; exit 1; }
+    tail -1 $OUT/bench.log | cut -c1-600 ;;
+  benchfast)
+    timeout -k 10 400 python -u bench.py --keep-corpus --no-cpu-baseline --steps 3 > $OUT/benchfast.log 2>&1 || { echo "bench failed"; tail -30 $OUT/benchfast.log; exit 1; }
+    tail -1 $OUT/benchfast.log | cut -c1-600 ;;
+  prof)
+    cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run -- python3 -u $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-file --steps 2 --warmup 1 --keep-corpus > $GRAFT_REPO_ROOT/$OUT/bench_prof.log 2>&1 || { echo "rocprof failed"; tail -30 $GRAFT_REPO_ROOT/$OUT/bench_prof.log; exit 1; }
+    cd $GRAFT_REPO_ROOT
+    python3 tools/rocprof_summary.py $(find $OUT/prof -name "*.db" | head -1) > $OUT/kernel_stats.txt 2>&1
+    head -24 $OUT/kernel_stats.txt
+    rm -rf $OUT/prof ;;
+  abfold)   # merge phase, fused trip kernel vs k_select + k_merge_batch, corpus in HBM, alternating
+    for rep in 1 2; do for f in 1 0; do
+      BPE355_FOLD=$f timeout -k 10 300 python -u bench.py --no-file --no-encode --no-cpu-baseline --steps 3 --warmup 1 > $OUT/abfold_${f}_$rep.log 2>&1 || { echo "abfold failed"; tail -20 $OUT/abfold_${f}_$rep.log; exit 1; }
+      python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().split(chr(10))[-1]); m=d['merge_loop']; print('FOLD=$f rep $rep merge_ms', m['ms'], 'us_per_trip', m['us_per_trip'], 'k_us', m['k_merge_batch_us'], 'parity', d['parity']['parity'])" $OUT/abfold_${f}_$rep.log
+    done; done ;;
+  probe)   # the merge-loop probe (build/variants/probe), fused and unfused
+    for f in 1 0; do
+      BPE355_FOLD=$f BPE355_PROBE=1 BPE355_LIB=build/variants/probe/libbpe355.so timeout -k 10 200 python -u bench.py --no-file --steps 1 --warmup 0 --no-encode --no-cpu-baseline --no-timing > $OUT/probe_$f.log 2> $OUT/probe_err_$f.log || { echo "probe failed"; tail -5 $OUT/probe_err_$f.log; exit 1; }
+      grep probe $OUT/probe_err_$f.log | head -12
+    done ;;
+  c4)
+    BPE355_STATS_OUT=$OUT/c4_exchange.json timeout -k 10 600 python -u -m pytest tests/test_gpu_c4.py -x -q --timeout 380 --timeout-method thread -k "words_full or rounds" > $OUT/c4.log 2>&1 || { echo "c4 failed"; tail -20 $OUT/c4.log; exit 1; }
+    cat $OUT/c4_exchange*.json ;;
+  esac
+done
+rm -f /tmp/bpe355_bench_*
+echo done

@@ -96,6 +96,7 @@ _SIGS = [
                                            ctypes.POINTER(_P), ctypes.POINTER(_SZ)]),
     ("bpe_result_stats", ctypes.c_int, [_P, ctypes.POINTER(TrainStats)]),
     ("bpe_result_free", None, [_P]),
+    ("bpe_release_device_memory", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_SZ)]),
     ("bpe_set_timing", None, [ctypes.c_int]),
     ("bpe_tok_create", ctypes.c_int, [_U8P, _SZ, _U8P, _SZ, ctypes.POINTER(ctypes.c_char_p),
                                       ctypes.c_int, ctypes.POINTER(_P)]),

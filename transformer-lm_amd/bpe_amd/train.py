@@ -14,7 +14,7 @@ from typing import List
 from . import _lib
 
 __all__ = ["train_bpe", "train_bpe_bytes", "train_bpe_device", "last_train_stats", "set_num_gpus",
-           "num_gpus"]
+           "num_gpus", "release_device_memory"]
 
 _last_stats: dict = {}
 _num_gpus: int | None = None
@@ -39,21 +39,43 @@ def last_train_stats() -> dict:
     return dict(_last_stats)
 
 
-def _finish(rc, res, what):
+def release_device_memory(device: int = -1) -> int:
+    """Hand back the device memory the trainer keeps between calls (the corpus buffer, the
+    counter's record pool and bins, the copy streams) on `device` (-1: every device); returns the
+    bytes freed.  train_bpe calls it after every call unless keep_device_buffers=True."""
+    L = _lib.lib()
+    freed = ctypes.c_size_t(0)
+    _lib.check(L.bpe_release_device_memory(int(device), ctypes.byref(freed)), "release_device_memory")
+    return int(freed.value)
+
+
+def _finish(rc, res, what, keep_device_buffers=True):
     global _last_stats
-    _lib.check(rc, what)
-    vocab, merges, stats = _lib.take_result(res)
+    try:
+        _lib.check(rc, what)
+        vocab, merges, stats = _lib.take_result(res)
+    finally:
+        # the reference holds nothing once train_bpe returns (train.py:231), and its caller trains
+        # the LM on the same GPU next (train.py:230-232)
+        if not keep_device_buffers:
+            try:
+                release_device_memory(-1)
+            except Exception:
+                if rc == 0:   # never hide the call's own error behind the release's
+                    raise
     _last_stats = stats
     return vocab, merges
 
 
 def train_bpe(input_path: str | os.PathLike, vocab_size: int, special_tokens: List[str] = [],
-              comm=None, split_file: bool = False):
+              comm=None, split_file: bool = False, keep_device_buffers: bool = False):
     """Train a byte-level BPE on the file at input_path (reference train.py:142-231).
 
     Without comm: one process on num_gpus() devices (set_num_gpus / BPE355_GPUS).
     comm: a bpe_amd.dist.Communicator (one process per GPU); the file is this rank's slab, or
     with split_file=True the whole corpus, of which each rank reads its share.
+    keep_device_buffers: keep the corpus buffer and the counter's scratch (~5 bytes of HBM per
+    corpus byte) for the next call instead of freeing them on return (bench.py's repeated steps).
     """
     L = _lib.lib()
     arr, n, _keep = _lib.c_strings(special_tokens)
@@ -64,10 +86,11 @@ def train_bpe(input_path: str | os.PathLike, vocab_size: int, special_tokens: Li
                                    ctypes.byref(res))
     else:
         rc = L.bpe_train_file(path, int(vocab_size), arr, n, num_gpus(), ctypes.byref(res))
-    return _finish(rc, res, f"train_bpe({os.fspath(input_path)!r})")
+    return _finish(rc, res, f"train_bpe({os.fspath(input_path)!r})", keep_device_buffers)
 
 
-def train_bpe_bytes(data: bytes, vocab_size: int, special_tokens: List[str] = [], comm=None):
+def train_bpe_bytes(data: bytes, vocab_size: int, special_tokens: List[str] = [], comm=None,
+                    keep_device_buffers: bool = False):
     """train_bpe on the raw bytes of a file (decoded exactly like the file would be)."""
     L = _lib.lib()
     arr, n, _keep = _lib.c_strings(special_tokens)
@@ -78,11 +101,11 @@ def train_bpe_bytes(data: bytes, vocab_size: int, special_tokens: List[str] = []
     else:
         rc = L.bpe_train_buffer_gpus(data, len(data), int(vocab_size), arr, n, num_gpus(),
                                      ctypes.byref(res))
-    return _finish(rc, res, "train_bpe_bytes")
+    return _finish(rc, res, "train_bpe_bytes", keep_device_buffers)
 
 
 def train_bpe_device(d_ptr: int, n: int, vocab_size: int, special_tokens: List[str] = [],
-                     comm=None, stream: int = 0):
+                     comm=None, stream: int = 0, keep_device_buffers: bool = False):
     """train_bpe on raw bytes already resident in device memory (e.g. a torch uint8 CUDA
     tensor's data_ptr()); used by bench.py so the timed region starts with data in HBM."""
     L = _lib.lib()
@@ -91,4 +114,4 @@ def train_bpe_device(d_ptr: int, n: int, vocab_size: int, special_tokens: List[s
     rc = L.bpe_train_device(ctypes.c_void_p(d_ptr), n, int(vocab_size), arr, k,
                             comm.handle if comm else None, ctypes.c_void_p(stream or None),
                             ctypes.byref(res))
-    return _finish(rc, res, "train_bpe_device")
+    return _finish(rc, res, "train_bpe_device", keep_device_buffers)

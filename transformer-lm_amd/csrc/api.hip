@@ -12,6 +12,7 @@
 #include <string>
 #include <vector>
 
+#include "count.h"
 #include "drive.h"
 #include "internal.h"
 
@@ -180,6 +181,19 @@ int bpe_runtime_info(int* compiled_hip_version, int* runtime_hip_version, char* 
 const char* bpe_last_error(void) { return bpe::g_err.c_str(); }
 int bpe_last_errno(void) { return bpe::g_errno; }
 void bpe_set_timing(int enable) { bpe::g_timing = enable != 0; }
+
+int bpe_release_device_memory(int device, size_t* freed_bytes) {
+    return bpe::guarded([&] {
+        if (freed_bytes) *freed_bytes = 0;
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+        BPE_REQUIRE(device < n, BPE_E_ARG, "device " + std::to_string(device) + " is not visible");
+        size_t b = bpe::corpus_release(device);
+        b += bpe::scratch_release(device);
+        bpe::dma_release(device);
+        if (freed_bytes) *freed_bytes = b;
+    });
+}
 
 int bpe_device_count(void) {
     int n = 0;

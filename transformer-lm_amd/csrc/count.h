@@ -43,7 +43,7 @@ struct Arrays3 {
 std::unique_ptr<Arrays3> scratch_take(size_t cap);   // exclusive until given back
 void scratch_give(std::unique_ptr<Arrays3> x);
 size_t scratch_cached_bytes(int dev);   // free sets of this device held by the cache
-void scratch_release(int dev);          // hand them back to the device allocator
+size_t scratch_release(int dev);        // hand them back to the device allocator (dev < 0: all); bytes
 
 // a level-2 work item of the record aggregation: a tile of one coarse bin's run
 struct L2Tile {

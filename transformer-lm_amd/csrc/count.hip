@@ -729,16 +729,30 @@ size_t scratch_cached_bytes(int dev) {
     return b;
 }
 
-void scratch_release(int dev) {
+size_t scratch_release(int dev) {
     std::vector<std::unique_ptr<Arrays3>> drop;
+    size_t bytes = 0;
     {
         std::lock_guard<std::mutex> g(scratch().m);
         auto& f = scratch().free_;
         for (size_t i = 0; i < f.size();)
-            if (f[i]->dev == dev) { drop.push_back(std::move(f[i])); f.erase(f.begin() + i); }
-            else ++i;
+            if (dev < 0 || f[i]->dev == dev) {
+                bytes += 3 * f[i]->cap * sizeof(uint64_t);
+                drop.push_back(std::move(f[i]));
+                f.erase(f.begin() + i);
+            } else {
+                ++i;
+            }
     }
-    drop.clear();   // hipFree outside the lock
+    if (drop.empty()) return bytes;
+    int cur = 0;
+    BPE_HIP(hipGetDevice(&cur));
+    for (auto& x : drop) {   // hipFree outside the lock, on the arrays' own device
+        (void)hipSetDevice(x->dev);
+        x.reset();
+    }
+    BPE_HIP(hipSetDevice(cur));
+    return bytes;
 }
 
 void scratch_give(std::unique_ptr<Arrays3> x) {

@@ -49,5 +49,9 @@ void train_source(const Source& src, int vocab_size, const std::vector<std::stri
 // of which this rank reads its share
 void train_source_comm(const Source& src, bool split, int vocab_size, const std::vector<std::string>& specials,
                        Comm* comm, TrainOutput& out);
+// bpe_release_device_memory: the corpus buffers kept for `dev` (< 0: every device) go back to the
+// device allocator, and the device's cached copy streams are destroyed; returns the bytes freed
+size_t corpus_release(int dev);
+void dma_release(int dev);
 
 }  // namespace bpe

@@ -177,6 +177,32 @@ void corpus_give(std::unique_ptr<CorpusBuf> x) {
 
 }  // namespace
 
+size_t corpus_release(int dev) {
+    std::vector<std::unique_ptr<CorpusBuf>> drop;
+    size_t bytes = 0;
+    {
+        std::lock_guard<std::mutex> g(corpus_cache().m);
+        auto& f = corpus_cache().free_;
+        for (size_t i = 0; i < f.size();)
+            if (dev < 0 || f[i]->dev == dev) {
+                bytes += f[i]->b.bytes();
+                drop.push_back(std::move(f[i]));
+                f.erase(f.begin() + i);
+            } else {
+                ++i;
+            }
+    }
+    if (drop.empty()) return bytes;
+    int cur = 0;
+    BPE_HIP(hipGetDevice(&cur));
+    for (auto& x : drop) {   // hipFree outside the lock, on the buffer's own device
+        (void)hipSetDevice(x->dev);
+        x->b.release();
+    }
+    BPE_HIP(hipSetDevice(cur));
+    return bytes;
+}
+
 // Reader threads and DMA streams of one transfer.  Measured on MI355X boxes with a page-cache-warm
 // 11.9 GB file (tools/microbench/numa_ab.hip, profiles/r03/e_load_ab.txt): DMA alone runs at
 // 50-52 GB/s on 1-2 streams but 37 GB/s on 16; pread alone at 45 GB/s on 16 threads; together,
@@ -243,20 +269,43 @@ struct DmaStreams {
 // stage_to_device / device_to_host; streams made and destroyed per call cost a round trip each,
 // and the two directions keep separate streams so that host-to-device and device-to-host copies
 // run side by side.
+// Index (device, dir, priority).  BPE355_D2H_PRIO is read per call, so its A/B switches between
+// two sets of streams within one process.
+struct DmaCache {
+    std::mutex m;
+    std::vector<DmaStreams*> made;
+};
+DmaCache& dma_cache() {
+    static DmaCache* c = new DmaCache;   // lives as long as the process
+    return *c;
+}
 const DmaStreams& cached_dma(int device, int dir) {
-    static std::mutex m;
-    static std::vector<DmaStreams*> made;   // index (device, dir)
-    std::lock_guard<std::mutex> g(m);
-    const size_t i = (size_t)device * 2 + (size_t)dir;
-    if (made.size() <= i) made.resize(i + 1, nullptr);
     // device-to-host copies run at the least priority: HIP serves them with a copy kernel, whose
     // workgroups should yield the CUs to the encode beside it (BPE355_D2H_PRIO=0: normal priority)
     const char* pe = std::getenv("BPE355_D2H_PRIO");
     const bool low = dir == 1 && !(pe && pe[0] == '0');
-    if (!made[i]) made[i] = new DmaStreams(device, dma_streams(), low);
-    return *made[i];
+    DmaCache& c = dma_cache();
+    std::lock_guard<std::mutex> g(c.m);
+    const size_t i = (size_t)device * 4 + (size_t)dir * 2 + (low ? 1 : 0);
+    if (c.made.size() <= i) c.made.resize(i + 1, nullptr);
+    if (!c.made[i]) c.made[i] = new DmaStreams(device, dma_streams(), low);
+    return *c.made[i];
 }
 }  // namespace
+
+void dma_release(int dev) {
+    std::vector<DmaStreams*> drop;
+    {
+        DmaCache& c = dma_cache();
+        std::lock_guard<std::mutex> g(c.m);
+        for (size_t i = 0; i < c.made.size(); ++i)
+            if (c.made[i] && (dev < 0 || (int)(i / 4) == dev)) {
+                drop.push_back(c.made[i]);
+                c.made[i] = nullptr;
+            }
+    }
+    for (auto* d : drop) delete d;   // synchronises, then destroys each stream
+}
 
 // ------------------------------------------------------------------ sources
 Source Source::open_path(const char* path) {

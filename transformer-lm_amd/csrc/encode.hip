@@ -423,10 +423,12 @@ struct ClipWin {   // one block's window with the bytes before window position l
 // The encoder's word table, over the training table's arrays (kv: 16-byte entries, pos): the
 // encoder counts nothing, so an entry's second word holds the word's first 8 bytes and a probe
 // is one 16-byte load, with no read of the text to verify a key:
-//   words of <= 15 bytes: kv[2s] = kInl | len << 56 | bytes 8..14, kv[2s + 1] = bytes 0..7
-//     (claimed by a CAS on the first word, then the second stored: a reader that sees the first
-//     before the second may miss the word and insert it again further on -- a duplicate slot,
-//     which encodes to the same ids);
+//   words of <= 15 bytes: kv[2s] = kInl | len << 56 | bytes 8..14, kv[2s + 1] = ~(bytes 0..7)
+//     (claimed by a CAS on the first word, then the second stored; it is never 0 -- that would
+//     take eight 0xFF bytes, which valid UTF-8 never holds -- so 0 means "not stored yet" and
+//     matches no word, not even one of NUL bytes.  A reader that sees the first word before the
+//     second may miss the word and insert it again further on -- a duplicate slot, which encodes
+//     to the same ids);
 //   longer words: kv[2s] = len << 40 | (offset + 1) of an occurrence, verified against the text.
 // pos[s] = an occurrence's offset (k_collect reads (offset, len) of every slot as before).
 constexpr int kEncInline = 15;
@@ -446,7 +448,7 @@ __device__ __forceinline__ size_t enc_table_add(const uint8_t* __restrict__ s, s
         if (k == 0) {
             k = atomicCAS(&kv[2 * slot], 0ULL, mine);
             if (k == 0) {   // claimed
-                if (inl) kv[2 * slot + 1] = wl;
+                if (inl) kv[2 * slot + 1] = ~wl;
                 pos[slot] = gp;
                 *inserted = true;
                 return slot;
@@ -454,7 +456,7 @@ __device__ __forceinline__ size_t enc_table_add(const uint8_t* __restrict__ s, s
             k0 = kv[2 * slot + 1];
         }
         if (inl) {
-            if (k == mine && k0 == wl) return slot;
+            if (k == mine && k0 == ~wl) return slot;
         } else if (!(k & kInl) && (k >> 40) == len) {
             const size_t q = (k & kOffMask) - 1;
             bool eq = true;
@@ -763,7 +765,7 @@ __global__ void __launch_bounds__(256, BPE355_ENC_SCAN_WG) k_enc_scan4(ScanArgs 
                             if (rec == kRecNone) rec = pending(1, gp, 0, 0, false);
                         } else if (len <= (size_t)kInline) {
                             rec = short_rec(r, len, gp);
-                        } else if (len >= (1ULL << kPendShift)) {
+                        } else if (len >= kMaxPretok) {
                             atomicOr(A.status, 2u);
                             rec = kRecSlot;
                         } else {
@@ -1817,14 +1819,15 @@ size_t encode_device(bpe_tokenizer& T, const uint8_t* d_text, size_t n, OutT* d_
         }
         unsigned st = 0;
         to_host(&st, status.p, 4, s);
-        if (st & 2u) throw Error{BPE_E_LIMIT, "a pre-token is longer than 16 MiB"};
+        if (st & 2u) throw Error{BPE_E_LIMIT, "a pre-token is 8 MiB or longer"};
         BPE_REQUIRE(!(st & 16u), BPE_E_HIP, "internal error: encode scan found an empty pre-token");
-        BPE_REQUIRE(attempt < 8, BPE_E_NOMEM, "word table overflow");
         if (st & 1u) {
+            BPE_REQUIRE(attempt < 8, BPE_E_NOMEM, "word table overflow");
             cap *= 4;
             continue;
         }
         if (st & 256u) {   // more pre-tokens than guessed: one per byte at most
+            BPE_REQUIRE(attempt < 8, BPE_E_HIP, "internal error: encode records overflow (retries)");
             BPE_REQUIRE(rec_cap < rec_cap_max, BPE_E_HIP, "internal error: encode records overflow");
             rec_cap = rec_cap_max;
             continue;

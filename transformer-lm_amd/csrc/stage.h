@@ -29,6 +29,9 @@ constexpr int kWin = kChunk + kHalo;
 constexpr int kPadded = kWin + (kWin / 64) * 4;   // +4 B per 64 B: threads' spans hit distinct banks
 constexpr int kVec = (kWin + 16 * 256 - 1) / (16 * 256);   // 16-B loads per thread per chunk
 constexpr unsigned long long kBusy = 1ULL << 63;
+// Longest pre-token the tables key: len << 40 must stay clear of bit 63 (kInl), so len < 2^23.
+// A longer one fails the call with BPE_E_LIMIT (status bit 2), in training and in encoding.
+constexpr unsigned long long kMaxPretok = 1ULL << 23;
 
 __host__ __device__ inline uint64_t short_hash(uint64_t lo, uint64_t hi, size_t len) {
     return mix64(lo ^ mix64(hi ^ (len << 56) ^ 0x9E3779B97F4A7C15ULL));
@@ -66,6 +69,10 @@ __device__ __forceinline__ size_t table_add(const uint8_t* __restrict__ s, const
                                             unsigned* __restrict__ status, bool* inserted) {
     *inserted = false;
     const bool inl = len <= (size_t)kInlineKey;
+    if (len >= kMaxPretok) {   // its key would read as an inline word
+        atomicOr(status, 2u);
+        return ~(size_t)0;
+    }
     const unsigned long long mine = inl ? kInl | ((unsigned long long)len << 56) | wl
                                         : ((unsigned long long)len << 40) | (p + 1);
     size_t slot = h & mask;

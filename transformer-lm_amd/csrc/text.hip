@@ -269,7 +269,7 @@ __global__ void __launch_bounds__(256, 3) k_count_words(const uint8_t* __restric
         if (len < 2) return;
         ++ntok;
         if (mode == 1) return;   // analysis knob (BPE355_COUNT_MODE=1): the scan alone
-        if (len >= (1ULL << 24)) {
+        if (len >= kMaxPretok) {
             atomicOr(status, 2u);
         } else if (len <= kInline) {
             uint64_t wl = 0, wh = 0;
@@ -579,7 +579,7 @@ bool CountPass::finish() {
     BPE_HIP(hipMemcpyAsync(&st, status.p, 4, hipMemcpyDeviceToHost, s));
     BPE_HIP(hipMemcpyAsync(&wc.n_pretokens, ntok.p, 8, hipMemcpyDeviceToHost, s));
     BPE_HIP(hipStreamSynchronize(s));
-    if (st & 2u) throw Error{BPE_E_LIMIT, "a pre-token is longer than 16 MiB"};
+    if (st & 2u) throw Error{BPE_E_LIMIT, "a pre-token is 8 MiB or longer"};
     for (size_t i = 0; i + 1 < ev.size(); i += 2) {
         float ms = 0;
         BPE_HIP(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));

@@ -74,6 +74,8 @@ struct RoundState {
     int new_is_new;
     unsigned err;
     unsigned n_single;
+    unsigned n_single_new;      // batched: words the current trip's rewrite made single (the apply folds
+                                // them into n_single, which the trip's own select phase reads)
     unsigned pool_used, pool_cap;
     unsigned long long pair_used;
     unsigned long long scan_slots;
@@ -922,7 +924,7 @@ struct BatchMember {
     unsigned ln, list_beg, list_len, use_list, cov_beg, cov_len, pool_off, isnew;
 };
 struct Batch {
-    int stop;            // 0 run, -1 nothing to do
+    int stop;            // 0 run, -1 nothing to do, > 0 the halt the apply raises
     int k;               // members
     int round, ntok;     // round of member 0, token count before the batch
     int trip, prev_k;    // trip number (cell parity), members of the previous trip
@@ -931,6 +933,10 @@ struct Batch {
     unsigned n_fresh;    // members that create a token
     unsigned nC_base;    // C entries before this trip's admissions (the apply scans them)
     unsigned idle_from;  // list mode: merge threads from this index on have no word (~0: scan mode)
+    // state the select decided that its own kernel must not see change (every workgroup of the
+    // fused trip kernel runs the select on the same inputs): the apply publishes them
+    unsigned pool_after; // st->pool_used after this trip's new tokens
+    long long T2next;    // the candidate-list threshold of this trip's apply (-> bs->T2)
     unsigned list_pre[kMaxBatch + 1];   // prefix sums of the members' list lengths
     BatchMember m[kMaxBatch];
 };
@@ -944,15 +950,17 @@ struct BatchState {
     unsigned long long rounds_batched;   // statistics: rounds taken in batches of k > 1
     unsigned long long trips_batched;
     long long T2;            // candidate-list threshold (>= T): every present key >= T2 is listed
-    unsigned list_n;         // keys the apply appended to the list (> kListCap: overflow)
-    unsigned pad;
+    // keys the apply appended to the list, by trip parity: trip t's select reads list (t & 1), its
+    // apply fills list ((t + 1) & 1) (> kListCap: overflow)
+    unsigned list_n[2];
     unsigned long long n_overflow, n_headmiss, n_short, k_hist[kMaxBatch + 1];   // diagnostics
     unsigned long long k1_why[6];   // single-merge trips: P1 a == b / P1 not fresh / no list / P2 fails / tie / end
 };
-// the candidate list k_select ranks, one thread per entry (build knob BPE355_LIST_CAP, a multiple
-// of 64; a trip whose list overflows it takes P1 alone and raises T2)
+// the candidate list the select ranks in its wave 0, one or two entries per lane (build knob
+// BPE355_LIST_CAP, 64 or 128; a trip whose list overflows it takes P1 alone and raises T2).  128
+// and 256 measured alike with the r04 select (zk_list_cap_ab.txt)
 #ifndef BPE355_LIST_CAP
-#define BPE355_LIST_CAP 256
+#define BPE355_LIST_CAP 128
 #endif
 constexpr unsigned kListCap = BPE355_LIST_CAP;
 static_assert(kListCap % 64 == 0 && kListCap >= 64, "whole waves of list threads");
@@ -1050,6 +1058,10 @@ __device__ __forceinline__ void cand_meta(const Cand& c, const ToksDev& K, const
 // look up its entries' metadata and rank them.  All global loads are issued before the first
 // barrier, so the kernel costs about one memory round trip plus the dedupe lookups' chain, then
 // the ranking, the rule and the record (wave 0).
+#ifndef BPE355_LIST_TARGET
+#define BPE355_LIST_TARGET 48
+#endif
+constexpr unsigned kListTarget = BPE355_LIST_TARGET;   // keys the next list should hold (T2 control)
 // waves of k_select that reduce the apply's partials (kPartPer each per thread); the list's waves
 // follow them (build knob BPE355_SEL_PART_WAVES).  4 waves with two partials per thread: a 512-
 // thread select, 252.2-253.7 ms of HBM-resident merges against 255.0-268.0 with 8 waves and
@@ -1058,64 +1070,99 @@ __device__ __forceinline__ void cand_meta(const Cand& c, const ToksDev& K, const
 #define BPE355_SEL_PART_WAVES 4
 #endif
 constexpr int kSelListWave = BPE355_SEL_PART_WAVES;   // first wave of the list
-#ifndef BPE355_LIST_TARGET
-#define BPE355_LIST_TARGET 48
-#endif
-constexpr unsigned kListTarget = BPE355_LIST_TARGET;   // keys the next list should hold (T2 control)
 constexpr bool kSelMetaAll = true;     // metadata of every listed key before the ranking
 constexpr int kSelThreads = 64 * kSelListWave + (int)kListCap;
-__global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__ st, BatchState* __restrict__ bs,
-                                                        PairsDev P, ToksDev K, IndexDev X, Batch* __restrict__ bt,
-                                                        const Partial* __restrict__ part,
-                                                        const Partial* __restrict__ list,
-                                                        uint32_t* __restrict__ m_a, uint32_t* __restrict__ m_b,
-                                                        uint32_t* __restrict__ m_new, uint32_t* __restrict__ m_mode,
-                                                        long long* __restrict__ m_cnt, int* __restrict__ trip_info,
-                                                        int trip_slot) {
-    // each thread of the partial waves reduces kPartPer partials
-    constexpr int kPartPer = (int)((kApplyGrid + 64 * kSelListWave - 1) / (64 * kSelListWave));
+// k_trip workgroups: 256 threads (four per CU).  One 1024-thread workgroup per CU decided faster
+// (the partials' re-reads by four workgroups per CU cost 1.3 us) but left an 11.8 us merge ->
+// apply gap: 289 vs 258 ms of merges (profiles/r05/d_fold_ab.txt)
+constexpr unsigned kTripThreads = 256;
+
+// The LDS of one batch decision
+struct SelLds {
+    Cand wave[8];                     // the partial waves' bests
+    Cand all[kListCap];
+    SelKey topkey[kListCap];          // the entries with fewer than kTopM larger counts,
+    unsigned top[kListCap];           // packed for the exact ranking (key, list index)
+    long long cnt[kListCap];
+    Cand list[kTopM];
+    TokMetaS meta[kTopM];
+    unsigned nw_old[kTopM];
+    Cand p1;                          // the exact best (wave 0, beside the ranking)
+    long long cnt_target, cnt_last;   // counts at sorted positions kListTarget - 1, ln - 1
+    unsigned ntop;
+};
+
+// where the publishing workgroup records a batch decision for the host (round records, the
+// block's trip records)
+struct SelOut {
+    uint32_t *m_a, *m_b, *m_new, *m_mode;
+    long long* m_cnt;
+    int* trip_info;
+    int trip_slot;
+};
+
+// The batch of a trip: reduce the apply's per-workgroup partials to the exact best candidate P1,
+// rank the candidate list (every present key >= T2) and apply the batch rule.  All global loads
+// are issued first, so the decision costs about one memory round trip plus the dedupe lookups'
+// chain, then the ranking, the rule and the record (wave 0).
+//   kNT = kSelThreads (k_select, one workgroup): waves 0-3 reduce the partials while the list
+//         waves rank;
+//   kNT = 256 (k_trip: EVERY workgroup of the fused trip kernel decides the same batch): each
+//         thread reduces two partials and holds one list entry.
+// The decision goes to OB (stop != 0: no trip this time; > 0 a halt code the apply raises).
+// It reads only state that no kernel of the trip changes before the apply: the select phase of
+// k_trip runs in every workgroup while other workgroups already rewrite, so everything it decides
+// from (st->n_single, pool_used, halt, the list counts, batch_seq, T2) is updated by the apply,
+// from the batch record.  `pub`: this workgroup publishes (the round records, trip records, the
+// next list's counter, the statistics).  The caller's barrier makes OB visible.
+template <int kNT>
+__device__ __forceinline__ void select_core(const RoundState* __restrict__ st, BatchState* __restrict__ bs,
+                                            const ToksDev& K, const IndexDev& X,
+                                            const Partial* __restrict__ part, const Partial* __restrict__ lists,
+                                            Batch& OB, SelLds& S, const SelOut& O, const bool pub) {
+    static_assert(kNT == kSelThreads || kNT == 256 || kNT == 1024,
+                  "k_select's shape, or one k_trip workgroup of 256 or 1024 threads");
+    // threads that reduce partials (the first kPartT) and the list thread of each entry (a
+    // 1024-thread k_trip workgroup decides as k_select does; its other waves wait at the barriers)
+    constexpr int kPartT = kNT == 256 ? kNT : 64 * kSelListWave;
+    constexpr int kPartW = kPartT / 64;
+    constexpr int kListT0 = kNT == 256 ? 0 : 64 * kSelListWave;
+    static_assert(kPartW <= 8 && (int)kListCap <= kNT - kListT0, "one list entry per list thread");
+    constexpr int kPartPer = (int)((kApplyGrid + kPartT - 1) / kPartT);
     static_assert(kPartPer >= 1 && kPartPer <= 4, "partials per thread of the partial waves");
-    __shared__ Cand s_wave[kSelListWave];
-    __shared__ Cand s_all[kListCap];
-    __shared__ SelKey s_topkey[kListCap];          // the entries with fewer than kTopM larger counts,
-    __shared__ unsigned s_top[kListCap], s_ntop;   // packed for the exact ranking (key, list index)
-    __shared__ Cand s_p1;                          // the exact best (wave 0, beside the ranking)
-    __shared__ Cand s_list[kTopM];
-    __shared__ long long s_cnt[kListCap];
-    __shared__ long long s_cnt_target, s_cnt_last;   // counts at sorted positions kListTarget - 1, ln - 1
-    __shared__ unsigned s_nw_old[kTopM];
-    __shared__ TokMetaS s_meta[kTopM];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int ptrip = bs->trip;
-    if (tid == 0) {
+    if (pub && tid == 0) {
         probe_stamp(st, ptrip, 0);
         if (BPE355_PROBE_CODE && ptrip > 0 && st->probe && ((ptrip - 1) % kProbeTrip) == 0)
             st->probe[kProbeSlots * (size_t)((ptrip - 1) / kProbeTrip) + 16] = __builtin_amdgcn_s_memrealtime();
     }
     // ---- every independent load first
     Partial q[kPartPer] = {};
-    if (wv < kSelListWave) {   // the buffer holds kApplyBatchBlocks entries
+    if (tid < kPartT) {   // the buffer holds kApplyGrid entries
 #pragma unroll
         for (int u = 0; u < kPartPer; ++u)
-            if (tid + u * 64 * kSelListWave < (int)kApplyGrid) q[u] = part[tid + u * 64 * kSelListWave];
+            if (tid + u * kPartT < (int)kApplyGrid) q[u] = part[tid + u * kPartT];
     }
+    const Partial* list = lists + (size_t)(ptrip & 1) * kListCap;   // this trip's list (trip parity)
     Partial lq{};
-    const int li = tid - 64 * kSelListWave;   // list entry of this thread (>= 0: list waves)
+    // list entry of this thread (>= 0: list threads)
+    const int li = tid >= kListT0 && tid < kListT0 + (int)kListCap ? tid - kListT0 : -1;
     if (li >= 0) lq = list[li];
     const int nparts = st->nparts;
-    const unsigned ln = bs->list_n;
+    const unsigned ln = bs->list_n[ptrip & 1];
     if (st->halt) {   // a trip queued behind a halt: nothing to do (the host takes over)
         if (tid == 0) {
-            bt->stop = -1;
-            if (trip_info) {
-                trip_info[4 * trip_slot] = -1; trip_info[4 * trip_slot + 1] = 0;
-                trip_info[4 * trip_slot + 2] = 0; trip_info[4 * trip_slot + 3] = 0;
+            OB.stop = -1;
+            if (pub && O.trip_info) {
+                int* ti = O.trip_info + 4 * O.trip_slot;
+                ti[0] = -1; ti[1] = 0; ti[2] = 0; ti[3] = 0;
             }
         }
         return;
     }
     // the rule's scalars (uniform: scalar loads, in flight with the vector loads above)
-    const int halt = st->halt, round = st->round, n_rounds = st->n_rounds, host_round = st->host_round;
+    const int round = st->round, n_rounds = st->n_rounds, host_round = st->host_round;
     const unsigned nC = st->nC, c_limit = st->c_limit;
     const long long T = st->T;
     const unsigned n_single = st->n_single, single_limit = st->single_limit;
@@ -1126,12 +1173,28 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     const int prev_k = bs->prev_k;
     const unsigned bid = bs->batch_seq + 1;
     const long long T2old = bs->T2;
-    if (tid == 0) probe_stamp(st, ptrip, 1);
-    if (wv < kSelListWave) {   // P1: the exact best over the partials
+    if (pub && tid == 0) probe_stamp(st, ptrip, 1);
+    // the list: each entry's metadata first (its chain of dependent loads overlaps the partials'
+    // arrival), then each entry's rank among the entries
+    const int nl = ln <= kListCap ? (int)ln : 0;
+    const bool have = li >= 0 && li < nl;
+    const Cand x = have ? Cand{lq.cnt, lq.ka, lq.kb, lq.slot, lq.a, lq.b} : cand_none();
+    TokMetaS lm{};
+    unsigned lold = ~0u;
+    if (li >= 0) {
+        if (li < kTopM) S.list[li] = cand_none();
+        if (li == 0) { S.cnt_target = LLONG_MAX; S.cnt_last = LLONG_MAX; S.ntop = 0; }
+        S.all[li] = x;
+        S.cnt[li] = x.cnt;
+        if (pub && li == 0 && lq.slot != 0xfffffffeu) probe_stamp(st, ptrip, 24);   // the list entry arrived
+        if (have && kSelMetaAll) cand_meta(x, K, X, lm, lold);
+        if (pub && li == 0 && lold != 0xfffffffeu && lm.la != 0xfffffffeu) probe_stamp(st, ptrip, 25);   // metadata + dedupe
+    }
+    if (tid < kPartT) {   // P1: the exact best over the partials
         Cand best = cand_none();
 #pragma unroll
         for (int u = 0; u < kPartPer; ++u) {
-            const int idx = tid + u * 64 * kSelListWave;
+            const int idx = tid + u * kPartT;
             if (idx < nparts) {
                 const Cand c{q[u].cnt, q[u].ka, q[u].kb, q[u].slot, q[u].a, q[u].b};
                 if (cand_better(c, best, K.pool, K.off, K.len)) best = c;
@@ -1141,32 +1204,18 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
             const Cand oc = shfl_xor_cand(best, o);
             if (cand_better(oc, best, K.pool, K.off, K.len)) best = oc;
         }
-        if (lane == 0) s_wave[wv] = best;
+        if (lane == 0) S.wave[wv] = best;
     }
-    // the list: each entry's rank among the entries, then the metadata of the top kTopM
-    const int nl = ln <= kListCap ? (int)ln : 0;
-    const bool have = li >= 0 && li < nl;
-    const Cand x = have ? Cand{lq.cnt, lq.ka, lq.kb, lq.slot, lq.a, lq.b} : cand_none();
-    TokMetaS lm{};
-    unsigned lold = ~0u;
-    if (li >= 0) {
-        if (li < kTopM) s_list[li] = cand_none();
-        if (li == 0) { s_cnt_target = LLONG_MAX; s_cnt_last = LLONG_MAX; s_ntop = 0; }
-        s_all[li] = x;
-        s_cnt[li] = x.cnt;
-        if (li == 0 && lq.slot != 0xfffffffeu) probe_stamp(st, ptrip, 24);   // the list entry arrived
-        if (have && kSelMetaAll) cand_meta(x, K, X, lm, lold);   // overlaps the partials' reduction
-        if (li == 0 && lold != 0xfffffffeu && lm.la != 0xfffffffeu) probe_stamp(st, ptrip, 25);   // metadata + dedupe
-    }
-    if (tid == 0) probe_stamp(st, ptrip, 26);   // wave 0's partials reduced
-    if (BPE355_PROBE_CODE && tid == 0 && st->probe && (ptrip % kProbeTrip) == 0) st->probe[kProbeSlots * (size_t)(ptrip / kProbeTrip) + 30] = ln + 1;
+    if (pub && tid == 0) probe_stamp(st, ptrip, 26);   // wave 0's partials reduced
+    if (BPE355_PROBE_CODE && pub && tid == 0 && st->probe && (ptrip % kProbeTrip) == 0)
+        st->probe[kProbeSlots * (size_t)(ptrip / kProbeTrip) + 30] = ln + 1;
     __syncthreads();
-    if (li == 0) probe_stamp(st, ptrip, 27);
+    if (pub && li == 0) probe_stamp(st, ptrip, 27);
     if (wv == 0) {   // P1 over the waves' bests, while the list waves rank (off the rule's path)
-        Cand p = s_wave[0];
-        for (int w = 1; w < kSelListWave; ++w)
-            if (cand_better(s_wave[w], p, K.pool, K.off, K.len)) p = s_wave[w];
-        if (lane == 0) s_p1 = p;
+        Cand p = S.wave[0];
+        for (int w = 1; w < kPartW; ++w)
+            if (cand_better(S.wave[w], p, K.pool, K.off, K.len)) p = S.wave[w];
+        if (lane == 0) S.p1 = p;
     }
     long long tgt = LLONG_MAX, last = LLONG_MAX;
     // rank by count alone first (one 8-byte compare per entry); only an entry with fewer than
@@ -1178,35 +1227,35 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         rc = 0;
 #pragma unroll 8
         for (int j = 0; j < nl; ++j) {
-            const long long cj = s_cnt[j];
+            const long long cj = S.cnt[j];
             rc += cj > x.cnt ? 1 : 0;
             ec += cj == x.cnt ? 1 : 0;
         }
         if (rc < kTopM) {
-            const unsigned pos = atomicAdd(&s_ntop, 1u);
-            s_top[pos] = li;
-            s_topkey[pos] = SelKey{x.cnt, x.ka, x.kb, (unsigned long long)x.b << 32 | x.a};
+            const unsigned pos = atomicAdd(&S.ntop, 1u);
+            S.top[pos] = li;
+            S.topkey[pos] = SelKey{x.cnt, x.ka, x.kb, (unsigned long long)x.b << 32 | x.a};
         }
         // the count at sorted position t is the least count whose first position is <= t
         tgt = rc <= (int)kListTarget - 1 ? x.cnt : LLONG_MAX;
         last = x.cnt;
     }
-    if (li == 0) probe_stamp(st, ptrip, 29);   // count ranks done
+    if (pub && li == 0) probe_stamp(st, ptrip, 29);   // count ranks done
     __syncthreads();
-    if (li == 0) probe_stamp(st, ptrip, 31);   // every list thread's count rank done
+    if (pub && li == 0) probe_stamp(st, ptrip, 31);   // every list thread's count rank done
     if (have && rc < kTopM) {
         // (count, a's 8-byte prefix, b's) branch-free over the small set; only equal prefixes of
-        // different tokens need the bytes (rare: then cand_better)
-        // with no other entry of its count, the count rank is the exact rank (the usual case);
-        // otherwise the ties are ordered by bytes over the packed top entries, which hold every
-        // entry of this count (each has the same rc < kTopM)
-        const int m = ec > 1 ? (int)s_ntop : 0;
+        // different tokens need the bytes (rare: then cand_better).  With no other entry of its
+        // count, the count rank is the exact rank (the usual case); otherwise the ties are ordered
+        // by bytes over the packed top entries, which hold every entry of this count (each has
+        // the same rc < kTopM)
+        const int m = ec > 1 ? (int)S.ntop : 0;
         int rank = ec > 1 ? 0 : rc;
         bool tail = false;
 #pragma unroll 4
         for (int t = 0; t < m; ++t) {
-            const int j = (int)s_top[t];
-            const SelKey y = s_topkey[t];
+            const int j = (int)S.top[t];
+            const SelKey y = S.topkey[t];
             const unsigned ya = (unsigned)y.ab, yb = (unsigned)(y.ab >> 32);
             const bool gt = y.cnt > x.cnt, eq = y.cnt == x.cnt && j != li;
             const bool ad = ya != x.a, bd = yb != x.b;
@@ -1216,65 +1265,63 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         if (tail) {
             rank = 0;
             for (int t = 0; t < m; ++t) {
-                const int j = (int)s_top[t];
-                rank += (j != li && cand_better(s_all[j], x, K.pool, K.off, K.len)) ? 1 : 0;
+                const int j = (int)S.top[t];
+                rank += (j != li && cand_better(S.all[j], x, K.pool, K.off, K.len)) ? 1 : 0;
             }
         }
         if (rank < kTopM) {
             if (!kSelMetaAll) cand_meta(x, K, X, lm, lold);
-            s_list[rank] = x;
-            s_meta[rank] = lm;
-            s_nw_old[rank] = lold;
+            S.list[rank] = x;
+            S.meta[rank] = lm;
+            S.nw_old[rank] = lold;
         }
     }
-    if (li == 0) probe_stamp(st, ptrip, 28);   // ranked
-    if (li >= 0) {   // wave minima, then one LDS atomic per wave
+    if (pub && li == 0) probe_stamp(st, ptrip, 28);   // ranked
+    if (li >= 0 && (kListT0 > 0 || wv < (int)(kListCap / 64))) {   // wave minima, then one LDS atomic per wave
         for (int o = 32; o > 0; o >>= 1) {
             tgt = min(tgt, (long long)__shfl_xor(tgt, o));
             last = min(last, (long long)__shfl_xor(last, o));
         }
         if (lane == 0 && last != LLONG_MAX) {
-            atomicMin(&s_cnt_target, tgt);
-            atomicMin(&s_cnt_last, last);
+            atomicMin(&S.cnt_target, tgt);
+            atomicMin(&S.cnt_last, last);
         }
     }
     __syncthreads();
-    if (tid == 0) probe_stamp(st, ptrip, 2);
+    if (pub && tid == 0) probe_stamp(st, ptrip, 2);
     if (wv != 0) return;
     // ---- wave 0: the rule and the record, lane i holding candidate i (no workgroup barrier)
-    const Cand p1 = s_p1;
+    const Cand p1 = S.p1;
     // the list's head is the global best whenever the best is >= T2 and nothing overflowed; the
-    // ranks are distinct, so s_list holds a prefix
-    if (lane == 0) probe_stamp(st, ptrip, 17);
-    const bool list_ok = ln <= kListCap && s_list[0].cnt != LLONG_MIN && s_list[0].slot == p1.slot &&
-                         s_list[0].a == p1.a && s_list[0].b == p1.b;
+    // ranks are distinct, so S.list holds a prefix
+    if (pub && lane == 0) probe_stamp(st, ptrip, 17);
+    const bool list_ok = ln <= kListCap && S.list[0].cnt != LLONG_MIN && S.list[0].slot == p1.slot &&
+                         S.list[0].a == p1.a && S.list[0].b == p1.b;
     int nf = 1;
     if (list_ok) {
         const unsigned long long vm =
-            __ballot(lane >= 1 && lane < kTopM && s_list[lane < kTopM ? lane : 0].cnt != LLONG_MIN) | 1ull;
+            __ballot(lane >= 1 && lane < kTopM && S.list[lane < kTopM ? lane : 0].cnt != LLONG_MIN) | 1ull;
         nf = __builtin_ctzll(~vm);
     }
     int stop = HALT_NONE;
-    if (halt) stop = halt;
-    else if (round >= n_rounds) stop = HALT_DONE;
+    if (round >= n_rounds) stop = HALT_DONE;
     else if (nC > c_limit) stop = HALT_REBUILD;                        // C bloated: re-threshold
     else if (p1.cnt == LLONG_MIN || p1.cnt < T) stop = HALT_REBUILD;   // max(C) < T: re-threshold
     else if (round >= host_round || n_single > single_limit ||
              pair_used + 2ull * (unsigned)(ntok + kMaxBatch) * kMaxBatch > pair_limit ||
              pool_used + (unsigned long long)kMaxBatch * max_len > pool_cap)
         stop = HALT_HOST;
-    if (BPE355_STATS_CODE && lane == 0 && !halt) {   // no-return atomics: nothing waits on them
+    if (BPE355_STATS_CODE && pub && lane == 0) {   // no-return atomics: nothing waits on them
         if (ln > kListCap) atomicAdd(&bs->n_overflow, 1ull);
         else if (!list_ok) atomicAdd(&bs->n_headmiss, 1ull);
         else if (nf < kTopM) atomicAdd(&bs->n_short, 1ull);
     }
-    if (stop) {
+    if (stop) {   // the apply raises the halt (nothing this trip's kernels read changes before it)
         if (lane == 0) {
-            if (!halt) st->halt = stop;
-            bt->stop = -1;
-            if (trip_info) {
-                trip_info[4 * trip_slot] = -1; trip_info[4 * trip_slot + 1] = 0;
-                trip_info[4 * trip_slot + 2] = 0; trip_info[4 * trip_slot + 3] = 0;
+            OB.stop = stop;
+            if (pub && O.trip_info) {
+                int* ti = O.trip_info + 4 * O.trip_slot;
+                ti[0] = -1; ti[1] = 0; ti[2] = 0; ti[3] = 0;
             }
         }
         return;
@@ -1285,15 +1332,15 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     unsigned old = ~0u;
     if (i == 0) {
         e = p1;
-        if (list_ok) { m = s_meta[0]; old = s_nw_old[0]; }
+        if (list_ok) { m = S.meta[0]; old = S.nw_old[0]; }
         else cand_meta(p1, K, X, m, old);   // rare: P1 alone, its metadata here
     } else if (i < nf) {
-        e = s_list[i];
-        m = s_meta[i];
-        old = s_nw_old[i];
+        e = S.list[i];
+        m = S.meta[i];
+        old = S.nw_old[i];
     }
     const bool fr = i < nf && old == ~0u;
-    if (lane == 0) probe_stamp(st, ptrip, 18);
+    if (pub && lane == 0) probe_stamp(st, ptrip, 18);
     const unsigned long long h = m.ha * m.pb + m.hb;
     const unsigned lk = m.la + m.lb;
     // (1) tokens disjoint from, and (3) new bytes different from, every earlier candidate's.
@@ -1318,8 +1365,8 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
                 clash |= tc;
                 if (!tc && hj == hi && lj == li_) {   // equal hashes: compare the bytes (rare)
                     bool eq = true;
-                    for (unsigned x = 0; x < li_ && eq; ++x)
-                        eq = concat_byte(K, aj, laj, bj, x) == concat_byte(K, ai, lai, bi, x);
+                    for (unsigned y = 0; y < li_ && eq; ++y)
+                        eq = concat_byte(K, aj, laj, bj, y) == concat_byte(K, ai, lai, bi, y);
                     clash |= eq;
                 }
             }
@@ -1345,7 +1392,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         // (4') a tie at the boundary is harmless unless a tied non-member could seed a new pair:
         // a pair created by the batch has at most the count of the old pair (x, a_j) or (b_j, y)
         // it replaces, so with every tied non-member free of those shapes, no new pair reaches
-        // count(Pk).  Every key >= T2 is listed, so the tied keys are all in s_all.
+        // count(Pk).  Every key >= T2 is listed, so the tied keys are all in S.all.
         if (k_strict < k && k > 1) {
             const long long c = readlane64((unsigned long long)e.cnt, k - 1);
             unsigned ma[kMaxBatch], mb[kMaxBatch], ms[kMaxBatch];
@@ -1357,14 +1404,14 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
             }
             bool bad = false;
             for (int t = lane; t < nl; t += 64) {
-                const Cand q = s_all[t];
-                if (q.cnt != c) continue;
+                const Cand y = S.all[t];
+                if (y.cnt != c) continue;
                 bool member = false, seeds = false;
 #pragma unroll
                 for (int j = 0; j < kMaxBatch; ++j) {
                     if (j >= k) break;
-                    member |= q.slot == ms[j];
-                    seeds |= q.b == ma[j] || q.a == mb[j];
+                    member |= y.slot == ms[j];
+                    seeds |= y.b == ma[j] || y.a == mb[j];
                 }
                 bad |= !member && seeds;
             }
@@ -1373,9 +1420,9 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
             k = k_strict;
         }
     }
-    if (lane == 0) probe_stamp(st, ptrip, 19);
+    if (pub && lane == 0) probe_stamp(st, ptrip, 19);
     const bool fr0 = __builtin_amdgcn_readlane((int)fr, 0);
-    if (BPE355_STATS_CODE && k == 1 && lane == 0) {
+    if (BPE355_STATS_CODE && pub && k == 1 && lane == 0) {
         const int why = p1.a == p1.b ? 0 : !fr0 ? 1 : nf == 1 ? 2 : k_rule == 1 ? 3 : 4;
         atomicAdd(&bs->k1_why[why], 1ull);
     }
@@ -1397,8 +1444,7 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
     const unsigned tot_pool = __builtin_amdgcn_readlane((int)pre_pool, k);
     const unsigned tot_list = __builtin_amdgcn_readlane((int)pre_list, k);
     const unsigned tot_fresh = __builtin_amdgcn_readlane((int)pre_fresh, k);
-    Batch& B = *bt;
-    if (i <= k) B.list_pre[i] = pre_list;
+    if (i <= k) OB.list_pre[i] = pre_list;
     if (mem) {
         BatchMember M;
         M.a = e.a; M.b = e.b; M.slot = e.slot; M.cnt = e.cnt;
@@ -1414,28 +1460,29 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
         M.cov_beg = bu;
         M.cov_len = fr ? lu : kNoAnc;   // dedupe: uncovered until the next index build
         M.pool_off = pool_used + pre_pool;
-        B.m[i] = M;
-        m_a[round + i] = e.a; m_b[round + i] = e.b; m_new[round + i] = M.nw;
-        m_mode[round + i] = use ? lu : 0xffffffffu;
-        if (m_cnt) m_cnt[round + i] = e.cnt;
+        OB.m[i] = M;
+        if (pub) {
+            O.m_a[round + i] = e.a; O.m_b[round + i] = e.b; O.m_new[round + i] = M.nw;
+            O.m_mode[round + i] = use ? lu : 0xffffffffu;
+            if (O.m_cnt) O.m_cnt[round + i] = e.cnt;
+        }
     }
     if (lane == 0) {
-        B.stop = 0;
-        B.k = k;
-        B.round = round;
-        B.ntok = ntok;
-        B.trip = ptrip;
-        B.prev_k = prev_k;
-        B.batch_id = bid;
-        B.nC_base = nC;
-        B.full_scan = full;
+        OB.stop = 0;
+        OB.k = k;
+        OB.round = round;
+        OB.ntok = ntok;
+        OB.trip = ptrip;
+        OB.prev_k = prev_k;
+        OB.batch_id = bid;
+        OB.nC_base = nC;
+        OB.full_scan = full;
         {   // the merge's idle workgroups: past the listed words, when every member has a list
-            const bool lists = k > 1 ? !full : use;   // lane 0: member 0's own flag
-            B.idle_from = lists ? tot_list : ~0u;
+            const bool lists_ok = k > 1 ? !full : use;   // lane 0: member 0's own flag
+            OB.idle_from = lists_ok ? tot_list : ~0u;
         }
-        B.n_fresh = tot_fresh;
-        st->pool_used = pool_used + tot_pool;
-        bs->batch_seq = bid;
+        OB.n_fresh = tot_fresh;
+        OB.pool_after = pool_used + tot_pool;
         {   // the next list: about kListTarget keys.  With the list ranked, T2 = the count of the
             // kListTarget-th best (this trip pops at most kMaxBatch of those above it); on overflow
             // raise T2 halfway to the top; with too few keys, extend the range below the last one
@@ -1443,26 +1490,36 @@ __global__ void __launch_bounds__(kSelThreads) k_select(RoundState* __restrict__
             const long long t2 = T2old < T ? T : T2old;
             long long nt;
             if (ln > kListCap) nt = t2 + (top - t2) / 2;
-            else if (ln >= kListTarget) nt = s_cnt_target;
-            else if (ln > 0) nt = s_cnt_last - (top - s_cnt_last) - 1;
+            else if (ln >= kListTarget) nt = S.cnt_target;
+            else if (ln > 0) nt = S.cnt_last - (top - S.cnt_last) - 1;
             else nt = T;
-            bs->T2 = nt < T ? T : (nt > top ? top : nt);
-            bs->list_n = 0;   // the apply of this trip fills it again
+            OB.T2next = nt < T ? T : (nt > top ? top : nt);
         }
-        if (BPE355_STATS_CODE) {
-            if (k > 1) {
-                atomicAdd(&bs->rounds_batched, (unsigned long long)k);
-                atomicAdd(&bs->trips_batched, 1ull);
+        if (pub) {
+            bs->list_n[(ptrip + 1) & 1] = 0;   // the list this trip's apply fills (nothing reads it before)
+            if (BPE355_STATS_CODE) {
+                if (k > 1) {
+                    atomicAdd(&bs->rounds_batched, (unsigned long long)k);
+                    atomicAdd(&bs->trips_batched, 1ull);
+                }
+                atomicAdd(&bs->k_hist[k], 1ull);
             }
-            atomicAdd(&bs->k_hist[k], 1ull);
+            if (O.trip_info) {   // for the host: first round, members, scan mode, list entries
+                int* ti = O.trip_info + 4 * O.trip_slot;
+                ti[0] = round; ti[1] = k; ti[2] = full; ti[3] = (int)tot_list;
+            }
+            probe_stamp(st, ptrip, 3);
+            probe_stamp(st, ptrip, 4);
         }
-        if (trip_info) {   // for the host: first round, members, scan mode, list entries
-            trip_info[4 * trip_slot] = round; trip_info[4 * trip_slot + 1] = k;
-            trip_info[4 * trip_slot + 2] = full; trip_info[4 * trip_slot + 3] = (int)tot_list;
-        }
-        probe_stamp(st, ptrip, 3);
-        probe_stamp(st, ptrip, 4);
     }
+}
+
+__global__ void __launch_bounds__(kSelThreads) k_select(const RoundState* __restrict__ st, BatchState* __restrict__ bs,
+                                                        ToksDev K, IndexDev X, Batch* __restrict__ bt,
+                                                        const Partial* __restrict__ part,
+                                                        const Partial* __restrict__ lists, SelOut O) {
+    __shared__ SelLds S;
+    select_core<kSelThreads>(st, bs, K, X, part, lists, *bt, S, O, true);
 }
 
 // end of a block of trips: the state and the trips' records -> pinned host memory (plain vector
@@ -1524,16 +1581,16 @@ __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigne
     }
 }
 
+// The merge-apply rewrite of a trip's batch B (the batch record in memory for k_merge_batch, the
+// workgroup's own LDS copy in k_trip).  l_lr: the workgroup's LDS-summed cells (2 kLdsB per member).
 template <class TokT>
-__global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st, const Batch* __restrict__ bt,
-                                                     PairsDev P, ToksDev K, WordsDev<TokT> W, IndexDev X,
-                                                     unsigned long long* __restrict__ LRbase, size_t lr_member,
-                                                     size_t lr_parity, uint32_t* __restrict__ tags) {
-    __shared__ unsigned long long l_lr[2 * kLdsB * kMaxBatch];
+__device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Batch& B, PairsDev P, ToksDev K,
+                                           WordsDev<TokT> W, IndexDev X, unsigned long long* __restrict__ LRbase,
+                                           size_t lr_member, size_t lr_parity, uint32_t* __restrict__ tags,
+                                           unsigned long long* l_lr) {
     __shared__ unsigned s_ma[kMaxBatch], s_mb[kMaxBatch], s_mn[kMaxBatch];   // the members' tokens
     __shared__ unsigned s_pre[kMaxBatch + 1], s_lbeg[kMaxBatch];   // list prefix sums, list starts
     const int tid = threadIdx.x;
-    const Batch& B = *bt;
     // every field the prologue needs in one round trip (none depends on another)
     const int stop = B.stop, k = B.k, b_trip = B.trip, b_ntok = B.ntok, b_prev_k = B.prev_k;
     const unsigned idle_from = B.idle_from;
@@ -1551,26 +1608,17 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
         for (unsigned q = blockIdx.x * blockDim.x + tid; q < (unsigned)b_prev_k * nprev; q += S)
             st_merge(&LRo[(size_t)(q / nprev) * lr_member + q % nprev], 0ull);
     };
-    {   // list mode: workgroups past the listed words (and past the members' registrations) have
-        // nothing to do -- skip their LDS clear, barriers and flush
-        const unsigned bid = blockIdx.x;
-        if (bid >= (unsigned)k && bid < W.lblk0 && bid * blockDim.x >= idle_from) {
-            clear_prev();
-            if (tid == 0) probe_done(st, &st->probe_merge_done, b_trip, 14);
-            return;
-        }
-    }
-    if (tid < k) {
-        s_ma[tid] = ma; s_mb[tid] = mb; s_mn[tid] = mn;
-        s_lbeg[tid] = mlb;
-    }
-    if (tid <= k) s_pre[tid] = mpre;
-    if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 5);
-    for (unsigned q = tid; q < 2 * kLdsB * (unsigned)k; q += blockDim.x) l_lr[q] = 0;
-    unsigned long long* LRt = LRbase + (size_t)(B.trip & 1) * lr_parity;   // member j at + j * lr_member
-
-    if ((int)blockIdx.x < k) {   // block j pops member j, covers and registers its new token
-        const BatchMember& M = B.m[blockIdx.x];
+    // Member j's pop and new-token registration (nothing in this launch reads them: the apply
+    // and the next trip do) go to the first k workgroups without words when there are enough of
+    // them, else to workgroups 0..k-1 after their rewrite: either way no rewrite waits behind the
+    // registration's chain of dependent loads (the token bytes of a and b)
+    const unsigned gl = min(gridDim.x, W.lblk0);   // the slot-class blocks that exist
+    const unsigned busy = idle_from == ~0u ? gl : min(gl, (idle_from + blockDim.x - 1) / blockDim.x);
+    const unsigned reg0 = busy + (unsigned)k <= gl ? busy : 0u;   // (the grid has >= kMaxBatch blocks)
+    const int reg_j = (int)blockIdx.x - (int)reg0;
+    auto register_member = [&]() {
+        if (reg_j < 0 || reg_j >= k) return;
+        const BatchMember& M = B.m[reg_j];
         if (tid == 0) {
             P.cnt[M.slot] = 0;                       // byte_pair_frequencies.pop(best_pair)
             atomicAnd(&P.flag[M.slot], ~kPresent);
@@ -1589,7 +1637,26 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
                 K.hash[M.nw] = M.hash; K.pw[M.nw] = M.pw; K.key8[M.nw] = M.k8;
             }
         }
+    };
+    {   // list mode: workgroups past the listed words have no rewrite -- skip their LDS clear,
+        // barriers and flush
+        const unsigned bid = blockIdx.x;
+        if (bid >= busy && bid < gl) {
+            register_member();
+            clear_prev();
+            if (tid == 0) probe_done(st, &st->probe_merge_done, b_trip, 14);
+            return;
+        }
     }
+    if (tid < k) {
+        s_ma[tid] = ma; s_mb[tid] = mb; s_mn[tid] = mn;
+        s_lbeg[tid] = mlb;
+    }
+    if (tid <= k) s_pre[tid] = mpre;
+    if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 5);
+    for (unsigned q = tid; q < 2 * kLdsB * (unsigned)k; q += blockDim.x) l_lr[q] = 0;
+    unsigned long long* LRt = LRbase + (size_t)(B.trip & 1) * lr_parity;   // member j at + j * lr_member
+
     __syncthreads();   // l_lr cleared
     if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 6);
 
@@ -1671,7 +1738,8 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
         }
     }
     singles = wave_sum(singles);   // words that became one token (rare: no contention)
-    if ((tid & 63) == 0 && singles) atomicAdd(&st->n_single, singles);
+    // (the apply adds them to n_single, which this trip's select phase reads in every workgroup)
+    if ((tid & 63) == 0 && singles) atomicAdd(&st->n_single_new, singles);
     __syncthreads();
     if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 7);
     for (unsigned q = tid; q < 2 * kLdsB * (unsigned)k; q += blockDim.x) {
@@ -1680,10 +1748,54 @@ __global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st
     }
     if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 8);
     clear_prev();
+    register_member();
     if (BPE355_PROBE_CODE && st->probe) {
         __syncthreads();
         if (tid == 0) probe_done(st, &st->probe_merge_done, B.trip, 14);
     }
+}
+
+// the rewrite of the batch k_select decided (BPE355_FOLD=0)
+template <class TokT>
+__global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st, const Batch* __restrict__ bt,
+                                                     PairsDev P, ToksDev K, WordsDev<TokT> W, IndexDev X,
+                                                     unsigned long long* __restrict__ LRbase, size_t lr_member,
+                                                     size_t lr_parity, uint32_t* __restrict__ tags) {
+    __shared__ unsigned long long l_lr[2 * kLdsB * kMaxBatch];
+    merge_body<TokT>(st, *bt, P, K, W, X, LRbase, lr_member, lr_parity, tags, l_lr);
+}
+
+// One trip's select and merge in ONE launch.  Every workgroup decides the
+// batch itself -- the decision is a function of state that nothing in this launch changes
+// (select_core) -- so no workgroup waits for another and the select's kernel boundary is gone.
+// Block 0 also publishes the batch record the apply reads.  Measured on the bench config it is
+// no faster than k_select + k_merge_batch (257.4-258.3 vs 255.4 ms of merges): the boundary it
+// saves (2-4 us) is paid back by the decision's own loads, which every workgroup repeats (the
+// apply's 24 KB of partials arrive 1.3 us later with 1024 readers than with one), so it is the
+// BPE355_FOLD=1 option, not the default.  The select's LDS and the
+// rewrite's LDS-summed cells share one union: the cells are cleared after the decision.
+template <class TokT>
+__global__ void __launch_bounds__(kTripThreads) k_trip(RoundState* __restrict__ st, BatchState* __restrict__ bs,
+                                              PairsDev P, ToksDev K, WordsDev<TokT> W, IndexDev X,
+                                              Batch* __restrict__ bt, const Partial* __restrict__ part,
+                                              const Partial* __restrict__ lists, SelOut O,
+                                              unsigned long long* __restrict__ LRbase, size_t lr_member,
+                                              size_t lr_parity, uint32_t* __restrict__ tags) {
+    __shared__ union TripLds {
+        SelLds sel;
+        unsigned long long lr[2 * kLdsB * kMaxBatch];
+    } u;
+    __shared__ Batch s_b;
+    const bool pub = blockIdx.x == 0;
+    select_core<kTripThreads>(st, bs, K, X, part, lists, s_b, u.sel, O, pub);
+    __syncthreads();
+    if (pub) {   // the apply's copy of the decision
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(&s_b);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(bt);
+        for (unsigned i = threadIdx.x; i < (unsigned)(sizeof(Batch) / 4); i += blockDim.x) dst[i] = src[i];
+    }
+    if (s_b.stop) return;
+    merge_body<TokT>(st, s_b, P, K, W, X, LRbase, lr_member, lr_parity, tags, u.lr);
 }
 
 // Apply the trip's deltas and list the next trip's candidates.  Items:
@@ -1729,10 +1841,20 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     static_assert(offsetof(BatchMember, b) == 4 && offsetof(BatchMember, nw) == 8, "a, b, nw adjacent");
     const int b_stop = B.stop, b_k = B.k, b_trip = B.trip, b_ntok = B.ntok;
     const unsigned b_fresh = B.n_fresh, b_nC = B.nC_base;
-    const long long T = st->T, T2raw = bs->T2;
+    const long long b_T2 = B.T2next;
+    const long long T = st->T, T2bs = bs->T2;
+    const int bs_trip = bs->trip;
     const unsigned st_nC = st->nC;   // scan_only: no admissions during the scan, so stable
     const unsigned t_raw = tid < 3 * kMaxBatch ? reinterpret_cast<const unsigned*>(&B.m[tid / 3])[tid % 3] : ~0u;
-    if (!scan_only && b_stop) return;   // halted: part[] keeps the lists the next select reads
+    if (!scan_only && b_stop) {   // no trip: part[] and the list keep what the next select reads
+        if (b_stop > 0 && blockIdx.x == 0 && tid == 0) st->halt = b_stop;   // the select's halt
+        return;
+    }
+    // the threshold of the list this apply fills (the trip's decision, or after a rebuild the
+    // last one), and which of the two lists: the next trip's parity
+    const long long T2raw = scan_only ? T2bs : b_T2;
+    const unsigned lpar = (unsigned)(scan_only ? bs_trip : b_trip + 1) & 1u;
+    list += (size_t)lpar * kListCap;
     const int k = scan_only ? 0 : b_k;
     const bool pw0 = !scan_only && blockIdx.x == 0 && tid == 0;
     if (pw0) probe_stamp(st, b_trip, 9);
@@ -1741,12 +1863,14 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
         const int i = tid;
         const bool have = i < 3 * k;
         const unsigned ti = have ? t_raw : ~0u;
+        // For k > 1 the 3k tokens are distinct: the members' tokens are disjoint, a != b, and the
+        // new tokens are fresh ids (select_core's rule).  For k == 1 only a == b can repeat (a new
+        // token's bytes are longer than a's and b's), so no general dedupe pass is needed.
+        unsigned roles = 1u << (i % 3);
         bool dup = false;
-        unsigned roles = 0;   // members' tokens are disjoint for k > 1: one member per token
-        for (int j = 0; j < 3 * kMaxBatch; ++j) {
-            const unsigned tj = __builtin_amdgcn_readlane((int)ti, j);
-            dup |= j < i && tj == ti;
-            if (j < 3 * k && tj == ti) roles |= 1u << (j % 3);
+        if (k == 1 && __builtin_amdgcn_readlane((int)ti, 0) == __builtin_amdgcn_readlane((int)ti, 1)) {
+            if (i == 0) roles = 3u;   // a == b: one entry, both roles
+            dup = i == 1;
         }
         const bool keep = have && !dup;
         const unsigned long long km = __ballot(keep);
@@ -1945,12 +2069,12 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
         part[blockIdx.x] = Partial{best.cnt, best.ka, best.kb, best.slot, best.a, best.b, 0};
         // the workgroup's list entries and C admissions: one reservation each
         const unsigned nl = s_nl, nc = min(s_nc, kApplyCLds);
-        s_lbase = nl ? atomicAdd(&bs->list_n, nl) : 0u;
+        s_lbase = nl ? atomicAdd(&bs->list_n[lpar], nl) : 0u;
         s_cbase = nc ? atomicAdd(&st->nC, nc) : 0u;
         if (s_ins) atomicAdd(&st->pair_used, (unsigned long long)s_ins);   // read by the next select
     }
-    __syncthreads();
-    {
+    if (s_nl | s_nc) {   // (uniform: read after the barrier) only workgroups with entries wait
+        __syncthreads();
         const unsigned nl = min(s_nl, kListCap), nc = min(s_nc, kApplyCLds);
         const unsigned lb = s_lbase, cb = s_cbase;
         if ((unsigned)tid < nl && lb + tid < kListCap) list[lb + tid] = s_lst[tid];
@@ -1968,11 +2092,16 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     }
     if (blockIdx.x == 0 && tid == 0) {
         st->nparts = gridDim.x;
-        if (!scan_only) {   // finish the trip: k rounds done
+        if (!scan_only) {   // finish the trip: k rounds done; the state its select decided from
             st->round = B.round + k;
             st->ntok = B.ntok + (int)B.n_fresh;
             bs->trip = B.trip + 1;
             bs->prev_k = k;
+            st->pool_used = B.pool_after;
+            bs->batch_seq = B.batch_id;
+            bs->T2 = b_T2;
+            st->n_single += st->n_single_new;
+            st->n_single_new = 0;
         }
     }
     if (pw0) probe_stamp(st, B.trip, 13);
@@ -2554,6 +2683,8 @@ class MergeLoop {
     unsigned n_words_ = 0, max_len_ = 0;
     HostWords<TokT> words_;
     WordsDev<TokT> wdev_{};
+    WordsDev<TokT> wdev_trip_{};    // the slot classes over k_trip's workgroups
+    unsigned trip_grid_ = 1;
     unsigned merge_grid_ = 1;
     unsigned merge_grid_cur_ = 0;   // k_merge_batch blocks for the next block of trips (0: merge_grid_)
     double scan_bytes_ = 0, long_bytes_ = 0;
@@ -2577,6 +2708,7 @@ class MergeLoop {
     DevBuf<uint32_t> m_a_, m_b_, m_new_, m_mode_;
     // batched rounds (single rank): several exact merges per trip (k_select)
     bool batched_ = false;
+    bool fused_ = false;         // k_trip (BPE355_FOLD=1), else k_select + k_merge_batch
     int max_batch_ = kMaxBatch;
     long long trips_launched_ = 0, trips_run_ = 0, rounds_batched_ = 0;
     DevBuf<BatchState> bs_;
@@ -2804,6 +2936,21 @@ void MergeLoop<TokT>::layout_blocks() {
     blk += W.lnblk;
     merge_grid_ = std::max(blk, (unsigned)kMaxBatch);   // k_merge_batch: block j registers member j
     wdev_ = W;
+    {   // k_trip's layout: the same classes over kTripThreads-thread workgroups
+        constexpr unsigned r = kTripThreads / 256;
+        WordsDev<TokT> Wb = W;
+        unsigned bb = 0;
+        for (int c = 0; c < kNumCls; ++c) {
+            Wb.c[c].blk0 = bb;
+            Wb.c[c].nblk = W.c[c].n ? std::max(1u, ceil_div(W.c[c].nblk, r)) : 0;
+            bb += Wb.c[c].nblk;
+        }
+        Wb.lblk0 = bb;
+        Wb.lnblk = std::min(ceil_div(W.ln, kTripThreads), 64u / r);
+        bb += Wb.lnblk;
+        trip_grid_ = std::max(bb, (unsigned)kMaxBatch);
+        wdev_trip_ = Wb;
+    }
     if (std::getenv("BPE355_TRACE"))
         std::fprintf(stderr, "[bpe355] words per slot class: %u %u %u %u, long %u (%llu ids); merge grid %u\n", W.c[0].n,
                      W.c[1].n, W.c[2].n, W.c[3].n, W.ln, (unsigned long long)long_tokens_, merge_grid_);
@@ -2901,7 +3048,7 @@ int MergeLoop<TokT>::rebuild() {
     push_state();
     hipLaunchKernelGGL(k_build_C, dim3(grid), dim3(256), 0, s_, pairs(), pcap_, T, st_.p);
     if (batched_) {   // the rebuilt C's best (partials) and candidate list
-        BPE_HIP(hipMemsetAsync(&bs_.p->list_n, 0, sizeof(unsigned), s_));
+        BPE_HIP(hipMemsetAsync(&bs_.p->list_n[0], 0, sizeof(bs_.p->list_n), s_));
         hipLaunchKernelGGL(k_apply_batch, dim3(kApplyBatchBlocks), dim3(kApplyBatchThreads), 0, s_, st_.p, bs_.p,
                            (const Batch*)batch_.p, pairs(), toks(), LR_.p, 2ull * tok_cap_,
                            (size_t)kMaxBatch * 2ull * tok_cap_, tok_cap_, part_.p, list_.p, 1);
@@ -2961,7 +3108,10 @@ void MergeLoop<TokT>::run() {
             for (auto& e : blk_ev_) BPE_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         }
         if (const char* e = std::getenv("BPE355_TRIPS")) trips_ = std::max(1, std::min(std::atoi(e), kTrips));
-        list_.alloc(kListCap);
+        list_.alloc(2 * kListCap);   // by trip parity
+        // select and merge of a trip in one launch (k_trip), or k_select + k_merge_batch
+        const char* fe = std::getenv("BPE355_FOLD");
+        fused_ = fe && fe[0] == '1';
     }
     m_a_.alloc(n_rounds_); m_b_.alloc(n_rounds_); m_new_.alloc(n_rounds_); m_mode_.alloc(n_rounds_);
     const char* round_log = std::getenv("BPE355_ROUND_LOG");   // analysis knob: per-round records
@@ -3419,13 +3569,20 @@ void MergeLoop<TokT>::launch_block(int slot, bool timing, std::vector<hipEvent_t
     for (int t = 0; t < trips_; ++t) {
         const bool timed = timing && (trips_launched_ + t) % kTimingStride == 0;
         hipEvent_t* e = &ev[2 * ((size_t)slot * kTrips + t)];
-        hipLaunchKernelGGL(k_select, dim3(1), dim3(kSelThreads), 0, s_, st_.p, bs_.p, pairs(), toks(), idev_,
-                           batch_.p, (const Partial*)part_.p, (const Partial*)list_.p, m_a_.p, m_b_.p, m_new_.p,
-                           m_mode_.p, m_cnt_.p, ti, t);
-        hipExtLaunchKernelGGL(k_merge_batch<TokT>, dim3(merge_grid()), dim3(256), 0, s_,
-                              timed ? e[0] : nullptr, timed ? e[1] : nullptr, 0,
-                              st_.p, (const Batch*)batch_.p, pairs(), toks(), wdev_, idev_, LR_.p, lr_member,
-                              lr_parity, tags_.p);
+        const SelOut so{m_a_.p, m_b_.p, m_new_.p, m_mode_.p, m_cnt_.p, ti, t};
+        if (fused_ && sizeof(TokT) == 2) {   // (u32 ids: k_trip would spill at 1024 threads)
+            hipExtLaunchKernelGGL(k_trip<TokT>, dim3(trip_grid_), dim3(kTripThreads), 0, s_,
+                                  timed ? e[0] : nullptr, timed ? e[1] : nullptr, 0,
+                                  st_.p, bs_.p, pairs(), toks(), wdev_trip_, idev_, batch_.p, (const Partial*)part_.p,
+                                  (const Partial*)list_.p, so, LR_.p, lr_member, lr_parity, tags_.p);
+        } else {
+            hipLaunchKernelGGL(k_select, dim3(1), dim3(kSelThreads), 0, s_, (const RoundState*)st_.p, bs_.p, toks(),
+                               idev_, batch_.p, (const Partial*)part_.p, (const Partial*)list_.p, so);
+            hipExtLaunchKernelGGL(k_merge_batch<TokT>, dim3(merge_grid()), dim3(256), 0, s_,
+                                  timed ? e[0] : nullptr, timed ? e[1] : nullptr, 0,
+                                  st_.p, (const Batch*)batch_.p, pairs(), toks(), wdev_, idev_, LR_.p, lr_member,
+                                  lr_parity, tags_.p);
+        }
         hipLaunchKernelGGL(k_apply_batch, dim3(apply_blocks), dim3(kApplyBatchThreads), 0, s_, st_.p, bs_.p,
                            (const Batch*)batch_.p, pairs(), toks(), LR_.p, lr_member, lr_parity, ntb, part_.p,
                            list_.p, 0);
