@@ -39,6 +39,18 @@ for step in "$@"; do
       BPE355_FOLD=$f timeout -k 10 300 python -u bench.py --no-file --no-encode --no-cpu-baseline --steps 3 --warmup 1 > $OUT/abfold_${f}_$rep.log 2>&1 || { echo "abfold failed"; tail -20 $OUT/abfold_${f}_$rep.log; exit 1; }
       python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().split(chr(10))[-1]); m=d['merge_loop']; print('FOLD=$f rep $rep merge_ms', m['ms'], 'us_per_trip', m['us_per_trip'], 'k_us', m['k_merge_batch_us'], 'parity', d['parity']['parity'])" $OUT/abfold_${f}_$rep.log
     done; done ;;
+  ab:*)   # merge phase with an env knob at 1 vs 0 (ab:NAME), corpus in HBM, alternating, 2 reps
+    V=${step#ab:}
+    for rep in 1 2; do for f in 1 0; do
+      env $V=$f timeout -k 10 300 python -u bench.py --no-file --no-encode --no-cpu-baseline --steps 3 --warmup 1 > $OUT/ab_${V}_${f}_$rep.log 2>&1 || { echo "ab failed"; tail -20 $OUT/ab_${V}_${f}_$rep.log; exit 1; }
+      python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().split(chr(10))[-1]); m=d['merge_loop']; print('$V=$f rep $rep merge_ms', m['ms'], 'us_per_trip', m['us_per_trip'], 'k_us', m['k_merge_batch_us'], 'count_ms', d['device_resident']['phases_ms']['t_count_ms'] if d.get('device_resident') else None, 'parity', d['parity']['parity'])" $OUT/ab_${V}_${f}_$rep.log
+    done; done ;;
+  probeab:*)   # the merge-loop probe with an env knob at 1 and 0
+    V=${step#probeab:}
+    for f in 1 0; do
+      env $V=$f BPE355_PROBE=1 BPE355_LIB=build/variants/probe/libbpe355.so timeout -k 10 200 python -u bench.py --no-file --steps 1 --warmup 0 --no-encode --no-cpu-baseline --no-timing > $OUT/probe_${V}_$f.log 2> $OUT/probe_err_${V}_$f.log || { echo "probe failed"; tail -5 $OUT/probe_err_${V}_$f.log; exit 1; }
+      grep probe $OUT/probe_err_${V}_$f.log | head -12
+    done ;;
   probe)   # the merge-loop probe (build/variants/probe), fused and unfused
     for f in 1 0; do
       BPE355_FOLD=$f BPE355_PROBE=1 BPE355_LIB=build/variants/probe/libbpe355.so timeout -k 10 200 python -u bench.py --no-file --steps 1 --warmup 0 --no-encode --no-cpu-baseline --no-timing > $OUT/probe_$f.log 2> $OUT/probe_err_$f.log || { echo "probe failed"; tail -5 $OUT/probe_err_$f.log; exit 1; }
