@@ -14,6 +14,12 @@ for step in "$@"; do
   quick)
     timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_release.py tests/test_gpu_limits.py "tests/test_gpu_c4.py::test_c4_ranks_rounds_1g" tests/test_gpu_train.py tests/test_gpu_encode.py > $OUT/pytest_quick.log 2>&1 || { echo "quick tests failed"; tail -40 $OUT/pytest_quick.log; exit 1; }
     tail -1 $OUT/pytest_quick.log ;;
+  pmc)   # HBM traffic per launch (two --pmc passes) -> profiles/r05/traffic.json (bench.py reads it)
+    bash tools/gpu_pmc_all.sh $TAG/pmc || exit 1
+    mkdir -p profiles/r05 && cp $OUT/pmc/traffic.json profiles/r05/traffic.json ;;
+  probe1)   # the merge-loop probe of the default configuration
+    BPE355_PROBE=1 BPE355_LIB=build/variants/probe/libbpe355.so timeout -k 10 200 python -u bench.py --no-file --steps 1 --warmup 0 --no-encode --no-cpu-baseline --no-timing > $OUT/probe.log 2> $OUT/probe_err.log || { echo "probe failed"; tail -5 $OUT/probe_err.log; exit 1; }
+    grep probe $OUT/probe_err.log > $OUT/merge_probe.txt; head -12 $OUT/merge_probe.txt ;;
   scale)
     timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_scale.py > $OUT/pytest_scale.log 2>&1 || { echo "scale tests failed"; tail -40 $OUT/pytest_scale.log; exit 1; }
     tail -1 $OUT/pytest_scale.log ;;

@@ -960,7 +960,7 @@ struct BatchState {
 // BPE355_LIST_CAP, 64 or 128; a trip whose list overflows it takes P1 alone and raises T2).  128
 // and 256 measured alike with the r04 select (zk_list_cap_ab.txt)
 #ifndef BPE355_LIST_CAP
-#define BPE355_LIST_CAP 128
+#define BPE355_LIST_CAP 256
 #endif
 constexpr unsigned kListCap = BPE355_LIST_CAP;
 static_assert(kListCap % 64 == 0 && kListCap >= 64, "whole waves of list threads");
