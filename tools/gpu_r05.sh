@@ -51,6 +51,13 @@ for step in "$@"; do
       env $V=$f timeout -k 10 300 python -u bench.py --no-file --no-encode --no-cpu-baseline --steps 3 --warmup 1 > $OUT/ab_${V}_${f}_$rep.log 2>&1 || { echo "ab failed"; tail -20 $OUT/ab_${V}_${f}_$rep.log; exit 1; }
       python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().split(chr(10))[-1]); m=d['merge_loop']; print('$V=$f rep $rep merge_ms', m['ms'], 'us_per_trip', m['us_per_trip'], 'k_us', m['k_merge_batch_us'], 'count_ms', d['device_resident']['phases_ms']['t_count_ms'] if d.get('device_resident') else None, 'parity', d['parity']['parity'])" $OUT/ab_${V}_${f}_$rep.log
     done; done ;;
+  abvar:*)   # merge phase and count, the default library vs build/variants/NAME (abvar:NAME), alternating, 2 reps
+    V=${step#abvar:}
+    for rep in 1 2; do for lib in default $V; do
+      if [ $lib = default ]; then LIBENV=""; else LIBENV="BPE355_LIB=build/variants/$V/libbpe355.so"; fi
+      env $LIBENV timeout -k 10 300 python -u bench.py --no-file --no-encode --no-cpu-baseline --steps 3 --warmup 1 > $OUT/abvar_${lib}_$rep.log 2>&1 || { echo "abvar failed"; tail -20 $OUT/abvar_${lib}_$rep.log; exit 1; }
+      python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().split(chr(10))[-1]); m=d['merge_loop']; print('$lib rep $rep merge_ms', m['ms'], 'us_per_trip', m['us_per_trip'], 'k_us', m['k_merge_batch_us'], 'trips', m['trips'], 'count_ms', d['device_resident']['phases_ms']['t_count_ms'] if d.get('device_resident') else None, 'parity', d['parity']['parity'])" $OUT/abvar_${lib}_$rep.log
+    done; done ;;
   probeab:*)   # the merge-loop probe with an env knob at 1 and 0
     V=${step#probeab:}
     for f in 1 0; do

@@ -43,6 +43,19 @@ __host__ __device__ __forceinline__ int uc_class(uint32_t cp) {
     return (Tab::bits(pg, (cp & 255u) >> 2) >> ((cp & 3u) * 2)) & 3;
 }
 
+// SWAR helpers on 4 bytes at once: per-byte results are flags in bit 7 of each byte
+// bit 7 of each byte of z that is zero (exact per byte: no carry crosses a byte)
+__host__ __device__ __forceinline__ uint32_t zero_bytes(uint32_t z) {
+    return ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;
+}
+// the four byte flags (bits 7, 15, 23, 31) as a nibble (bit i = byte i): t = m | m << 7 has the
+// flags of bytes 2, 3 at bits 30, 31 and those of bytes 0, 1 at 14, 15, which << 14 moves to 28, 29
+// (no other set bit of t lands in 28..31); two shift-or ops and a shift
+__host__ __device__ __forceinline__ uint32_t flag_nibble(uint32_t m) {
+    const uint32_t t = m | (m << 7);
+    return (t | (t << 14)) >> 28;
+}
+
 __host__ __device__ __forceinline__ int ctz128(u128 x) {
     const uint64_t lo = (uint64_t)x;
     return lo ? __builtin_ctzll(lo) : 64 + __builtin_ctzll((uint64_t)(x >> 64));
@@ -56,38 +69,38 @@ __host__ __device__ __forceinline__ int ctz128(u128 x) {
 // segment's first byte, and at it, are the caller's to clear / force.
 template <class Tab, class Win>
 __host__ __device__ __forceinline__ uint64_t token_starts64(const Win& w, int vhi) {
-    // per-byte flags, built 4 bytes at a time into 32-bit pieces (a rolled loop over the window's
-    // dwords keeps the register footprint small); the rest is derived from these seven
+    // per-byte flags, built 4 bytes at a time (SWAR: byte-wise range checks by adds that cannot
+    // carry out of a byte, flags in bit 7 of each byte, then packed to nibbles) into 32-bit
+    // pieces; the rest is derived from these seven.  (The byte-by-byte form it replaces compiled
+    // to ~470 instructions per 8 bytes, 40 % of them scalar mask operations, which the CU's one
+    // scalar unit serialises over all its waves.)  The rolled loop over the window's dwords keeps
+    // the register footprint small: unrolled, all 22 window loads are hoisted and the kernel spills.
     uint32_t fL[3] = {0, 0, 0}, fN[3] = {0, 0, 0}, fS[3] = {0, 0, 0}, fSP[3] = {0, 0, 0};
     uint32_t fAP[3] = {0, 0, 0}, fC[3] = {0, 0, 0}, fNA[3] = {0, 0, 0};
 #pragma unroll
     for (int seg = 0; seg < 3; ++seg) {
 #pragma unroll 1
-        for (int kk = 0; kk < 8; ++kk) {
-            const int k = seg * 8 + kk;
-            if (k >= kStartWin / 4) break;
-            const uint32_t x = w.dword(k);
-            uint32_t l = 0, nn = 0, sp = 0, spc = 0, ap = 0, ct = 0, na = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint32_t b = (x >> (8 * i)) & 0xffu;
-                const uint32_t m = 1u << i;
-                if (b < 0x80u) {
-                    if ((b | 0x20u) - 'a' < 26u) l |= m;
-                    else if (b - '0' < 10u) nn |= m;
-                    else if (b == 0x20u || b - 9u < 5u) sp |= m;
-                    if (b == 0x20u) spc |= m;
-                    if (b == 0x27u) ap |= m;
-                } else if (b < 0xC0u) {
-                    ct |= m;
-                } else {
-                    na |= m;
-                }
-            }
-            const int sh = 4 * kk;
-            fL[seg] |= l << sh; fN[seg] |= nn << sh; fS[seg] |= sp << sh; fSP[seg] |= spc << sh;
-            fAP[seg] |= ap << sh; fC[seg] |= ct << sh; fNA[seg] |= na << sh;
-        }
+      for (int kk = 0; kk < 8; ++kk) {
+        const int k = seg * 8 + kk;
+        if (k >= kStartWin / 4) break;
+        const uint32_t x = w.dword(k);
+        const uint32_t hi = x & 0x80808080u;       // non-ASCII bytes
+        const uint32_t asc = hi ^ 0x80808080u;     // ASCII bytes
+        const uint32_t lo7 = x & 0x7F7F7F7Fu;
+        const uint32_t lw = lo7 | 0x20202020u;     // ASCII letters folded to lower case
+        // [a-z]: lw >= 0x61 and lw < 0x7B; [0-9]: 0x30 <= lo7 < 0x3A; \t..\r: 0x09 <= lo7 < 0x0E
+        const uint32_t l = (lw + 0x1F1F1F1Fu) & ~(lw + 0x05050505u) & asc;
+        const uint32_t nn = (lo7 + 0x50505050u) & ~(lo7 + 0x46464646u) & asc;
+        const uint32_t spc = zero_bytes(x ^ 0x20202020u);   // U+0020
+        const uint32_t sp = ((lo7 + 0x77777777u) & ~(lo7 + 0x72727272u) & asc) | spc;
+        const uint32_t ap = zero_bytes(x ^ 0x27272727u);    // U+0027
+        const uint32_t ct = hi & ~(x << 1);        // 10xxxxxx: continuation bytes
+        const uint32_t na = hi & (x << 1);         // 11xxxxxx: lead bytes of 2..4-byte characters
+        const int sh = 4 * kk;
+        fL[seg] |= flag_nibble(l) << sh; fN[seg] |= flag_nibble(nn) << sh; fS[seg] |= flag_nibble(sp) << sh;
+        fSP[seg] |= flag_nibble(spc) << sh; fAP[seg] |= flag_nibble(ap) << sh;
+        fC[seg] |= flag_nibble(ct) << sh; fNA[seg] |= flag_nibble(na) << sh;
+      }
     }
     auto join = [](const uint32_t (&f)[3]) -> u128 {
         return (u128)f[0] | ((u128)f[1] << 32) | ((u128)f[2] << 64);

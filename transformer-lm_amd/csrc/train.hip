@@ -956,9 +956,10 @@ struct BatchState {
     unsigned long long n_overflow, n_headmiss, n_short, k_hist[kMaxBatch + 1];   // diagnostics
     unsigned long long k1_why[6];   // single-merge trips: P1 a == b / P1 not fresh / no list / P2 fails / tie / end
 };
-// the candidate list the select ranks in its wave 0, one or two entries per lane (build knob
-// BPE355_LIST_CAP, 64 or 128; a trip whose list overflows it takes P1 alone and raises T2).  128
-// and 256 measured alike with the r04 select (zk_list_cap_ab.txt)
+// the candidate list the select ranks, one thread per entry (build knob BPE355_LIST_CAP, a multiple
+// of 64; a trip whose list overflows it takes P1 alone and raises T2).  128 took 56 more trips at
+// the bench config for the same merge phase (255.6 ms, profiles/r05/g_bench_default.log; r04:
+// zk_list_cap_ab.txt)
 #ifndef BPE355_LIST_CAP
 #define BPE355_LIST_CAP 256
 #endif
