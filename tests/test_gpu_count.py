@@ -7,7 +7,8 @@ the bench corpus takes and on the ones only knobs reach on small inputs:
   * few workgroups each streaming many chunks (BPE355_STREAM_WG): pages fill and turn over;
   * the file path's segment launches (BPE355_SEG_MB) continuing each workgroup's page;
   * an unaligned device pointer (the byte-wise staging path);
-  * adversarial text (every pattern branch, multi-byte characters at every alignment).
+  * adversarial text (every pattern branch, multi-byte characters at every alignment);
+  * text dense in words longer than 16 bytes (the long-word segments, full and not).
 """
 from __future__ import annotations
 
@@ -119,6 +120,52 @@ def test_file_partial_aggregation(knob, tmp_path, every):
     assert st["n_count_records"] > 0
     assert st["n_count_batches"] > 2
     assert got == oracle.train_raw(data, 3000, EOT)
+
+
+def _long_word_text(seed, n_words):
+    """text dense in pre-tokens longer than 16 bytes (ASCII, 2- and 3-byte letters, digits,
+    whitespace runs), many of them repeated, between ordinary synthetic text"""
+    rng = np.random.default_rng(seed)
+    alpha = "abcdefghijklmnopqrstuvwxyz" + "éßøñ" + "жщы" + "中文字"
+    vocab = []
+    for _ in range(400):
+        k = int(rng.integers(9, 40))
+        w = "".join(alpha[int(i)] for i in rng.integers(0, len(alpha), k))
+        vocab.append(w if rng.random() < 0.8 else "".join(str(int(d)) for d in rng.integers(0, 10, 2 * k)))
+    filler = synth_text.generate(seed, 400_000, "mixed")
+    parts = []
+    for _ in range(n_words):
+        parts.append(" " + vocab[int(rng.integers(0, len(vocab)))] if rng.random() < 0.7
+                     else " " + "".join(alpha[int(i)] for i in rng.integers(0, len(alpha), int(rng.integers(17, 90)))))
+        if rng.random() < 0.1:   # indentation: whitespace runs of 17-40 bytes, the hot long words
+            parts.append("\n" + " " * int(rng.integers(17, 41)) + "x")
+        if rng.random() < 0.05:
+            o = int(rng.integers(0, len(filler) - 300))
+            parts.append(filler[o:o + 300])
+    return "".join(parts).encode("utf-8")
+
+
+@pytest.mark.parametrize("seg", [None, "1", "7"])
+def test_long_words_listed(knob, seg):
+    """words longer than kInline go to each counting workgroup's segment and k_count_long adds
+    them after the launch; a full segment (BPE355_LONG_SEG: entries per workgroup) sends the rest
+    to the table directly -- the same counts either way"""
+    knob("BPE355_REC_POOL", "1e8")
+    if seg:
+        knob("BPE355_LONG_SEG", seg)
+    data = _long_word_text(5, 120_000)
+    assert _device_word_counts(data, EOT) == _want_words(data, EOT)
+
+
+def test_long_words_file_segments(knob, tmp_path):
+    # segments are emptied behind every k_count2 launch of the file path
+    knob("BPE355_REC_POOL", "1e8")
+    knob("BPE355_SEG_MB", 1)
+    data = _long_word_text(6, 150_000)
+    p = tmp_path / "c.txt"
+    p.write_bytes(data)
+    got = bpe_amd.train_bpe(p, 800, EOT)
+    assert got == oracle.train_raw(data, 800, EOT)
 
 
 @pytest.mark.parametrize("shift", [1, 3, 7])

@@ -12,7 +12,7 @@ _lib.check(L.bpe_synth_corpus_device(ctypes.c_void_p(c.data_ptr()), n, 2, 0, 0, 
 torch.cuda.synchronize()
 L.bpe_set_timing(1)
 for i in range(3):
-    train_bpe_device(c.data_ptr(), n, 256, ["<|endoftext|>"])
+    train_bpe_device(c.data_ptr(), n, 256, ["<|endoftext|>"], keep_device_buffers=True)
     st = last_train_stats()
 print(f"mode {os.environ.get('BPE355_COUNT_MODE', '0')}: k_count2 {st['count_kernel_ms']:.2f} ms, "
       f"reduce {st['count_reduce_ms']:.2f} ms, count phase {st['t_count_ms']:.2f} ms, records {st['n_count_records']}",

@@ -47,12 +47,26 @@ def merges_sha(merges) -> str:
                                    for a, b in merges)).hexdigest()
 
 
+class ProgressLog(list):
+    """cpu_ref's progress list, also appended to a JSON-lines file as it grows (a long run can be
+    read while it goes)"""
+    def __init__(self, path):
+        super().__init__()
+        self.path = path
+
+    def append(self, x):
+        super().append(x)
+        if self.path:
+            with open(self.path, "a") as f:
+                f.write(json.dumps(x) + "\n")
+
+
 def leg(args):
-    mode, mb, vocab, cap_s, seed, flavour = args
+    mode, mb, vocab, cap_s, seed, flavour, plog = args
     from oracle import cpu_ref
     text = sample_text(mb, seed, flavour)
     nb = len(text.encode("utf-8"))
-    prog: list = []
+    prog: list = ProgressLog(plog if mode == "full" else None)
     t0 = time.perf_counter()
     _, merges, info = cpu_ref.train(text, vocab, [EOT], round_cap_s=cap_s if mode == "capped" else None,
                                     progress=prog)
@@ -65,7 +79,7 @@ def leg(args):
             "complete": info["complete"], "ms_per_round": round(per_round * 1e3, 3),
             "projected_wall_s": round(projected, 3), "MBps_projected": round(nb / projected / 1e6, 5),
             "MBps_measured": round(nb / wall / 1e6, 5) if info["complete"] else None,
-            "merges_sha256": merges_sha(merges), "progress": prog}
+            "merges_sha256": merges_sha(merges), "progress": list(prog)}
 
 
 def main():
@@ -76,8 +90,9 @@ def main():
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--flavour", type=int, default=0)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--progress-file", default=None, help="JSON lines of the full leg's progress")
     a = ap.parse_args()
-    legs = [(m, a.mb, a.vocab, a.cap_s, a.seed, a.flavour) for m in ("capped", "full")]
+    legs = [(m, a.mb, a.vocab, a.cap_s, a.seed, a.flavour, a.progress_file) for m in ("capped", "full")]
     with mp.get_context("fork").Pool(2) as pool:
         capped, full = pool.map(leg, legs)
     err = capped["projected_wall_s"] / full["wall_s"] - 1.0

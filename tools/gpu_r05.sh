@@ -20,6 +20,9 @@ for step in "$@"; do
   probe1)   # the merge-loop probe of the default configuration
     BPE355_PROBE=1 BPE355_LIB=build/variants/probe/libbpe355.so timeout -k 10 200 python -u bench.py --no-file --steps 1 --warmup 0 --no-encode --no-cpu-baseline --no-timing > $OUT/probe.log 2> $OUT/probe_err.log || { echo "probe failed"; tail -5 $OUT/probe_err.log; exit 1; }
     grep probe $OUT/probe_err.log > $OUT/merge_probe.txt; head -12 $OUT/merge_probe.txt ;;
+  count)
+    timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_count.py > $OUT/pytest_count.log 2>&1 || { echo "count tests failed"; tail -40 $OUT/pytest_count.log; exit 1; }
+    tail -1 $OUT/pytest_count.log ;;
   scale)
     timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_scale.py > $OUT/pytest_scale.log 2>&1 || { echo "scale tests failed"; tail -40 $OUT/pytest_scale.log; exit 1; }
     tail -1 $OUT/pytest_scale.log ;;

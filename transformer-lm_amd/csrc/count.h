@@ -26,6 +26,12 @@ struct RecPool {
     unsigned* wg_used;
     unsigned* page_ch;     // per page: records per coarse bin (kCoarse), written with page_used
     unsigned* wg_ch;       // per counting workgroup: its current page's coarse histogram
+    // words longer than kInline (their bytes are not in a record): per counting workgroup a
+    // segment of lw_per_wg entries {offset | len << 40}, added to the table by k_count_long after
+    // each k_count2 launch (lw == nullptr: k_count2 adds them itself)
+    unsigned long long* lw;
+    unsigned* lw_n;
+    unsigned lw_per_wg;
     int on;
 };
 
@@ -53,7 +59,9 @@ struct L2Tile {
 
 struct RecPoolOwner {
     std::unique_ptr<Arrays3> rec;    // the pool: lo, hi, meta
-    DevBuf<unsigned> page_used, n_pages, wg_used, page_ch, wg_ch;
+    DevBuf<unsigned> page_used, n_pages, wg_used, page_ch, wg_ch, lw_n;
+    DevBuf<unsigned long long> lw;
+    unsigned lw_per_wg = 0;
     DevBuf<unsigned> held, done, list, list_n;   // page selection of the incremental aggregation
     std::unique_ptr<Arrays3> B;                   // level-1 destination
     DevBuf<unsigned> coff, d_t0, fhist, n_tiles;
@@ -74,6 +82,9 @@ struct RecPoolOwner {
 };
 
 unsigned count2_grid(size_t n_chunks);
+// the long words k_count2 listed (R.lw) into the table; enqueued behind each k_count2 launch
+void count_long_launch(const uint8_t* text, const WordCounts& wc, unsigned long long* fill, unsigned* status,
+                       const RecPool& R, unsigned grid, hipStream_t s);
 void count2_launch(const uint8_t* text, size_t lo, size_t hi, size_t c0, size_t nc, unsigned grid,
                    const WordCounts& wc, unsigned long long* fill, unsigned* status, unsigned long long* ntok,
                    const RecPool& R, const unsigned long long* gate, hipStream_t s, hipEvent_t e0, hipEvent_t e1);

@@ -77,12 +77,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     __shared__ int s_stop, s_page, s_old;
     __shared__ unsigned s_used;
     __shared__ unsigned s_ch[kCoarse];   // the current page's records per coarse bin
+    __shared__ unsigned s_nlong;         // entries in this workgroup's long-word segment
     const int tid = threadIdx.x;
     for (int i = tid; i < kCache2; i += blockDim.x) { c_key[i] = 0; c_cnt[i] = 0; c_mark[i] = 0; }
     load_cls2(tid, blockDim.x);
     if (tid == 0) {
         s_page = R.on ? R.wg_page[blockIdx.x] : -1;
         s_used = R.on ? R.wg_used[blockIdx.x] : 0u;
+        s_nlong = R.lw ? R.lw_n[blockIdx.x] : 0u;
     }
     if (tid < kCoarse) s_ch[tid] = R.on ? R.wg_ch[(size_t)blockIdx.x * kCoarse + tid] : 0u;
     unsigned long long ntok = 0, inserted = 0, n_miss = 0, n_long = 0;
@@ -157,7 +159,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 
         // ---- the pre-tokens that start in this thread's 64 bytes
         // (analysis knob BPE355_COUNT_MODE, timing only -- counts are then incomplete: 1 masks
-        // only, 2 + token bounds, 3 + packing and hashing, 4 + the LDS cache, misses dropped)
+        // only, 2 + token bounds, 3 + packing and hashing, 4 + the LDS cache, misses dropped; 5 all
+        // but the words longer than kInline)
         if (mode == 1) continue;
         const size_t rem = n > base ? n - base : 0;
         const uint32_t tend = rem < (size_t)kWin ? (uint32_t)rem : (uint32_t)kWin;   // staged text end
@@ -189,6 +192,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
             const size_t gpos = base + r;
             if (len > (size_t)kInline) {
                 ++n_long;
+                if (mode == 5) continue;
+                // listed for k_count_long: hashing it here (byte loads from HBM, a byte-wise
+                // compare in the table) stalled the whole wave on one lane -- 12 of 47.5 ms of
+                // this kernel at 11.9 GB for 0.3 % of the pre-tokens (BPE355_COUNT_MODE=5)
+                if (R.lw && len < kMaxPretok) {
+                    const unsigned li = atomicAdd(&s_nlong, 1u);
+                    if (li < R.lw_per_wg) {
+                        R.lw[(size_t)blockIdx.x * R.lw_per_wg + li] = (unsigned long long)gpos | ((unsigned long long)len << 40);
+                        continue;
+                    }
+                }
                 bool ins;
                 table_add(s, s, gpos, len, 0, 0, hash_word(s, gpos, len), 1, kv, pos, mask, status, &ins);
                 inserted += ins;
@@ -268,6 +282,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
         R.wg_page[blockIdx.x] = s_page;
         R.wg_used[blockIdx.x] = s_used;
     }
+    if (tid == 0 && R.lw) R.lw_n[blockIdx.x] = s_nlong < R.lw_per_wg ? s_nlong : R.lw_per_wg;
     if (tid < kCoarse && R.on) R.wg_ch[(size_t)blockIdx.x * kCoarse + tid] = s_ch[tid];
     ntok = wave_sum(ntok);
     inserted = wave_sum(inserted);
@@ -279,6 +294,91 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
         if (n_long) atomicAdd(n_tok + 2, n_long);
         if (inserted) atomicAdd(fill, inserted);
     }
+}
+
+// bytes [a, a + len) and [b, b + len) of s equal (8 independent loads per step)
+__device__ __forceinline__ bool bytes_equal(const uint8_t* __restrict__ s, size_t a, size_t b, size_t len) {
+    for (size_t i = 0; i < len; i += 8) {
+        const size_t m = len - i < 8 ? len - i : 8;
+        uint64_t x = 0, y = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if ((size_t)j < m) {
+                x |= (uint64_t)s[a + i + j] << (8 * j);
+                y |= (uint64_t)s[b + i + j] << (8 * j);
+            }
+        if (x != y) return false;
+    }
+    return true;
+}
+
+constexpr int kLongSlots = 2048;   // k_count_long's LDS table (a segment holds ~1-3 K distinct words)
+constexpr int kLongProbe = 16;
+
+// The long words of counting workgroup b's segment into the table.  The frequent ones are
+// whitespace runs (at 2 GB of the bench corpus twelve words of 21-32 bytes make 480 K of the 855 K
+// long pre-tokens), so adding them one by one serialises on a few table slots (same-address
+// atomics): they are summed per segment first in an LDS table keyed by (hash, length), an
+// occurrence joining an entry only when its bytes equal the entry's first occurrence.  Then one
+// table add per entry.  The segment is emptied for the next k_count2 launch.
+__global__ void __launch_bounds__(256) k_count_long(const uint8_t* __restrict__ s, RecPool R,
+                                                    unsigned long long* __restrict__ kv,
+                                                    unsigned long long* __restrict__ pos, size_t mask,
+                                                    unsigned long long* __restrict__ fill, unsigned* __restrict__ status) {
+    __shared__ unsigned long long t_h[kLongSlots];   // the word hash (0: free, ~0: being claimed)
+    __shared__ unsigned long long t_pos[kLongSlots];
+    __shared__ unsigned t_len[kLongSlots], t_cnt[kLongSlots];
+    constexpr unsigned long long kClaim = ~0ULL;
+    for (int i = threadIdx.x; i < kLongSlots; i += blockDim.x) { t_h[i] = 0; t_cnt[i] = 0; }
+    __syncthreads();
+    const unsigned b = blockIdx.x;
+    const unsigned n = R.lw_n[b];
+    unsigned long long inserted = 0;
+    for (unsigned i = threadIdx.x; i < n; i += blockDim.x) {
+        const unsigned long long e = R.lw[(size_t)b * R.lw_per_wg + i];
+        const size_t gpos = (size_t)(e & kOffMask), len = (size_t)(e >> 40);
+        const uint64_t h = hash_word(s, gpos, len);
+        bool done = false;
+        if (h != 0 && h != kClaim) {
+            unsigned sl = (unsigned)(h >> 24) & (kLongSlots - 1);
+            for (int probe = 0; probe < kLongProbe && !done; ++probe, sl = (sl + 1) & (kLongSlots - 1)) {
+                unsigned long long k = t_h[sl];
+                if (k == 0) {
+                    k = atomicCAS(&t_h[sl], 0ULL, kClaim);
+                    if (k == 0) {   // claimed: position and length first (drained), then the hash
+                        t_pos[sl] = gpos;
+                        t_len[sl] = (unsigned)len;
+                        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        atomicExch(&t_h[sl], h);
+                        atomicAdd(&t_cnt[sl], 1u);
+                        done = true;
+                        break;
+                    }
+                }
+                // (a slot being claimed is passed over: the word may then sit twice; the table merges)
+                if (k == h && t_len[sl] == (unsigned)len && bytes_equal(s, t_pos[sl], gpos, len)) {
+                    atomicAdd(&t_cnt[sl], 1u);
+                    done = true;
+                }
+            }
+        }
+        if (!done) {
+            bool ins;
+            table_add(s, s, gpos, len, 0, 0, h, 1, kv, pos, mask, status, &ins);
+            inserted += ins;
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kLongSlots; i += blockDim.x) {
+        const unsigned long long h = t_h[i];
+        if (h == 0 || h == kClaim) continue;
+        bool ins;
+        table_add(s, s, (size_t)t_pos[i], (size_t)t_len[i], 0, 0, h, t_cnt[i], kv, pos, mask, status, &ins);
+        inserted += ins;
+    }
+    inserted = wave_sum(inserted);
+    if ((threadIdx.x & 63) == 0 && inserted) atomicAdd(fill, inserted);
+    if (threadIdx.x == 0) R.lw_n[b] = 0u;   // (n was read by every thread before the first barrier)
 }
 
 // ------------------------------------------------------------------ record aggregation
@@ -671,6 +771,13 @@ void count2_launch(const uint8_t* text, size_t lo, size_t hi, size_t c0, size_t 
     BPE_HIP(hipGetLastError());
 }
 
+void count_long_launch(const uint8_t* text, const WordCounts& wc, unsigned long long* fill, unsigned* status,
+                       const RecPool& R, unsigned grid, hipStream_t s) {
+    if (!R.lw) return;
+    hipLaunchKernelGGL(k_count_long, dim3(grid), dim3(256), 0, s, text, R, wc.kv.p, wc.pos.p, wc.cap - 1, fill, status);
+    BPE_HIP(hipGetLastError());
+}
+
 namespace {
 struct ScratchArrays {
     std::mutex m;
@@ -803,6 +910,13 @@ void RecPoolOwner::init(size_t n_bytes, unsigned grid, hipStream_t s) {
     BPE_HIP(hipMemsetAsync(wg_ch.p, 0, 4ull * grid * kCoarse, s));
     held.alloc(max_pages);
     done.alloc(max_pages);
+    // long-word segments: ~1 entry per KiB of text (the bench corpus has one per 2.3 KiB); a
+    // full segment sends the rest of its workgroup's long words to the table directly
+    lw_per_wg = (unsigned)std::min<size_t>(1u << 24, std::max<size_t>(1024, n_bytes / 1024 / grid + 1));
+    if (const char* e = std::getenv("BPE355_LONG_SEG")) lw_per_wg = (unsigned)std::max(1, std::atoi(e));   // test knob
+    lw.alloc((size_t)lw_per_wg * grid);
+    lw_n.alloc(grid);
+    BPE_HIP(hipMemsetAsync(lw_n.p, 0, 4ull * grid, s));
     // the aggregation's buffers, sized for one batch of every page (no allocation while the
     // file path aggregates between segment copies): level 1 lands in B, level 2 back in the pages
     B = scratch_take(cap);
@@ -842,6 +956,9 @@ RecPool RecPoolOwner::dev() const {
     R.wg_used = wg_used.p;
     R.page_ch = page_ch.p;
     R.wg_ch = wg_ch.p;
+    R.lw = lw.p;
+    R.lw_n = lw_n.p;
+    R.lw_per_wg = lw_per_wg;
     R.on = rec != nullptr;
     return R;
 }

@@ -33,8 +33,18 @@ constexpr unsigned long long kBusy = 1ULL << 63;
 // A longer one fails the call with BPE_E_LIMIT (status bit 2), in training and in encoding.
 constexpr unsigned long long kMaxPretok = 1ULL << 23;
 
+// Two 64-bit multiplies (the earlier mix64(lo ^ mix64(hi ...)) took four, and on the count and
+// encode scans, which hash every pre-token, those quarter-rate v_mul's were the largest VALU cost):
+// hi and len folded in through one odd multiply, then a one-multiply finalizer whose xor-shifts
+// bring every input bit into the low bits (the table slots) and the high ones (bins, cache sets).
+// Checked against the old form on the bench corpus's 934 K distinct words: no full collisions,
+// the same bin / cache-set spread and table probe length (tools/hash_quality.py,
+// profiles/r05/j_hash_quality.json).
 __host__ __device__ inline uint64_t short_hash(uint64_t lo, uint64_t hi, size_t len) {
-    return mix64(lo ^ mix64(hi ^ (len << 56) ^ 0x9E3779B97F4A7C15ULL));
+    uint64_t z = lo ^ ((hi ^ (uint64_t)len) * 0x9E3779B97F4A7C15ULL);
+    z ^= z >> 32;
+    z *= 0xD6E8FEB86659FD93ULL;
+    return z ^ (z >> 32);
 }
 
 // The staged window lives in dynamic LDS (kPadded bytes per workgroup), addressed directly:

@@ -527,6 +527,7 @@ void CountPass::range(size_t lo, size_t hi) {
         RecPool R{};
         if (rec) R = rec->dev();
         count2_launch(text, lo, hi, c0, c1 - c0, grid2, wc, fill.p, status.p, ntok.p, R, gate, s, e0, e1);
+        count_long_launch(text, wc, fill.p, status.p, R, grid2, s);
         return;
     }
     // timed launch: the events are stamped by the kernel's own dispatch packet (the interval
