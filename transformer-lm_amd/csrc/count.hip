@@ -296,22 +296,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     }
 }
 
-// bytes [a, a + len) and [b, b + len) of s equal (8 independent loads per step)
-__device__ __forceinline__ bool bytes_equal(const uint8_t* __restrict__ s, size_t a, size_t b, size_t len) {
-    for (size_t i = 0; i < len; i += 8) {
-        const size_t m = len - i < 8 ? len - i : 8;
-        uint64_t x = 0, y = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if ((size_t)j < m) {
-                x |= (uint64_t)s[a + i + j] << (8 * j);
-                y |= (uint64_t)s[b + i + j] << (8 * j);
-            }
-        if (x != y) return false;
-    }
-    return true;
-}
-
 constexpr int kLongSlots = 2048;   // k_count_long's LDS table (a segment holds ~1-3 K distinct words)
 constexpr int kLongProbe = 16;
 

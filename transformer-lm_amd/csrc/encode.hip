@@ -459,9 +459,7 @@ __device__ __forceinline__ size_t enc_table_add(const uint8_t* __restrict__ s, s
             if (k == mine && k0 == ~wl) return slot;
         } else if (!(k & kInl) && (k >> 40) == len) {
             const size_t q = (k & kOffMask) - 1;
-            bool eq = true;
-            for (size_t i = 0; i < len && eq; ++i) eq = s[q + i] == s[gp + i];
-            if (eq) return slot;
+            if (bytes_equal(s, q, gp, len)) return slot;
         }
         slot = (slot + 1) & mask;
     }

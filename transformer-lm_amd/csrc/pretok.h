@@ -134,15 +134,57 @@ __device__ __forceinline__ Idx token_end(const Src& s, Idx n, Idx p) {
     return (e == n || last == p) ? e : last;
 }
 
-// FNV-1a over the bytes, then a final avalanche: used to place words in the count table.
-template <class Src>
-__device__ __forceinline__ uint64_t hash_word(const Src& s, size_t p, size_t len) {
+// Bytes [p, p + len) of s as little-endian 8-byte chunks (the last one zero-padded), read with
+// aligned 8-byte loads and funnel shifts: one load per chunk, and never past the aligned word
+// that holds byte p + len - 1 (which lies in the same page as that byte).
+struct Chunks8 {
+    const uint64_t* a;
+    unsigned sh;
+    size_t left;
+    uint64_t cur;
+    __device__ __forceinline__ Chunks8(const uint8_t* __restrict__ s, size_t p, size_t len) {
+        const uintptr_t x = reinterpret_cast<uintptr_t>(s + p);
+        a = reinterpret_cast<const uint64_t*>(x & ~(uintptr_t)7);
+        sh = (unsigned)(x & 7) * 8;
+        left = len;
+        cur = len ? a[0] : 0;
+    }
+    __device__ __forceinline__ uint64_t next() {   // left > 0
+        ++a;
+        uint64_t v;
+        if (sh == 0) {
+            v = cur;
+            cur = left > 8 ? *a : 0;
+        } else {   // the chunk runs into the next aligned word unless it ends in this one
+            const uint64_t nx = sh / 8 + left > 8 ? *a : 0;
+            v = (cur >> sh) | (nx << (64 - sh));
+            cur = nx;
+        }
+        if (left < 8) v &= (1ULL << (8 * left)) - 1;
+        left = left > 8 ? left - 8 : 0;
+        return v;
+    }
+};
+
+// The hash of a word longer than kInline (the count table's and the encoder's), 8 bytes per step,
+// then a final avalanche.  (The r04 form, FNV-1a byte by byte, made one dependent load per byte:
+// a wave waited ~25 round trips on any lane holding such a word.)
+__device__ __forceinline__ uint64_t hash_word(const uint8_t* __restrict__ s, size_t p, size_t len) {
+    Chunks8 c(s, p, len);
     uint64_t h = 0xcbf29ce484222325ULL;
-    for (size_t i = 0; i < len; ++i) h = (h ^ s[p + i]) * 0x100000001b3ULL;
+    while (c.left) h = (h ^ c.next()) * 0x9E3779B97F4A7C15ULL;
     return mix64(h ^ len);
 }
 __device__ __forceinline__ uint64_t hash_word(const uint8_t* __restrict__ s, size_t len) {
     return hash_word(s, 0, len);
+}
+
+// bytes [a, a + len) and [b, b + len) of s are equal (8 bytes per step)
+__device__ __forceinline__ bool bytes_equal(const uint8_t* __restrict__ s, size_t a, size_t b, size_t len) {
+    Chunks8 x(s, a, len), y(s, b, len);
+    while (x.left)
+        if (x.next() != y.next()) return false;
+    return true;
 }
 
 }  // namespace bpe

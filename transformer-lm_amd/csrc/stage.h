@@ -68,6 +68,18 @@ __device__ __forceinline__ void pack_word(const Src& t, size_t p, size_t len, ui
     }
 }
 
+// the word at q of s equals the one at p of t (len > kInline)
+template <class Src>
+__device__ __forceinline__ bool words_equal(const uint8_t* __restrict__ s, size_t q, const Src& t, size_t p, size_t len) {
+    bool eq = true;
+    for (size_t i = 0; i < len && eq; ++i) eq = s[q + i] == t[p + i];
+    return eq;
+}
+__device__ __forceinline__ bool words_equal(const uint8_t* __restrict__ s, size_t q, const uint8_t* t, size_t p,
+                                            size_t len) {
+    return t == s ? bytes_equal(s, q, p, len) : words_equal<const uint8_t*>(s, q, t, p, len);
+}
+
 // Add `c` occurrences of a word (c = 0: find or insert only).  Returns its slot, or ~0 when
 // the probe limit is hit (status bit 1); *inserted = whether this call created the key.
 // wl/wh: the packed bytes (words <= 16 bytes); t/p: the word's bytes for longer ones.
@@ -107,8 +119,7 @@ __device__ __forceinline__ size_t table_add(const uint8_t* __restrict__ s, const
                 pack_word(s, q, len, l2, h2);
                 eq = l2 == wl && h2 == wh;
             } else {
-                eq = true;
-                for (size_t i = 0; i < len && eq; ++i) eq = s[q + i] == t[p + i];
+                eq = words_equal(s, q, t, p, len);
             }
         }
         if (eq) {
