@@ -23,6 +23,9 @@ for step in "$@"; do
   count)
     timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_count.py > $OUT/pytest_count.log 2>&1 || { echo "count tests failed"; tail -40 $OUT/pytest_count.log; exit 1; }
     tail -1 $OUT/pytest_count.log ;;
+  trainpar)   # the training parity tests (goldens, tie-heavy, scale)
+    timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_train.py tests/test_gpu_scale.py > $OUT/pytest_trainpar.log 2>&1 || { echo "train parity tests failed"; tail -40 $OUT/pytest_trainpar.log; exit 1; }
+    tail -1 $OUT/pytest_trainpar.log ;;
   scale)
     timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_scale.py > $OUT/pytest_scale.log 2>&1 || { echo "scale tests failed"; tail -40 $OUT/pytest_scale.log; exit 1; }
     tail -1 $OUT/pytest_scale.log ;;

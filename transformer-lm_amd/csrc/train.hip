@@ -890,13 +890,15 @@ __global__ void __launch_bounds__(256) k_argmax(RoundState* __restrict__ st, Pai
 // ------------------------------------------------------------------ batched rounds
 // Several merges per round trip, exactly.  At a state S, let P1 > P2 > ... be the candidates in
 // the reference's order (count, then bytes; train.py:187-189).  The top k form a batch when
-//   (1) their tokens are pairwise disjoint and (2) a != b for each (k > 1),
+//   (1) no member's b is any member's a (members may share an a, or share a b) and
+//   (2) a != b for each (k > 1),
 //   (3) each a + b is new bytes: not an existing token, not another member's (vocab.py:29),
 //   (4) count(Pk) >= T and count(Pk) > count of the next candidate in C (keys outside C are
 //       below T), so every pair outside the batch has a count strictly below count(Pk).
 // Then the reference takes P1, ..., Pk in exactly that order:
-//   * disjoint tokens: merging Pi never touches an occurrence of Pj (j != i), so Pj's count is
-//     unchanged until its turn; with a != b every occurrence of Pi is merged;
+//   * merging Pi = (ai, bi) removes only the pairs (x, ai) and (bi, y) at its occurrences; with
+//     no b equal to an a, no member has either shape and no two members' occurrences overlap, so
+//     Pj's count is unchanged until its turn; with a != b every occurrence of Pi is merged;
 //   * an occurrence of a pair created by the batch sits where, before the batch, two original
 //     tokens met -- an occurrence of an old pair that is not a member (members' occurrences are
 //     all merged) -- so its count is below count(Pk); old non-members only lose counts.
@@ -916,12 +918,23 @@ constexpr int kTopM = kMaxBatch + 1;
 constexpr int kClashI = kMaxBatch <= 16 ? 16 : 32;
 constexpr int kClashJ = 64 / kClashI;
 constexpr unsigned kLdsB = 128;          // LDS-summed cells per member (ids below kLdsB)
+// Batch members may share an a or a b (rule (1) below).  With 0, every member's tokens are
+// distinct from the others' (rounds 1-4): on the bench corpus's merge sequence that rule alone
+// ends 2583 of 3682 batches against 498 of 2430 (tools/sim_batch.py, cap 16)
+#ifndef BPE355_SHARE_TOK
+#define BPE355_SHARE_TOK 1
+#endif
+constexpr bool kShareTok = BPE355_SHARE_TOK != 0;
 
 struct BatchMember {
     unsigned a, b, nw, slot;
     long long cnt;
     unsigned long long hash, k8, pw;
     unsigned ln, list_beg, list_len, use_list, cov_beg, cov_len, pool_off, isnew;
+    // members sharing a token: the first member with this a (ga) / this b (gb) holds the mask of
+    // every member with it, the others 0.  The apply updates (x, a) and (b, y) once, from the
+    // group's summed cells (a key has one updater).
+    unsigned ga, gb;
 };
 struct Batch {
     int stop;            // 0 run, -1 nothing to do, > 0 the halt the apply raises
@@ -1344,7 +1357,8 @@ __device__ __forceinline__ void select_core(const RoundState* __restrict__ st, B
     if (pub && lane == 0) probe_stamp(st, ptrip, 18);
     const unsigned long long h = m.ha * m.pb + m.hb;
     const unsigned lk = m.la + m.lb;
-    // (1) tokens disjoint from, and (3) new bytes different from, every earlier candidate's.
+    // (1) a different from every earlier candidate's b and b from every earlier a (kShareTok;
+    // else all four tokens distinct), and (3) new bytes different from every earlier candidate's.
     // The kClashI x kClashI (i, j) pairs are spread over the wave: lane L checks i = L % kClashI
     // against j = L / kClashI + t * kClashJ, then the kClashJ lanes of each i combine (one pass of
     // lane shuffles instead of a serial readlane chain over j)
@@ -1362,7 +1376,7 @@ __device__ __forceinline__ void select_core(const RoundState* __restrict__ st, B
             const unsigned long long hj = __shfl(h, j);
             const unsigned lj = __shfl((int)lk, j), laj = __shfl((int)m.la, j);
             if (j < ci && iv) {
-                const bool tc = aj == ai || aj == bi || bj == ai || bj == bi;
+                const bool tc = aj == bi || bj == ai || (!kShareTok && (aj == ai || bj == bi));
                 clash |= tc;
                 if (!tc && hj == hi && lj == li_) {   // equal hashes: compare the bytes (rare)
                     bool eq = true;
@@ -1432,7 +1446,30 @@ __device__ __forceinline__ void select_core(const RoundState* __restrict__ st, B
     const bool mem = i < k;
     const unsigned lu = m.za <= m.zb ? m.za : m.zb, bu = m.za <= m.zb ? m.ba : m.bb;
     const bool use = lu != kNoAnc && lu <= X.full_threshold;
-    const unsigned add_pool = mem && fr ? lk : 0u, add_fresh = mem && fr ? 1u : 0u, add_list = mem && use ? lu : 0u;
+    // the members' token groups (equal a's, equal b's: the group's first member carries its mask)
+    // and posting lists two members share (the later one walks none of it: the word is claimed
+    // once and every member's hits are found on it)
+    unsigned ga = 0, gb = 0;
+    bool dup_list = false;
+    if (kShareTok) {
+#pragma unroll
+        for (int j = 0; j < kMaxBatch; ++j) {
+            const unsigned aj = __builtin_amdgcn_readlane((int)e.a, j), bj = __builtin_amdgcn_readlane((int)e.b, j);
+            const unsigned uj = __builtin_amdgcn_readlane((int)bu, j), lj = __builtin_amdgcn_readlane((int)lu, j);
+            const bool usej = __builtin_amdgcn_readlane((int)use, j) != 0;
+            const bool in = j < k;   // (uniform)
+            ga |= (unsigned)(in && aj == e.a) << j;
+            gb |= (unsigned)(in && bj == e.b) << j;
+            dup_list |= in && j < i && usej && uj == bu && lj == lu;
+        }
+        const unsigned below = (1u << (i & 31)) - 1;   // (lanes i >= k are not members)
+        if (ga & below) ga = 0;
+        if (gb & below) gb = 0;
+    } else {
+        ga = gb = 1u << i;
+    }
+    const unsigned add_pool = mem && fr ? lk : 0u, add_fresh = mem && fr ? 1u : 0u,
+                   add_list = mem && use && !dup_list ? lu : 0u;
     unsigned pre_pool = add_pool, pre_fresh = add_fresh, pre_list = add_list;   // inclusive scans
     for (int d = 1; d <= kMaxBatch; d <<= 1) {
         const unsigned tp = __shfl_up((int)pre_pool, d), tf = __shfl_up((int)pre_fresh, d),
@@ -1461,6 +1498,8 @@ __device__ __forceinline__ void select_core(const RoundState* __restrict__ st, B
         M.cov_beg = bu;
         M.cov_len = fr ? lu : kNoAnc;   // dedupe: uncovered until the next index build
         M.pool_off = pool_used + pre_pool;
+        M.ga = ga;
+        M.gb = gb;
         OB.m[i] = M;
         if (pub) {
             O.m_a[round + i] = e.a; O.m_b[round + i] = e.b; O.m_new[round + i] = M.nw;
@@ -1552,8 +1591,8 @@ __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigne
     const unsigned long long c = S.cnt[i];   // issued with the slot
     TokT e[W];
     __builtin_memcpy(e, r, sizeof(e));
-    // the members this word holds: members' tokens are disjoint and their new tokens fresh, so a
-    // rewrite neither makes nor breaks another member's pair and the original word decides
+    // the members this word holds: no member's b is another's a and the new tokens are fresh, so
+    // a rewrite neither makes nor breaks another member's pair and the original word decides
     unsigned hits = 0;
     for (int j = 0; j < B.k; ++j) {
         const TokT ta = (TokT)sm_a[j], tb = (TokT)sm_b[j];
@@ -1828,7 +1867,8 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
                                                                     Partial* __restrict__ part,
                                                                     Partial* __restrict__ list, int scan_only) {
     __shared__ unsigned s_tok[3 * kMaxBatch];
-    __shared__ unsigned s_role[3 * kMaxBatch];   // S entry: member << 3 | roles (1 a, 2 b, 4 new)
+    __shared__ unsigned s_role[3 * kMaxBatch];   // S entry: members' mask << 3 | role (1 a, 2 b, 4 new)
+    __shared__ unsigned s_grp[2 * kMaxBatch];    // member j's a group (2j) and b group (2j + 1)
     __shared__ unsigned s_filt[kSFilterWords];   // bit (x mod 4096): x may be in S
     __shared__ int s_ns;
     __shared__ Cand s_wave[kApplyBatchThreads / 64];
@@ -1847,6 +1887,8 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     const int bs_trip = bs->trip;
     const unsigned st_nC = st->nC;   // scan_only: no admissions during the scan, so stable
     const unsigned t_raw = tid < 3 * kMaxBatch ? reinterpret_cast<const unsigned*>(&B.m[tid / 3])[tid % 3] : ~0u;
+    static_assert(offsetof(BatchMember, gb) == offsetof(BatchMember, ga) + 4, "ga, gb adjacent");
+    const unsigned g_raw = tid < 3 * kMaxBatch && tid % 3 < 2 ? (&B.m[tid / 3].ga)[tid % 3] : 0u;
     if (!scan_only && b_stop) {   // no trip: part[] and the list keep what the next select reads
         if (b_stop > 0 && blockIdx.x == 0 && tid == 0) st->halt = b_stop;   // the select's halt
         return;
@@ -1864,22 +1906,25 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
         const int i = tid;
         const bool have = i < 3 * k;
         const unsigned ti = have ? t_raw : ~0u;
-        // For k > 1 the 3k tokens are distinct: the members' tokens are disjoint, a != b, and the
-        // new tokens are fresh ids (select_core's rule).  For k == 1 only a == b can repeat (a new
-        // token's bytes are longer than a's and b's), so no general dedupe pass is needed.
+        // For k > 1 a token has one role: no member's b is another's a, a != b, and the new tokens
+        // are fresh ids (select_core's rule); an a (a b) several members share is kept once, by
+        // the group's first member, with the group's mask.  For k == 1 only a == b can repeat (a
+        // new token's bytes are longer than a's and b's), so no general dedupe pass is needed.
         unsigned roles = 1u << (i % 3);
+        const unsigned gm = i % 3 == 2 ? 1u << (i / 3) : g_raw;   // the members behind this entry
         bool dup = false;
         if (k == 1 && __builtin_amdgcn_readlane((int)ti, 0) == __builtin_amdgcn_readlane((int)ti, 1)) {
             if (i == 0) roles = 3u;   // a == b: one entry, both roles
             dup = i == 1;
         }
-        const bool keep = have && !dup;
+        if (have && i % 3 < 2) s_grp[2 * (i / 3) + i % 3] = gm;
+        const bool keep = have && !dup && gm != 0;
         const unsigned long long km = __ballot(keep);
         for (unsigned w = i; w < kSFilterWords; w += 64) s_filt[w] = 0;
         if (keep) {
             const unsigned pos = __builtin_amdgcn_mbcnt_hi((unsigned)(km >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)km, 0u));
             s_tok[pos] = ti;
-            s_role[pos] = (unsigned)(i / 3) << 3 | roles;
+            s_role[pos] = gm << 3 | roles;
             atomicOr(&s_filt[(ti >> 5) % kSFilterWords], 1u << (ti & 31));
         }
         if (i == 0) {
@@ -1909,6 +1954,16 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
         return r;
     };
     auto in_S = [&](unsigned x) { return find_S(x) >= 0; };
+    // the cells at index ci of the members in mask (one load unless members share the token)
+    auto cell_sum = [&](unsigned mask, size_t ci) -> unsigned long long {
+        unsigned long long t = 0;
+        while (mask) {
+            const unsigned j = (unsigned)__builtin_ctz(mask);
+            mask &= mask - 1;
+            t += LRc[(size_t)j * lr_member + ci];
+        }
+        return t;
+    };
     const long long T2 = T2raw < T ? T : T2raw;
     Cand best = cand_none();   // this thread's best candidate (exact argmax)
     unsigned n_ins = 0;        // pair-table keys this thread inserted
@@ -1968,14 +2023,19 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
             ce[u] = make_uint4(0, 0, 0, 0);
             if (v < n_cell) {
                 const unsigned j = v / per_member, r = v % per_member, x = r >> 2, op = r & 3;
-                dv[u] = LRc[(size_t)j * lr_member + 2 * (size_t)x + (op >> 1)];
+                const size_t ci = 2 * (size_t)x + (op >> 1);
+                dv[u] = LRc[(size_t)j * lr_member + ci];
+                if (kShareTok && !(op & 1)) {   // (x, a_j) or (b_j, x): one updater per token group
+                    const unsigned gmask = s_grp[2 * j + (op >> 1)];
+                    if (gmask != 1u << j) dv[u] = gmask ? cell_sum(gmask, ci) : 0ull;
+                }
             } else if (v < n_cell + n_sp) {
                 const unsigned sp = v - n_cell;
                 const unsigned p = s_tok[sp / ns], q = s_tok[sp % ns];
                 const unsigned rp = s_role[sp / ns], rq = s_role[sp % ns];
-                // q's member sees p on its left (cell 2p), p's member sees q on its right (2q + 1)
-                if (rq & 5) dv[u] = LRc[(size_t)(rq >> 3) * lr_member + 2 * (size_t)p];
-                if (rp & 6) dw[u] = LRc[(size_t)(rp >> 3) * lr_member + 2 * (size_t)q + 1];
+                // q's members see p on their left (cell 2p), p's see q on their right (2q + 1)
+                if (rq & 5) dv[u] = cell_sum(rq >> 3, 2 * (size_t)p);
+                if (rp & 6) dw[u] = cell_sum(rp >> 3, 2 * (size_t)q + 1);
             } else if (v < n_items) {
                 ce[u] = P.C[v - n_cell - n_sp];
             }
@@ -2005,7 +2065,7 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
                 const unsigned sp = v - n_cell;
                 const unsigned rp = s_role[sp / ns], rq = s_role[sp % ns];
                 const long long lq = (long long)dv[u], lp = (long long)dw[u];
-                const bool popped = (rp >> 3) == (rq >> 3) && (rp & 1) && (rq & 2);
+                const bool popped = ((rp >> 3) & (rq >> 3)) != 0 && (rp & 1) && (rq & 2);
                 long long inc = 0, dec = 0;
                 if (rq & 1) dec += lq;
                 if (rq & 4) inc += lq;
@@ -2025,8 +2085,8 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
                 // does an item of this trip update the key?
                 const int sp_ = find_S(p), sq_ = find_S(q);
                 const unsigned rp = sp_ >= 0 ? s_role[sp_] : 0u, rq = sq_ >= 0 ? s_role[sq_] : 0u;
-                const unsigned long long t1 = (rq & 5) ? LRc[(size_t)(rq >> 3) * lr_member + 2 * (size_t)p] : 0ull;
-                const unsigned long long t2 = (rp & 6) ? LRc[(size_t)(rp >> 3) * lr_member + 2 * (size_t)q + 1] : 0ull;
+                const unsigned long long t1 = (rq & 5) ? cell_sum(rq >> 3, 2 * (size_t)p) : 0ull;
+                const unsigned long long t2 = (rp & 6) ? cell_sum(rp >> 3, 2 * (size_t)q + 1) : 0ull;
                 touched[u] = (t1 | t2) != 0;
                 hf[u] = P.flag[ce[u].x];
                 hc[u] = P.cnt[ce[u].x];
