@@ -64,6 +64,17 @@ for step in "$@"; do
       env $LIBENV timeout -k 10 300 python -u bench.py --no-file --no-encode --no-cpu-baseline --steps 3 --warmup 1 > $OUT/abvar_${lib}_$rep.log 2>&1 || { echo "abvar failed"; tail -20 $OUT/abvar_${lib}_$rep.log; exit 1; }
       python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().split(chr(10))[-1]); m=d['merge_loop']; print('$lib rep $rep merge_ms', m['ms'], 'us_per_trip', m['us_per_trip'], 'k_us', m['k_merge_batch_us'], 'trips', m['trips'], 'count_ms', d['device_resident']['phases_ms']['t_count_ms'] if d.get('device_resident') else None, 'parity', d['parity']['parity'])" $OUT/abvar_${lib}_$rep.log
     done; done ;;
+  abmulti:*)   # merge phase: the default library and build/variants/{A,B,...} (abmulti:A,B), alternating, 2 reps
+    VS="default ${step#abmulti:}"; VS=${VS//,/ }
+    for rep in 1 2; do for lib in $VS; do
+      if [ $lib = default ]; then LIBENV=""; else LIBENV="BPE355_LIB=build/variants/$lib/libbpe355.so"; fi
+      env $LIBENV timeout -k 10 300 python -u bench.py --no-file --no-encode --no-cpu-baseline --steps 3 --warmup 1 > $OUT/abm_${lib}_$rep.log 2>&1 || { echo "abmulti failed"; tail -20 $OUT/abm_${lib}_$rep.log; exit 1; }
+      python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().split(chr(10))[-1]); m=d['merge_loop']; print('$lib rep $rep merge_ms', m['ms'], 'us_per_trip', m['us_per_trip'], 'k_us', m['k_merge_batch_us'], 'trips', m['trips'], 'parity', d['parity']['parity'])" $OUT/abm_${lib}_$rep.log
+    done; done ;;
+  trace:*)   # the select's statistics (a BPE355_STATS_CODE build): k histogram, why batches end
+    V=${step#trace:}
+    BPE355_TRACE=1 BPE355_LIB=build/variants/$V/libbpe355.so timeout -k 10 200 python -u bench.py --no-file --steps 1 --warmup 0 --no-encode --no-cpu-baseline --no-timing > $OUT/trace_$V.log 2> $OUT/trace_err_$V.log || { echo "trace failed"; tail -5 $OUT/trace_err_$V.log; exit 1; }
+    grep -E "trips:|batch ended" $OUT/trace_err_$V.log ;;
   probeab:*)   # the merge-loop probe with an env knob at 1 and 0
     V=${step#probeab:}
     for f in 1 0; do

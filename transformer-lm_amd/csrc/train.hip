@@ -917,7 +917,10 @@ constexpr int kTopM = kMaxBatch + 1;
 // the select's clash check: candidates i < kClashI (a power of two >= kMaxBatch), kClashJ lanes each
 constexpr int kClashI = kMaxBatch <= 16 ? 16 : 32;
 constexpr int kClashJ = 64 / kClashI;
-constexpr unsigned kLdsB = 128;          // LDS-summed cells per member (ids below kLdsB)
+#ifndef BPE355_LDS_B
+#define BPE355_LDS_B 128
+#endif
+constexpr unsigned kLdsB = BPE355_LDS_B;   // LDS-summed cells per member (ids below kLdsB)
 // Batch members may share an a or a b (rule (1) below).  With 0, every member's tokens are
 // distinct from the others' (rounds 1-4): on the bench corpus's merge sequence that rule alone
 // ends 2583 of 3682 batches against 498 of 2430 (tools/sim_batch.py, cap 16)
@@ -925,6 +928,12 @@ constexpr unsigned kLdsB = 128;          // LDS-summed cells per member (ids bel
 #define BPE355_SHARE_TOK 1
 #endif
 constexpr bool kShareTok = BPE355_SHARE_TOK != 0;
+// Rule (4'): a tied non-member that seeds member j's new pairs cuts the batch after P_j (1), or
+// back to the members above the tie (0, rounds 1-4)
+#ifndef BPE355_TIE_BY_MEMBER
+#define BPE355_TIE_BY_MEMBER 1
+#endif
+constexpr bool kTieByMember = BPE355_TIE_BY_MEMBER != 0;
 
 struct BatchMember {
     unsigned a, b, nw, slot;
@@ -968,6 +977,9 @@ struct BatchState {
     unsigned list_n[2];
     unsigned long long n_overflow, n_headmiss, n_short, k_hist[kMaxBatch + 1];   // diagnostics
     unsigned long long k1_why[6];   // single-merge trips: P1 a == b / P1 not fresh / no list / P2 fails / tie / end
+    // what ended each batch: the cap / the ranked list ran out / candidate k failed the token or
+    // freshness rules / the count gap or a tie at the boundary cut it / P1 not batchable
+    unsigned long long end_why[5];
 };
 // the candidate list the select ranks, one thread per entry (build knob BPE355_LIST_CAP, a multiple
 // of 64; a trip whose list overflows it takes P1 alone and raises T2).  128 took 56 more trips at
@@ -1407,7 +1419,11 @@ __device__ __forceinline__ void select_core(const RoundState* __restrict__ st, B
         // (4') a tie at the boundary is harmless unless a tied non-member could seed a new pair:
         // a pair created by the batch has at most the count of the old pair (x, a_j) or (b_j, y)
         // it replaces, so with every tied non-member free of those shapes, no new pair reaches
-        // count(Pk).  Every key >= T2 is listed, so the tied keys are all in S.all.
+        // count(Pk).  Every key >= T2 is listed, so the tied keys are all in S.all.  A pair
+        // member j creates exists only after P_j's merge, so it can precede only members after j:
+        // with j the first member a tied non-member seeds, the batch keeps P1 .. P_j (and at
+        // least the members above the tie).  Former members past the cut never seed one (no b
+        // of one member is another's a), so the shorter batch needs no second check.
         if (k_strict < k && k > 1) {
             const long long c = readlane64((unsigned long long)e.cnt, k - 1);
             unsigned ma[kMaxBatch], mb[kMaxBatch], ms[kMaxBatch];
@@ -1417,20 +1433,22 @@ __device__ __forceinline__ void select_core(const RoundState* __restrict__ st, B
                 mb[j] = __builtin_amdgcn_readlane((int)e.b, j);
                 ms[j] = __builtin_amdgcn_readlane((int)e.slot, j);
             }
-            bool bad = false;
+            int jb = k;   // the first member a tied non-member seeds (k: none)
             for (int t = lane; t < nl; t += 64) {
                 const Cand y = S.all[t];
                 if (y.cnt != c) continue;
-                bool member = false, seeds = false;
+                bool member = false;
+                int js = k;
 #pragma unroll
                 for (int j = 0; j < kMaxBatch; ++j) {
                     if (j >= k) break;
                     member |= y.slot == ms[j];
-                    seeds |= y.b == ma[j] || y.a == mb[j];
+                    if (js == k && (y.b == ma[j] || y.a == mb[j])) js = j;
                 }
-                bad |= !member && seeds;
+                if (!member) jb = min(jb, js);
             }
-            k = __ballot(bad) ? k_strict : k;
+            for (int o = 32; o > 0; o >>= 1) jb = min(jb, __shfl_xor(jb, o));
+            k = min(k, max(kTieByMember ? jb + 1 : (jb < k ? 0 : k), k_strict));
         } else {
             k = k_strict;
         }
@@ -1440,6 +1458,10 @@ __device__ __forceinline__ void select_core(const RoundState* __restrict__ st, B
     if (BPE355_STATS_CODE && pub && k == 1 && lane == 0) {
         const int why = p1.a == p1.b ? 0 : !fr0 ? 1 : nf == 1 ? 2 : k_rule == 1 ? 3 : 4;
         atomicAdd(&bs->k1_why[why], 1ull);
+    }
+    if (BPE355_STATS_CODE && pub && lane == 0) {
+        const int why = !(p1.a != p1.b && fr0) ? 4 : k < k_rule ? 3 : k_rule == maxb ? 0 : k_rule == nf ? 1 : 2;
+        atomicAdd(&bs->end_why[why], 1ull);
     }
     k = min(k, n_rounds - round);
     // per member: pool offset, new id, posting-list prefix (exclusive scans over lanes < k)
@@ -3416,6 +3438,9 @@ void MergeLoop<TokT>::run() {
             for (int i = 0; i <= kMaxBatch; ++i) std::fprintf(stderr, " %llu", b.k_hist[i]);
             std::fprintf(stderr, "; k=1 because: a==b %llu, not fresh %llu, no list %llu, P2 fails %llu, tie %llu\n",
                          b.k1_why[0], b.k1_why[1], b.k1_why[2], b.k1_why[3], b.k1_why[4]);
+            std::fprintf(stderr, "[bpe355] batch ended by: cap %llu, list ran out %llu, candidate k failed the token "
+                         "rules %llu, count gap / tie %llu, P1 alone %llu\n", b.end_why[0], b.end_why[1],
+                         b.end_why[2], b.end_why[3], b.end_why[4]);
         }
     }
     out_.stats.merge_kernel_ms = k1_ms;
