@@ -389,6 +389,64 @@ __device__ __forceinline__ uint32_t rewrite_slot(const TokT (&e)[W], TokT* __res
     return j;
 }
 
+// Several members' rewrites of one slot word in registers, then one compacting store (batched
+// trips).  rewrite_slot per member needed the word re-read from memory between members: a
+// dependent load per extra member on the thread's chain.  Here member j's matches replace
+// e[q] by new_j and leave a hole at q + 1 (a bit of `hole`, its value the sentinel), so every
+// index stays a compile-time constant.  A hole only ever follows a new token, which is no
+// member's a or b, so no match spans a hole and no hole starts a match; the left neighbour of a
+// match is e[q - 1], or e[q - 2] behind a hole; the right one is e[q + 2] (e[q + 1] is b, an
+// old token, so q + 2 is never a hole).  Matches of one member cannot overlap (a != b for
+// k > 1), and the ascending pass sees the already-rewritten left and the original right, as
+// rewrite_word (the reference's loop, train.py:196-224) does.  Returns the new length.
+template <class TokT, int W, class PA, class SinkOf>
+__device__ __forceinline__ uint32_t rewrite_slot_members(TokT (&e)[W], TokT* __restrict__ s, unsigned hits,
+                                                         PA ta, PA tb, PA tn,
+                                                         unsigned long long c, const SinkOf& sink_of) {
+    static_assert(W <= 64, "one hole bit per position");
+    const TokT sent = sentinel<TokT>();
+    const uint32_t len0 = (uint32_t)e[0];
+    unsigned long long hole = 0, chg = 0;
+    while (hits) {
+        const int j = __builtin_ctz(hits);
+        hits &= hits - 1;
+        const TokT a = (TokT)ta[j], b = (TokT)tb[j], nw = (TokT)tn[j];
+        const auto D = sink_of(j);
+#pragma unroll
+        for (int q = 1; q + 1 < W; ++q) {
+            if (e[q] == a && e[q + 1] == b) {
+                if (q > 1) {
+                    // e[q - 1], or e[q - 2] behind a hole (arithmetic, not a select of two array
+                    // loads, which would keep e[] out of registers)
+                    unsigned left = (unsigned)e[q - 1];
+                    if (q > 2) {
+                        const unsigned h = 0u - (unsigned)((hole >> (q - 1)) & 1);
+                        left ^= (left ^ (unsigned)e[q > 2 ? q - 2 : 1]) & h;
+                    }
+                    D.add(2u * left, c);                                          // (x,a)-=c, (x,new)+=c
+                }
+                if (q + 2 < W && e[q + 2 < W ? q + 2 : q] != sent)
+                    D.add(2u * (unsigned)e[q + 2 < W ? q + 2 : q] + 1, c);        // (b,y)-=c, (new,y)+=c
+                e[q] = nw;
+                e[q + 1] = sent;
+                hole |= 1ull << (q + 1);
+                chg |= 1ull << q;
+            }
+        }
+    }
+    uint32_t j = 0;   // output tokens so far
+#pragma unroll
+    for (int q = 1; q < W; ++q) {   // (no early exit: a data-dependent one un-unrolls the loop)
+        if ((uint32_t)q <= len0 && !((hole >> q) & 1)) {
+            if (j != (uint32_t)(q - 1) || ((chg >> q) & 1)) st_merge(&s[1 + j], e[q]);
+            ++j;
+        }
+    }
+    for (uint32_t p = j; p < len0; ++p) st_merge(&s[1 + p], sent);
+    st_merge(&s[0], (TokT)j);
+    return j;
+}
+
 // scan one slot class: U words in flight per thread, one 16-byte load per 16 bytes of slot
 template <class TokT, int C, class Sink>
 __device__ __forceinline__ void scan_class(const SlotCls<TokT>& S, unsigned bi, TokT a, TokT b,
@@ -934,6 +992,17 @@ constexpr bool kShareTok = BPE355_SHARE_TOK != 0;
 #define BPE355_TIE_BY_MEMBER 1
 #endif
 constexpr bool kTieByMember = BPE355_TIE_BY_MEMBER != 0;
+// A word several members hit: all of them rewritten in registers, one store pass (1), or one
+// member at a time through memory, the word re-read between members (0, rounds 1-4)
+#ifndef BPE355_REG_REWRITE
+#define BPE355_REG_REWRITE 1
+#endif
+constexpr bool kRegRewrite = BPE355_REG_REWRITE != 0;
+// the widest slot class rewritten in registers (the 64-id class needs ~60 more VGPRs)
+#ifndef BPE355_REG_REWRITE_MAXW
+#define BPE355_REG_REWRITE_MAXW 32
+#endif
+constexpr int kRegRewriteMaxW = BPE355_REG_REWRITE_MAXW;
 
 struct BatchMember {
     unsigned a, b, nw, slot;
@@ -1627,6 +1696,14 @@ __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigne
     // another thread's claim was loaded after that claim, so its copy here, torn or not, ends in a
     // failed claim or in no hit: only the claimant ever writes it.
     if (!hits || (tags && atomicMax(&tags[f], B.batch_id) >= B.batch_id)) return;
+    if (kRegRewrite && W <= kRegRewriteMaxW) {   // every member in registers, one compacting store
+        const auto sink_of = [&](int j) {
+            return DeltaSinkN<kLdsB>{LRt + (size_t)j * lr_member, (LdsU64*)(lds + 2 * kLdsB * j)};
+        };
+        const uint32_t nl = rewrite_slot_members(e, s, hits, sm_a, sm_b, sm_n, c, sink_of);
+        singles += nl < 2;
+        return;
+    }
     bool first = true;
     while (hits) {
         const int j = __builtin_ctz(hits);
@@ -1819,7 +1896,10 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
 
 // the rewrite of the batch k_select decided (BPE355_FOLD=0)
 template <class TokT>
-__global__ void __launch_bounds__(256) k_merge_batch(RoundState* __restrict__ st, const Batch* __restrict__ bt,
+#ifndef BPE355_MERGE_WAVES
+#define BPE355_MERGE_WAVES 4
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPE355_MERGE_WAVES))) k_merge_batch(RoundState* __restrict__ st, const Batch* __restrict__ bt,
                                                      PairsDev P, ToksDev K, WordsDev<TokT> W, IndexDev X,
                                                      unsigned long long* __restrict__ LRbase, size_t lr_member,
                                                      size_t lr_parity, uint32_t* __restrict__ tags) {
