@@ -26,6 +26,10 @@ for step in "$@"; do
   trainpar)   # the training parity tests (goldens, tie-heavy, scale)
     timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_train.py tests/test_gpu_scale.py > $OUT/pytest_trainpar.log 2>&1 || { echo "train parity tests failed"; tail -40 $OUT/pytest_trainpar.log; exit 1; }
     tail -1 $OUT/pytest_trainpar.log ;;
+  trainpar:*)   # the training parity tests on build/variants/NAME
+    V=${step#trainpar:}
+    BPE355_LIB=build/variants/$V/libbpe355.so timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_train.py tests/test_gpu_scale.py > $OUT/pytest_trainpar_$V.log 2>&1 || { echo "train parity tests ($V) failed"; tail -40 $OUT/pytest_trainpar_$V.log; exit 1; }
+    echo "$V: $(tail -1 $OUT/pytest_trainpar_$V.log)" ;;
   scale)
     timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_scale.py > $OUT/pytest_scale.log 2>&1 || { echo "scale tests failed"; tail -40 $OUT/pytest_scale.log; exit 1; }
     tail -1 $OUT/pytest_scale.log ;;
