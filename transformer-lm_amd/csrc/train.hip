@@ -1443,12 +1443,21 @@ __device__ __forceinline__ void select_core(const RoundState* __restrict__ st, B
     // The kClashI x kClashI (i, j) pairs are spread over the wave: lane L checks i = L % kClashI
     // against j = L / kClashI + t * kClashJ, then the kClashJ lanes of each i combine (one pass of
     // lane shuffles instead of a serial readlane chain over j)
+    // each candidate's posting list (the shorter of a's and b's) and whether the merge uses it
+    const unsigned lu = m.za <= m.zb ? m.za : m.zb, bu = m.za <= m.zb ? m.ba : m.bb;
+    const bool use = lu != kNoAnc && lu <= X.full_threshold;
+    const unsigned long long lkey = use && lu > 0 ? (unsigned long long)bu << 32 | lu : 0ull;
     bool clash = false;
+    // beside the clash check, for the members' token groups (kShareTok): the candidates with i's
+    // a (sa) and with i's b (sb), and whether an earlier candidate walks i's posting list (dl)
+    unsigned sa = 0, sb = 0;
+    bool dl = false;
     {
         const int ci = lane % kClashI, cj0 = lane / kClashI;
         const unsigned ai = __shfl((int)e.a, ci), bi = __shfl((int)e.b, ci);
         const unsigned long long hi = __shfl(h, ci);
         const unsigned li_ = __shfl((int)lk, ci), lai = __shfl((int)m.la, ci);
+        const unsigned long long lki = kShareTok ? __shfl(lkey, ci) : 0ull;
         const bool iv = ci < nf;
 #pragma unroll
         for (int t = 0; t < kClashI / kClashJ; ++t) {
@@ -1456,6 +1465,12 @@ __device__ __forceinline__ void select_core(const RoundState* __restrict__ st, B
             const unsigned aj = __shfl((int)e.a, j), bj = __shfl((int)e.b, j);
             const unsigned long long hj = __shfl(h, j);
             const unsigned lj = __shfl((int)lk, j), laj = __shfl((int)m.la, j);
+            if (kShareTok) {
+                const unsigned long long lkj = __shfl(lkey, j);
+                sa |= (unsigned)(aj == ai) << j;
+                sb |= (unsigned)(bj == bi) << j;
+                dl |= j < ci && lki != 0 && lkj == lki;
+            }
             if (j < ci && iv) {
                 const bool tc = aj == bi || bj == ai || (!kShareTok && (aj == ai || bj == bi));
                 clash |= tc;
@@ -1467,7 +1482,14 @@ __device__ __forceinline__ void select_core(const RoundState* __restrict__ st, B
                 }
             }
         }
-        for (int o = kClashI; o < 64; o <<= 1) clash |= __shfl_xor((int)clash, o) != 0;
+        for (int o = kClashI; o < 64; o <<= 1) {
+            clash |= __shfl_xor((int)clash, o) != 0;
+            if (kShareTok) {
+                sa |= (unsigned)__shfl_xor((int)sa, o);
+                sb |= (unsigned)__shfl_xor((int)sb, o);
+                dl |= __shfl_xor((int)dl, o) != 0;
+            }
+        }
         if (i >= kClashI) clash = false;   // lanes < kClashI hold their own i's result
     }
     // k: the first candidate that fails (count >= T, (2) a != b, fresh, no clash), within the
@@ -1535,29 +1557,20 @@ __device__ __forceinline__ void select_core(const RoundState* __restrict__ st, B
     k = min(k, n_rounds - round);
     // per member: pool offset, new id, posting-list prefix (exclusive scans over lanes < k)
     const bool mem = i < k;
-    const unsigned lu = m.za <= m.zb ? m.za : m.zb, bu = m.za <= m.zb ? m.ba : m.bb;
-    const bool use = lu != kNoAnc && lu <= X.full_threshold;
-    // the members' token groups (equal a's, equal b's: the group's first member carries its mask)
-    // and posting lists two members share (the later one walks none of it: the word is claimed
-    // once and every member's hits are found on it)
-    unsigned ga = 0, gb = 0;
+    // the members' token groups (equal a's, equal b's: the group's first member carries the
+    // group's mask) and posting lists two members share (the later one walks none of it: the
+    // word is claimed once and every member's hits are found on it)
+    unsigned ga, gb;
     bool dup_list = false;
     if (kShareTok) {
-#pragma unroll
-        for (int j = 0; j < kMaxBatch; ++j) {
-            const unsigned aj = __builtin_amdgcn_readlane((int)e.a, j), bj = __builtin_amdgcn_readlane((int)e.b, j);
-            const unsigned uj = __builtin_amdgcn_readlane((int)bu, j), lj = __builtin_amdgcn_readlane((int)lu, j);
-            const bool usej = __builtin_amdgcn_readlane((int)use, j) != 0;
-            const bool in = j < k;   // (uniform)
-            ga |= (unsigned)(in && aj == e.a) << j;
-            gb |= (unsigned)(in && bj == e.b) << j;
-            dup_list |= in && j < i && usej && uj == bu && lj == lu;
-        }
-        const unsigned below = (1u << (i & 31)) - 1;   // (lanes i >= k are not members)
+        const unsigned km = (unsigned)((1ull << k) - 1), below = (1u << (i & 31)) - 1;
+        ga = sa & km;
+        gb = sb & km;
         if (ga & below) ga = 0;
         if (gb & below) gb = 0;
+        dup_list = dl;   // (an earlier candidate with the list is a member when i is)
     } else {
-        ga = gb = 1u << i;
+        ga = gb = 1u << (i & 31);
     }
     const unsigned add_pool = mem && fr ? lk : 0u, add_fresh = mem && fr ? 1u : 0u,
                    add_list = mem && use && !dup_list ? lu : 0u;
