@@ -73,7 +73,7 @@ for step in "$@"; do
     for rep in 1 2; do for lib in $VS; do
       if [ $lib = default ]; then LIBENV=""; else LIBENV="BPE355_LIB=build/variants/$lib/libbpe355.so"; fi
       env $LIBENV timeout -k 10 300 python -u bench.py --no-file --no-encode --no-cpu-baseline --steps 3 --warmup 1 > $OUT/abm_${lib}_$rep.log 2>&1 || { echo "abmulti failed"; tail -20 $OUT/abm_${lib}_$rep.log; exit 1; }
-      python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().split(chr(10))[-1]); m=d['merge_loop']; print('$lib rep $rep merge_ms', m['ms'], 'us_per_trip', m['us_per_trip'], 'k_us', m['k_merge_batch_us'], 'trips', m['trips'], 'parity', d['parity']['parity'])" $OUT/abm_${lib}_$rep.log
+      python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().split(chr(10))[-1]); m=d['merge_loop']; dr=d.get('device_resident') or {}; print('$lib rep $rep merge_ms', m['ms'], 'us_per_trip', m['us_per_trip'], 'k_us', m['k_merge_batch_us'], 'trips', m['trips'], 'count_ms', dr.get('phases_ms',{}).get('t_count_ms'), 'agg_ms', (dr.get('count_aggregation') or {}).get('ms'), 'k_count2_us', (d.get('roofline_count') or {}).get('avg_launch_us'), 'parity', d['parity']['parity'])" $OUT/abm_${lib}_$rep.log
     done; done ;;
   trace:*)   # the select's statistics (a BPE355_STATS_CODE build): k histogram, why batches end
     V=${step#trace:}
