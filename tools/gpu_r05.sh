@@ -85,6 +85,10 @@ for step in "$@"; do
       env $V=$f BPE355_PROBE=1 BPE355_LIB=build/variants/probe/libbpe355.so timeout -k 10 200 python -u bench.py --no-file --steps 1 --warmup 0 --no-encode --no-cpu-baseline --no-timing > $OUT/probe_${V}_$f.log 2> $OUT/probe_err_${V}_$f.log || { echo "probe failed"; tail -5 $OUT/probe_err_${V}_$f.log; exit 1; }
       grep probe $OUT/probe_err_${V}_$f.log | head -12
     done ;;
+  probev:*)   # the merge-loop probe of build/variants/NAME (a BPE355_PROBE_CODE build)
+    V=${step#probev:}
+    BPE355_PROBE=1 BPE355_LIB=build/variants/$V/libbpe355.so timeout -k 10 200 python -u bench.py --no-file --steps 1 --warmup 0 --no-encode --no-cpu-baseline --no-timing > $OUT/probe_$V.log 2> $OUT/probe_err_$V.log || { echo "probe failed"; tail -5 $OUT/probe_err_$V.log; exit 1; }
+    grep probe $OUT/probe_err_$V.log > $OUT/merge_probe_$V.txt; head -12 $OUT/merge_probe_$V.txt ;;
   probe)   # the merge-loop probe (build/variants/probe), fused and unfused
     for f in 1 0; do
       BPE355_FOLD=$f BPE355_PROBE=1 BPE355_LIB=build/variants/probe/libbpe355.so timeout -k 10 200 python -u bench.py --no-file --steps 1 --warmup 0 --no-encode --no-cpu-baseline --no-timing > $OUT/probe_$f.log 2> $OUT/probe_err_$f.log || { echo "probe failed"; tail -5 $OUT/probe_err_$f.log; exit 1; }

@@ -1003,6 +1003,19 @@ constexpr bool kRegRewrite = BPE355_REG_REWRITE != 0;
 #define BPE355_REG_REWRITE_MAXW 32
 #endif
 constexpr int kRegRewriteMaxW = BPE355_REG_REWRITE_MAXW;
+// Which members a word holds: with at least this many members, each adjacent pair of the word is
+// looked up in an LDS table of the batch's pairs (hashed, 4096 one-byte slots: member + 1, 0xFF
+// when two members share a slot) instead of compared with every member -- k x (W - 2) compares
+// made the full scans of the first trips VALU-bound.  0: always compare with every member.
+#ifndef BPE355_PAIR_FILTER_K
+#define BPE355_PAIR_FILTER_K 4
+#endif
+constexpr int kPairFilterK = BPE355_PAIR_FILTER_K;
+constexpr unsigned kPairSlots = 4096;
+__device__ __forceinline__ unsigned pair_h12(unsigned x, unsigned y) {
+    return ((x * 0x9E3779B1u) ^ (y * 0x85EBCA77u)) >> 20;
+}
+typedef __attribute__((address_space(3))) uint8_t LdsU8;
 
 struct BatchMember {
     unsigned a, b, nw, slot;
@@ -1684,8 +1697,8 @@ template <class TokT, int C>
 __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigned i, const Batch& B,
                                                  unsigned long long* LRt, size_t lr_member,
                                                  unsigned long long* lds, const LdsU32* sm_a,
-                                                 const LdsU32* sm_b, const LdsU32* sm_n, unsigned& singles,
-                                                 uint32_t* tags = nullptr, unsigned f = 0) {
+                                                 const LdsU32* sm_b, const LdsU32* sm_n, const LdsU8* pm, bool use_pm,
+                                                 unsigned& singles, uint32_t* tags = nullptr, unsigned f = 0) {
     constexpr int W = slot_w(C);
     constexpr int V = W * (int)sizeof(TokT) / 16;
     TokT* s = S.slot + (size_t)i * W;
@@ -1698,12 +1711,39 @@ __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigne
     // the members this word holds: no member's b is another's a and the new tokens are fresh, so
     // a rewrite neither makes nor breaks another member's pair and the original word decides
     unsigned hits = 0;
-    for (int j = 0; j < B.k; ++j) {
-        const TokT ta = (TokT)sm_a[j], tb = (TokT)sm_b[j];
-        bool hit = false;
+    if (use_pm && W <= 32) {   // each pair of the word looked up in the batch's pair table, eight
+        // lookups in flight at a time (the 64-id class, rare, compares with every member)
+        const uint32_t len = (uint32_t)e[0];
 #pragma unroll
-        for (int q = 1; q + 1 < W; ++q) hit |= (e[q] == ta) & (e[q + 1] == tb);
-        hits |= (unsigned)hit << j;
+        for (int q0 = 1; q0 + 1 < W; q0 += 8) {
+            unsigned v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int q = q0 + u;
+                v[u] = q + 1 < W ? (unsigned)pm[pair_h12((unsigned)e[q + 1 < W ? q : 1], (unsigned)e[q + 1 < W ? q + 1 : 1])] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int q = q0 + u;
+                if (q + 1 < W && (uint32_t)q < len && v[u]) {
+                    const unsigned x = (unsigned)e[q + 1 < W ? q : 1], y = (unsigned)e[q + 1 < W ? q + 1 : 1];
+                    if (v[u] != 0xFFu) {
+                        const unsigned j = v[u] - 1;
+                        hits |= (unsigned)((x == sm_a[j]) & (y == sm_b[j])) << j;
+                    } else {   // two members share the slot
+                        for (int j = 0; j < B.k; ++j) hits |= (unsigned)((x == sm_a[j]) & (y == sm_b[j])) << j;
+                    }
+                }
+            }
+        }
+    } else {
+        for (int j = 0; j < B.k; ++j) {
+            const TokT ta = (TokT)sm_a[j], tb = (TokT)sm_b[j];
+            bool hit = false;
+#pragma unroll
+            for (int q = 1; q + 1 < W; ++q) hit |= (e[q] == ta) & (e[q + 1] == tb);
+            hits |= (unsigned)hit << j;
+        }
     }
     // claimed only on a hit (most list entries miss: no atomic for them).  A word rewritten under
     // another thread's claim was loaded after that claim, so its copy here, torn or not, ends in a
@@ -1742,6 +1782,7 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
                                            unsigned long long* l_lr) {
     __shared__ unsigned s_ma[kMaxBatch], s_mb[kMaxBatch], s_mn[kMaxBatch];   // the members' tokens
     __shared__ unsigned s_pre[kMaxBatch + 1], s_lbeg[kMaxBatch];   // list prefix sums, list starts
+    __shared__ unsigned s_pm[kPairSlots / 4];   // the batch's pair table (bytes; kPairFilterK)
     const int tid = threadIdx.x;
     // every field the prologue needs in one round trip (none depends on another)
     const int stop = B.stop, k = B.k, b_trip = B.trip, b_ntok = B.ntok, b_prev_k = B.prev_k;
@@ -1808,8 +1849,26 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
     if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 5);
     for (unsigned q = tid; q < 2 * kLdsB * (unsigned)k; q += blockDim.x) l_lr[q] = 0;
     unsigned long long* LRt = LRbase + (size_t)(B.trip & 1) * lr_parity;   // member j at + j * lr_member
+    const bool use_pm = kPairFilterK > 0 && k >= kPairFilterK;   // (uniform)
+    if (use_pm)
+        for (unsigned q = tid; q < kPairSlots / 4; q += blockDim.x) s_pm[q] = 0;
 
     __syncthreads();   // l_lr cleared
+    if (use_pm) {   // member j's pair -> slot: j + 1, or 0xFF where two members share a slot
+        if (tid < 64) {
+            const bool m = tid < k;
+            const unsigned h = pair_h12(ma, mb);
+            bool coll = false;
+#pragma unroll
+            for (int j = 0; j < kMaxBatch; ++j) {
+                const int hj = __shfl((int)h, j);   // (every lane active: lane j supplies its slot)
+                coll |= j < k && j != tid && hj == (int)h;
+            }
+            if (m) reinterpret_cast<uint8_t*>(s_pm)[h] = coll ? (uint8_t)0xFFu : (uint8_t)(tid + 1);
+        }
+        __syncthreads();
+    }
+    const LdsU8* pmp = (const LdsU8*)s_pm;
     if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 6);
 
     unsigned singles = 0;
@@ -1850,10 +1909,10 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
         if (B.full_scan) {
             const unsigned total = W.off[kNumCls];
             for (unsigned f = bid * blockDim.x + tid; f < total; f += nb * blockDim.x) {
-                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f,  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles);
-                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles);
-                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles);
-                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles);
+                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f,  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles);
+                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles);
+                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles);
+                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles);
             }
         } else {
             const unsigned total = B.list_pre[k];
@@ -1865,10 +1924,10 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
                     if (j + step < k && i >= s_pre[j + step]) j += step;
                 const unsigned f = X.list[s_lbeg[j] + (i - s_pre[j])];
                 // a word on several members' lists is rewritten by the first thread to claim it
-                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f,  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles, tags, f);
-                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles, tags, f);
-                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles, tags, f);
-                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, singles, tags, f);
+                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f,  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, tags, f);
+                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, tags, f);
+                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, tags, f);
+                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, tags, f);
             }
         }
     }
@@ -1912,7 +1971,7 @@ template <class TokT>
 #ifndef BPE355_MERGE_WAVES
 #define BPE355_MERGE_WAVES 4
 #endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPE355_MERGE_WAVES))) k_merge_batch(RoundState* __restrict__ st, const Batch* __restrict__ bt,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof(TokT) == 2 ? BPE355_MERGE_WAVES : 2))) k_merge_batch(RoundState* __restrict__ st, const Batch* __restrict__ bt,
                                                      PairsDev P, ToksDev K, WordsDev<TokT> W, IndexDev X,
                                                      unsigned long long* __restrict__ LRbase, size_t lr_member,
                                                      size_t lr_parity, uint32_t* __restrict__ tags) {
