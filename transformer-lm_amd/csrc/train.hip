@@ -975,6 +975,9 @@ constexpr int kTopM = kMaxBatch + 1;
 // the select's clash check: candidates i < kClashI (a power of two >= kMaxBatch), kClashJ lanes each
 constexpr int kClashI = kMaxBatch <= 16 ? 16 : 32;
 constexpr int kClashJ = 64 / kClashI;
+#ifndef BPE355_LDS_CELLS
+#define BPE355_LDS_CELLS 1
+#endif
 #ifndef BPE355_LDS_B
 #define BPE355_LDS_B 128
 #endif
@@ -1088,12 +1091,18 @@ struct TokMetaS {
     unsigned la, lb, za, zb, ba, bb;     // lengths; posting lists of a and b (len, begin)
 };
 
+// A member's cells: ids below N summed in LDS per workgroup (32-bit: a cell never exceeds the
+// member's own count, count(P_j) <= count(P_1), so `narrow` = count(P_1) < 2^32 holds for the
+// whole batch; otherwise every add goes to the global cells), the rest by global atomics.
+typedef __attribute__((address_space(3))) unsigned LdsU32;   // an LDS word (explicit address space)
 template <unsigned N>
 struct DeltaSinkN {
     unsigned long long* LR;     // this member's global cells
-    LdsU64* lds;                // this member's LDS cells (ids below N)
+    LdsU32* lds;                // this member's LDS cells (ids below N)
+    bool narrow;
     __device__ __forceinline__ void add(unsigned cell, unsigned long long c) const {
-        if (cell < 2 * N) __hip_atomic_fetch_add(&lds[cell], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (narrow && cell < 2 * N)
+            __hip_atomic_fetch_add(&lds[cell], (unsigned)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         else atomicAdd(&LR[cell], c);
     }
 };
@@ -1473,8 +1482,8 @@ __device__ __forceinline__ void select_core(const RoundState* __restrict__ st, B
         const unsigned long long lki = kShareTok ? __shfl(lkey, ci) : 0ull;
         const bool iv = ci < nf;
 #pragma unroll
-        for (int t = 0; t < kClashI / kClashJ; ++t) {
-            const int j = cj0 + t * kClashJ;
+        for (int t = 0; t < (kTopM + kClashJ - 1) / kClashJ && t < kClashI / kClashJ; ++t) {
+            const int j = cj0 + t * kClashJ;   // (candidates past kTopM - 1 are never ranked)
             const unsigned aj = __shfl((int)e.a, j), bj = __shfl((int)e.b, j);
             const unsigned long long hj = __shfl(h, j);
             const unsigned lj = __shfl((int)lk, j), laj = __shfl((int)m.la, j);
@@ -1688,7 +1697,6 @@ __global__ void __launch_bounds__(256) k_snapshot(const uint32_t* __restrict__ s
     for (unsigned i = threadIdx.x; i < n_ti; i += blockDim.x) h_ti[i] = ti[i];
 }
 
-typedef __attribute__((address_space(3))) unsigned LdsU32;   // an LDS word (explicit address space)
 
 // the slot word of class C addressed directly, every member applied in order.  claim: the word
 // (global slot index f) may be on several members' lists; the first thread to claim it rewrites
@@ -1696,7 +1704,7 @@ typedef __attribute__((address_space(3))) unsigned LdsU32;   // an LDS word (exp
 template <class TokT, int C>
 __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigned i, const Batch& B,
                                                  unsigned long long* LRt, size_t lr_member,
-                                                 unsigned long long* lds, const LdsU32* sm_a,
+                                                 unsigned* lds, bool narrow, const LdsU32* sm_a,
                                                  const LdsU32* sm_b, const LdsU32* sm_n, const LdsU8* pm, bool use_pm,
                                                  unsigned& singles, uint32_t* tags = nullptr, unsigned f = 0) {
     constexpr int W = slot_w(C);
@@ -1751,7 +1759,7 @@ __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigne
     if (!hits || (tags && atomicMax(&tags[f], B.batch_id) >= B.batch_id)) return;
     if (kRegRewrite && W <= kRegRewriteMaxW) {   // every member in registers, one compacting store
         const auto sink_of = [&](int j) {
-            return DeltaSinkN<kLdsB>{LRt + (size_t)j * lr_member, (LdsU64*)(lds + 2 * kLdsB * j)};
+            return DeltaSinkN<kLdsB>{LRt + (size_t)j * lr_member, (LdsU32*)(lds + 2 * kLdsB * j), narrow};
         };
         const uint32_t nl = rewrite_slot_members(e, s, hits, sm_a, sm_b, sm_n, c, sink_of);
         singles += nl < 2;
@@ -1767,7 +1775,7 @@ __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigne
             __builtin_memcpy(e, r, sizeof(e));
         }
         first = false;
-        const DeltaSinkN<kLdsB> D{LRt + (size_t)j * lr_member, (LdsU64*)(lds + 2 * kLdsB * j)};
+        const DeltaSinkN<kLdsB> D{LRt + (size_t)j * lr_member, (LdsU32*)(lds + 2 * kLdsB * j), narrow};
         const uint32_t nl = rewrite_slot(e, s, (TokT)sm_a[j], (TokT)sm_b[j], (TokT)sm_n[j], c, D);
         if (nl < 2) { ++singles; break; }
     }
@@ -1779,7 +1787,7 @@ template <class TokT>
 __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Batch& B, PairsDev P, ToksDev K,
                                            WordsDev<TokT> W, IndexDev X, unsigned long long* __restrict__ LRbase,
                                            size_t lr_member, size_t lr_parity, uint32_t* __restrict__ tags,
-                                           unsigned long long* l_lr) {
+                                           unsigned* l_lr) {
     __shared__ unsigned s_ma[kMaxBatch], s_mb[kMaxBatch], s_mn[kMaxBatch];   // the members' tokens
     __shared__ unsigned s_pre[kMaxBatch + 1], s_lbeg[kMaxBatch];   // list prefix sums, list starts
     __shared__ unsigned s_pm[kPairSlots / 4];   // the batch's pair table (bytes; kPairFilterK)
@@ -1787,6 +1795,9 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
     // every field the prologue needs in one round trip (none depends on another)
     const int stop = B.stop, k = B.k, b_trip = B.trip, b_ntok = B.ntok, b_prev_k = B.prev_k;
     const unsigned idle_from = B.idle_from;
+    // 32-bit LDS cells hold every member's sums (test knob BPE355_LDS_CELLS=0: every cell global,
+    // the path of a batch whose P1 count reaches 2^32)
+    const bool narrow = BPE355_LDS_CELLS && B.m[0].cnt < (1ll << 32);
     unsigned ma = 0, mb = 0, mn = 0, mlb = 0, mpre = 0;
     if (tid < kMaxBatch) { ma = B.m[tid].a; mb = B.m[tid].b; mn = B.m[tid].nw; mlb = B.m[tid].list_beg; }
     if (tid <= kMaxBatch) mpre = B.list_pre[tid];
@@ -1880,7 +1891,7 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
         // one member: the per-round rewrite (index list or a scan of every slot)
         const BatchMember& M = B.m[0];
         const TokT ta = (TokT)M.a, tb = (TokT)M.b, tn = (TokT)M.nw;
-        const DeltaSinkN<kLdsB> D{LRt, (LdsU64*)l_lr};
+        const DeltaSinkN<kLdsB> D{LRt, (LdsU32*)l_lr, narrow};
         if (M.use_list && bid < nb) {
             const uint32_t* L = X.list + M.list_beg;
             for (unsigned i = bid * blockDim.x + tid; i < M.list_len; i += nb * blockDim.x) {
@@ -1909,10 +1920,10 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
         if (B.full_scan) {
             const unsigned total = W.off[kNumCls];
             for (unsigned f = bid * blockDim.x + tid; f < total; f += nb * blockDim.x) {
-                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f,  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles);
-                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles);
-                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles);
-                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles);
+                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f,  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles);
+                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1],  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles);
+                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2],  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles);
+                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3],  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles);
             }
         } else {
             const unsigned total = B.list_pre[k];
@@ -1924,10 +1935,10 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
                     if (j + step < k && i >= s_pre[j + step]) j += step;
                 const unsigned f = X.list[s_lbeg[j] + (i - s_pre[j])];
                 // a word on several members' lists is rewritten by the first thread to claim it
-                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f,  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, tags, f);
-                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, tags, f);
-                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, tags, f);
-                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3],  B, LRt, lr_member, l_lr, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, tags, f);
+                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f,  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, tags, f);
+                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1],  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, tags, f);
+                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2],  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, tags, f);
+                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3],  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, tags, f);
             }
         }
     }
@@ -1941,7 +1952,7 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
                 bool hit = false;
                 for (uint32_t q = 0; q + 1 < len && !hit; ++q) hit = (t[q] == ta) & (t[q + 1] == tb);
                 if (!hit) continue;
-                const DeltaSinkN<kLdsB> D{LRt + (size_t)j * lr_member, (LdsU64*)(l_lr + 2 * kLdsB * j)};
+                const DeltaSinkN<kLdsB> D{LRt + (size_t)j * lr_member, (LdsU32*)(l_lr + 2 * kLdsB * j), narrow};
                 len = rewrite_word(t, len, ta, tb, (TokT)B.m[j].nw, W.lcnt[i], D, false);
                 W.llen[i] = len;
                 singles += (len < 2);
@@ -1954,8 +1965,8 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
     __syncthreads();
     if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 7);
     for (unsigned q = tid; q < 2 * kLdsB * (unsigned)k; q += blockDim.x) {
-        const unsigned long long v = l_lr[q];
-        if (v) atomicAdd(&LRt[(size_t)(q / (2 * kLdsB)) * lr_member + q % (2 * kLdsB)], v);
+        const unsigned v = l_lr[q];
+        if (v) atomicAdd(&LRt[(size_t)(q / (2 * kLdsB)) * lr_member + q % (2 * kLdsB)], (unsigned long long)v);
     }
     if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 8);
     clear_prev();
@@ -1975,7 +1986,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof
                                                      PairsDev P, ToksDev K, WordsDev<TokT> W, IndexDev X,
                                                      unsigned long long* __restrict__ LRbase, size_t lr_member,
                                                      size_t lr_parity, uint32_t* __restrict__ tags) {
-    __shared__ unsigned long long l_lr[2 * kLdsB * kMaxBatch];
+    __shared__ unsigned l_lr[2 * kLdsB * kMaxBatch];
     merge_body<TokT>(st, *bt, P, K, W, X, LRbase, lr_member, lr_parity, tags, l_lr);
 }
 
@@ -1997,7 +2008,7 @@ __global__ void __launch_bounds__(kTripThreads) k_trip(RoundState* __restrict__ 
                                               size_t lr_parity, uint32_t* __restrict__ tags) {
     __shared__ union TripLds {
         SelLds sel;
-        unsigned long long lr[2 * kLdsB * kMaxBatch];
+        unsigned lr[2 * kLdsB * kMaxBatch];
     } u;
     __shared__ Batch s_b;
     const bool pub = blockIdx.x == 0;
