@@ -146,7 +146,10 @@ def cpu_baselines(args, path, vocab, merges, L):
                    f"oracle/cpu_ref.py (pure-Python port with the reference's structure) on 1 core "
                    f"(host shows {cores}); count {big['t_count_s']:.1f}s + build {big['t_build_s']:.1f}s "
                    f"measured, {big['rounds_done']}/{big['rounds_total']} merge rounds measured in "
-                   f"{args.cpu_cap_s:.0f}s, the rest extrapolated at {big['ms_per_round']:.1f} ms/round"),
+                   f"{args.cpu_cap_s:.0f}s ({big['ms_per_round']:.1f} ms/round), the rest extrapolated along the "
+                   f"port's measured cost curve (x{big.get('growth_factor') or 1:.2f} on the flat rate; "
+                   f"oracle/cpu_port_growth.json, a complete 16 MB run)"),
+        "value_flat": big.get("MBps_flat"),
         "rounds_measured_frac": big["rounds_measured_frac"], "merges_per_s": big["merges_per_s"],
         "samples": r["train"],
         "c1": dict(r["c1"], note="tests/fixtures corpus.en at vocab 500 (reference test_train_bpe.py:28), "

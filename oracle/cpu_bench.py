@@ -10,8 +10,12 @@ Legs, all on this host's cores:
             models/tokenizer/train.py, the reference's structure), one core.
   train     the first 16 MB and 64 MB of the bench corpus at the bench vocab, the same port, one
             core each (two processes): pre-tokenize + count measured in full, the merge rounds
-            measured until a wall cap, the rest extrapolated at the measured mean per round
-            (rounds_measured_frac says how much was measured).
+            measured until a wall cap, the rest extrapolated (rounds_measured_frac says how much
+            was measured).  The extrapolation follows the port's measured cost curve
+            (cpu_port_growth.json: a complete 16 MB run, whose merges equal the C oracle's): a round
+            costs ~10 x more at the end than over the first rounds (the argmax scans every live
+            pair), so the flat mean of the first rounds under-estimated the complete run by 86.5 %
+            (VERDICT r04 item 7).  MBps is the corrected rate; MBps_flat the old flat one.
   encode    Tokenizer.encode port (cpu_ref.Encoder, tokenizer.py:92-138) of the first 64 MB with
             the GPU-trained merges, in 1 M-character pieces each encoded on its own -- the
             reference's dataset encoder (encode.py:31-36) -- over a pool of processes (cores
@@ -45,6 +49,27 @@ EOT = "<|endoftext|>"
 BLOCK = 4096
 
 
+def growth_factor(rounds_done: int, rounds_total: int):
+    """(mean ms per round over the whole run) / (mean over the first rounds_done rounds), from the
+    complete run's cumulative cost curve (cpu_port_growth.json), or None without it"""
+    f = HERE / "cpu_port_growth.json"
+    if not f.exists() or rounds_done <= 0:
+        return None
+    g = json.loads(f.read_text())
+    pts = g["points"]
+    r = min(rounds_done, pts[-1][0])
+    if r <= pts[0][0]:   # before the first point: its mean
+        t = pts[0][1] * r / pts[0][0]
+    else:
+        t = pts[-1][1]
+        for (r0, t0), (r1, t1) in zip(pts, pts[1:]):
+            if r0 <= r <= r1:
+                t = t0 + (t1 - t0) * (r - r0) / max(1, r1 - r0)
+                break
+    whole = pts[-1][1] / pts[-1][0]
+    return whole / (t / r) if t > 0 else None
+
+
 def _train_leg(args):
     """one pure-Python training on `m` bytes of a file (m = None: the whole file)"""
     path, m, vocab, cap_s = args
@@ -58,14 +83,19 @@ def _train_leg(args):
     nb = len(text.encode("utf-8"))
     # the rounds' mean excludes the one-time build of the words, pair counts and index
     per_round = (info["t_merge_s"] - info["t_build_s"]) / max(1, info["rounds_done"])
-    projected = info["t_count_s"] + info["t_build_s"] + per_round * info["rounds_total"]
+    flat = info["t_count_s"] + info["t_build_s"] + per_round * info["rounds_total"]
+    gf = None if info["complete"] else growth_factor(info["rounds_done"], info["rounds_total"])
+    projected = flat if gf is None else info["t_count_s"] + info["t_build_s"] + per_round * info["rounds_total"] * gf
     return {"bytes": nb, "vocab": vocab, "wall_s": round(wall, 3), "t_count_s": round(info["t_count_s"], 3),
             "t_build_s": round(info["t_build_s"], 3),
             "rounds_done": info["rounds_done"], "rounds_total": info["rounds_total"],
             "rounds_measured_frac": round(info["rounds_done"] / max(1, info["rounds_total"]), 4),
             "ms_per_round": round(per_round * 1e3, 3),
             "MBps": round(nb / projected / 1e6, 5) if projected > 0 else None,
-            "merges_per_s": round(1.0 / per_round, 2) if per_round > 0 else None,
+            "MBps_flat": round(nb / flat / 1e6, 5) if flat > 0 else None,
+            "growth_factor": round(gf, 3) if gf else None,
+            "merges_per_s": round(info["rounds_total"] / max(1e-9, projected - info["t_count_s"] - info["t_build_s"]), 2)
+                            if per_round > 0 else None,
             "complete": info["complete"],
             "merges_sha256": hashlib.sha256(b"".join(struct.pack("<I", len(a)) + a + struct.pack("<I", len(b)) + b
                                                      for a, b in merges)).hexdigest()}
