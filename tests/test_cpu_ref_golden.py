@@ -26,3 +26,21 @@ def test_cpu_ref_encode_matches_reference(name):
     vocab, merges = G.tokenizer_inputs(o)
     enc = cpu_ref.Encoder(vocab, merges, o["special_tokens"])
     assert enc.encode(G.encode_text(o)) == o["ids"]
+
+
+def test_cpu_baseline_growth_curve():
+    """the CPU baseline's extrapolation model (oracle/cpu_port_growth.json, from a complete run of
+    the port on the 16 MB bench sample): the whole run's mean round is dearer than the first
+    rounds' mean, and a complete run needs no correction"""
+    import json
+    import pathlib
+    from oracle import cpu_bench
+    g = json.loads((pathlib.Path(cpu_bench.__file__).parent / "cpu_port_growth.json").read_text())
+    pts = g["points"]
+    assert pts[-1][0] == g["rounds_total"] == 31743
+    assert all(b[0] > a[0] and b[1] >= a[1] for a, b in zip(pts, pts[1:]))   # cumulative
+    assert abs(cpu_bench.growth_factor(g["rounds_total"], g["rounds_total"]) - 1.0) < 1e-9
+    for r in (10, 199, 450, 1240, 5000):
+        assert cpu_bench.growth_factor(r, g["rounds_total"]) > 1.5
+    # the flat rate of the first rounds under-estimated the complete run by ~86 %
+    assert g["flat_projection_error"] < -0.5
