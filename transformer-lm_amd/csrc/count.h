@@ -43,8 +43,10 @@ constexpr int kCoarse = 1 << kCoarseBits;
 // stalls the host for hundreds of ms (the driver clears fresh VRAM).
 struct Arrays3 {
     DevBuf<uint64_t> a, b, c;
+    DevBuf<uint8_t> d;   // the level-1 destination's fine bins (allocated on first use as one)
     size_t cap = 0;
     int dev = -1;
+    size_t bytes() const { return 3 * cap * sizeof(uint64_t) + d.n; }
 };
 std::unique_ptr<Arrays3> scratch_take(size_t cap);   // exclusive until given back
 void scratch_give(std::unique_ptr<Arrays3> x);

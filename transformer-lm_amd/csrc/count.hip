@@ -500,13 +500,16 @@ __global__ void __launch_bounds__(64) k_rec_tiles(const unsigned long long* __re
 
 // records [s0, s0 + len) of (slo, shi, sme) to dest + cur[bin] (cur: LDS, advanced), bin = the 6
 // bits of the hash at `shift`, one LDS-sorted tile at a time
+// dfine (level 1): each record's next 6 hash bits, its level-2 bin, into a byte array beside the
+// destination, so the level-2 histogram reads one byte per record instead of 24
 __device__ __forceinline__ void part_tiles(const uint64_t* __restrict__ slo, const uint64_t* __restrict__ shi,
                                            const uint64_t* __restrict__ sme, size_t s0, size_t len, int shift,
                                            unsigned long long* cur, uint64_t* __restrict__ dlo,
                                            uint64_t* __restrict__ dhi, uint64_t* __restrict__ dme,
-                                           const unsigned* __restrict__ dpage = nullptr) {
+                                           const unsigned* __restrict__ dpage = nullptr,
+                                           uint8_t* __restrict__ dfine = nullptr) {
     __shared__ uint64_t st_lo[kPartTile], st_hi[kPartTile], st_me[kPartTile];
-    __shared__ uint8_t st_bin[kPartTile];
+    __shared__ uint8_t st_bin[kPartTile], st_fine[kPartTile];
     __shared__ unsigned t_cnt[kCoarse], t_off[kCoarse], t_cur[kCoarse];
     const int tid = threadIdx.x;
     constexpr int U = kPartTile / 1024;
@@ -515,15 +518,18 @@ __device__ __forceinline__ void part_tiles(const uint64_t* __restrict__ slo, con
     for (size_t t0 = 0; t0 < len; t0 += kPartTile) {
         const unsigned nt = (unsigned)(len - t0 < (size_t)kPartTile ? len - t0 : kPartTile);
         uint64_t a[U], b[U], m[U];
-        unsigned bin[U];
+        unsigned bin[U], fine[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const unsigned q = tid + u * 1024;
             bin[u] = kCoarse;
+            fine[u] = 0;
             if (q < nt) {
                 const size_t i = s0 + t0 + q;
                 a[u] = slo[i]; b[u] = shi[i]; m[u] = sme[i];
-                bin[u] = (unsigned)(rec_hash(a[u], b[u], m[u]) >> shift) & (kCoarse - 1);
+                const uint64_t h = rec_hash(a[u], b[u], m[u]);
+                bin[u] = (unsigned)(h >> shift) & (kCoarse - 1);
+                fine[u] = (unsigned)(h >> (shift - kCoarseBits)) & (kCoarse - 1);
                 atomicAdd(&t_cnt[bin[u]], 1u);
             }
         }
@@ -544,12 +550,14 @@ __device__ __forceinline__ void part_tiles(const uint64_t* __restrict__ slo, con
             if (bin[u] == kCoarse) continue;
             const unsigned q = t_off[bin[u]] + atomicAdd(&t_cur[bin[u]], 1u);
             st_lo[q] = a[u]; st_hi[q] = b[u]; st_me[q] = m[u]; st_bin[q] = (uint8_t)bin[u];
+            st_fine[q] = (uint8_t)fine[u];
         }
         __syncthreads();
         for (unsigned q = tid; q < nt; q += 1024) {   // consecutive q of one bin: one run
             const unsigned bb = st_bin[q];
             const size_t g = paged(cur[bb] + (q - t_off[bb]), dpage);
             dlo[g] = st_lo[q]; dhi[g] = st_hi[q]; dme[g] = st_me[q];
+            if (dfine) dfine[g] = st_fine[q];
         }
         __syncthreads();
         if (tid < kCoarse) { cur[tid] += t_cnt[tid]; t_cnt[tid] = 0; t_cur[tid] = 0; }
@@ -563,17 +571,17 @@ __global__ void __launch_bounds__(1024) k_rec_part1(RecPool R, const unsigned* _
                                                     const unsigned* __restrict__ coff,
                                                     const unsigned long long* __restrict__ cbase,
                                                     uint64_t* __restrict__ dlo, uint64_t* __restrict__ dhi,
-                                                    uint64_t* __restrict__ dme) {
+                                                    uint64_t* __restrict__ dme, uint8_t* __restrict__ dfine) {
     __shared__ unsigned long long cur[kCoarse];
     if (blockIdx.x >= *list_n) return;   // (the grid is sized for every page)
     const unsigned pg = list[blockIdx.x];
     if (threadIdx.x < kCoarse) cur[threadIdx.x] = cbase[threadIdx.x] + coff[(size_t)blockIdx.x * kCoarse + threadIdx.x];
-    part_tiles(R.lo, R.hi, R.meta, (size_t)pg * kPageRecs, R.page_used[pg], 64 - kCoarseBits, cur, dlo, dhi, dme);
+    part_tiles(R.lo, R.hi, R.meta, (size_t)pg * kPageRecs, R.page_used[pg], 64 - kCoarseBits, cur, dlo, dhi, dme,
+               nullptr, dfine);
 }
 
 // level 2, histogram: per tile of a coarse bin's run, records per fine bin
-__global__ void __launch_bounds__(1024) k_rec_fhist(const uint64_t* __restrict__ rlo, const uint64_t* __restrict__ rhi,
-                                                    const uint64_t* __restrict__ rme, const L2Tile* __restrict__ tiles,
+__global__ void __launch_bounds__(1024) k_rec_fhist(const uint8_t* __restrict__ rfine, const L2Tile* __restrict__ tiles,
                                                     const unsigned* __restrict__ n_tiles, unsigned* __restrict__ fhist) {
     __shared__ unsigned h[kCoarse];
     if (blockIdx.x >= *n_tiles) return;   // (the grid is sized for the largest batch)
@@ -586,9 +594,7 @@ __global__ void __launch_bounds__(1024) k_rec_fhist(const uint64_t* __restrict__
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const unsigned q = q0 + u * 1024;
-            f[u] = q < T.len ? (unsigned)(rec_hash(rlo[T.start + q], rhi[T.start + q], rme[T.start + q]) >>
-                                          (64 - 2 * kCoarseBits)) & (kCoarse - 1)
-                             : kCoarse;
+            f[u] = q < T.len ? (unsigned)rfine[T.start + q] : kCoarse;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -803,7 +809,7 @@ std::unique_ptr<Arrays3> scratch_take(size_t cap) {
     } catch (const Error& e) {
         if (e.code != BPE_E_NOMEM) throw;
         // the cache holds this device's other free sets: give them back and try once more
-        x->a.release(); x->b.release(); x->c.release();
+        x->a.release(); x->b.release(); x->c.release(); x->d.release();
         scratch_release(dev);
         x->a.alloc(cap);
         x->b.alloc(cap);
@@ -816,7 +822,7 @@ size_t scratch_cached_bytes(int dev) {
     std::lock_guard<std::mutex> g(scratch().m);
     size_t b = 0;
     for (auto& f : scratch().free_)
-        if (f->dev == dev) b += 3 * f->cap * sizeof(uint64_t);
+        if (f->dev == dev) b += f->bytes();
     return b;
 }
 
@@ -828,7 +834,7 @@ size_t scratch_release(int dev) {
         auto& f = scratch().free_;
         for (size_t i = 0; i < f.size();)
             if (dev < 0 || f[i]->dev == dev) {
-                bytes += 3 * f[i]->cap * sizeof(uint64_t);
+                bytes += f[i]->bytes();
                 drop.push_back(std::move(f[i]));
                 f.erase(f.begin() + i);
             } else {
@@ -873,7 +879,7 @@ void RecPoolOwner::init(size_t n_bytes, unsigned grid, hipStream_t s) {
     BPE_HIP(hipMemGetInfo(&free_b, &total_b));
     const size_t avail = free_b + scratch_cached_bytes(dev);
     const size_t reserve = std::max<size_t>(total_b / 16, n_bytes / 2);
-    size_t fit = avail > reserve ? (avail - reserve) / (6 * sizeof(uint64_t)) : 0;
+    size_t fit = avail > reserve ? (avail - reserve) / (6 * sizeof(uint64_t) + 1) : 0;
     if (const char* e = std::getenv("BPE355_REC_POOL_FIT")) fit = (size_t)std::atof(e);   // test knob
     if (fit < want) {
         if (fit < (size_t)grid * kPageRecs / 4)
@@ -904,6 +910,7 @@ void RecPoolOwner::init(size_t n_bytes, unsigned grid, hipStream_t s) {
     // the aggregation's buffers, sized for one batch of every page (no allocation while the
     // file path aggregates between segment copies): level 1 lands in B, level 2 back in the pages
     B = scratch_take(cap);
+    if (B->d.n < cap) B->d.alloc(cap);   // (kept with the set across calls)
     max_tiles = max_pages + kCoarse;
     coff.alloc((size_t)kCoarse * max_pages);
     ctot.alloc(kCoarse);
@@ -967,11 +974,10 @@ void RecPoolOwner::aggregate(bool final, const uint8_t* text, const WordCounts& 
     hipLaunchKernelGGL(k_rec_tiles, dim3(1), dim3(64), 0, s, ctot.p, cbase.p, d_tl.p, d_t0.p, n_tiles.p,
                        d_records.p);
     hipLaunchKernelGGL(k_rec_part1, dim3(max_pages), dim3(1024), 0, s, R, list.p, list_n.p, coff.p, cbase.p, B->a.p,
-                       B->b.p, B->c.p);
+                       B->b.p, B->c.p, B->d.p);
     // level 2: each coarse bin's run, in tiles -> the final bins, laid over the listed pages
     // (their records are all in B now)
-    hipLaunchKernelGGL(k_rec_fhist, dim3(max_tiles), dim3(1024), 0, s, B->a.p, B->b.p, B->c.p, d_tl.p, n_tiles.p,
-                       fhist.p);
+    hipLaunchKernelGGL(k_rec_fhist, dim3(max_tiles), dim3(1024), 0, s, B->d.p, d_tl.p, n_tiles.p, fhist.p);
     hipLaunchKernelGGL(k_rec_fscan, dim3(kBins), dim3(256), 0, s, fhist.p, d_t0.p, ftot.p);
     hipLaunchKernelGGL(k_rec_base, dim3(1), dim3(1024), 0, s, ftot.p, kBins, fbase.p);
     hipLaunchKernelGGL(k_rec_part2, dim3(max_tiles), dim3(1024), 0, s, B->a.p, B->b.p, B->c.p, d_tl.p, n_tiles.p,
