@@ -1157,6 +1157,30 @@ __device__ __forceinline__ Cand readlane_cand(const Cand& c, int j) {
     return r;
 }
 
+// The wave's best candidate in every lane.  The order is the count first (cand_better), so the
+// wave's largest count is found with 64-bit shuffles alone; its holder's candidate is the best
+// when it is the only one (then read from that lane), and only a tie at the top goes through the
+// full order (shuffles of the whole candidate, and the bytes when the 8-byte prefixes tie).
+// (kFastWaveBest = 0: the full order always.)
+#ifndef BPE355_FAST_WAVE_BEST
+#define BPE355_FAST_WAVE_BEST 1
+#endif
+__device__ __forceinline__ Cand wave_best(Cand best, const ToksDev& K) {
+    if (BPE355_FAST_WAVE_BEST) {
+        long long m = best.cnt;
+        for (int o = 32; o > 0; o >>= 1) m = max(m, (long long)__shfl_xor(m, o));
+        if (m == LLONG_MIN) return cand_none();
+        const unsigned long long hold = __ballot(best.cnt == m);
+        if (__popcll(hold) == 1) return readlane_cand(best, __ffsll((long long)hold) - 1);
+        if (best.cnt != m) best = cand_none();
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const Cand oc = shfl_xor_cand(best, o);
+        if (cand_better(oc, best, K.pool, K.off, K.len)) best = oc;
+    }
+    return best;
+}
+
 // A listed candidate's token metadata and dedupe lookup (does the pair's byte string exist as a
 // token already?).  The map holds every token up to the last trip's (k_apply_batch inserts them).
 __device__ __forceinline__ void cand_meta(const Cand& c, const ToksDev& K, const IndexDev& X, TokMetaS& m,
@@ -1317,10 +1341,7 @@ __device__ __forceinline__ void select_core(const RoundState* __restrict__ st, B
                 if (cand_better(c, best, K.pool, K.off, K.len)) best = c;
             }
         }
-        for (int o = 32; o > 0; o >>= 1) {
-            const Cand oc = shfl_xor_cand(best, o);
-            if (cand_better(oc, best, K.pool, K.off, K.len)) best = oc;
-        }
+        best = wave_best(best, K);
         if (lane == 0) S.wave[wv] = best;
     }
     if (pub && tid == 0) probe_stamp(st, ptrip, 26);   // wave 0's partials reduced
@@ -2301,10 +2322,7 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
         }
     }
     if (pw0) probe_stamp(st, B.trip, 11);
-    for (int o = 32; o > 0; o >>= 1) {
-        const Cand oc = shfl_xor_cand(best, o);
-        if (cand_better(oc, best, K.pool, K.off, K.len)) best = oc;
-    }
+    best = wave_best(best, K);
     n_ins = wave_sum(n_ins);
     if ((tid & 63) == 0 && n_ins) atomicAdd(&s_ins, n_ins);
     if ((tid & 63) == 0) s_wave[tid >> 6] = best;
