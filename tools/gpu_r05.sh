@@ -50,6 +50,12 @@ for step in "$@"; do
     python3 tools/rocprof_summary.py $(find $OUT/prof -name "*.db" | head -1) > $OUT/kernel_stats.txt 2>&1
     head -24 $OUT/kernel_stats.txt
     rm -rf $OUT/prof ;;
+  proffile)   # rocprofv3 kernel summary of the default (file-path) bench command, CPU baselines off
+    cd /tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run -- python3 -u $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --steps 3 --warmup 1 > $GRAFT_REPO_ROOT/$OUT/bench_proffile.log 2>&1 || { echo "rocprof failed"; tail -30 $GRAFT_REPO_ROOT/$OUT/bench_proffile.log; exit 1; }
+    cd $GRAFT_REPO_ROOT
+    python3 tools/rocprof_summary.py $(find $OUT/prof -name "*.db" | head -1) > $OUT/kernel_stats_file.txt 2>&1
+    head -24 $OUT/kernel_stats_file.txt
+    rm -rf $OUT/prof ;;
   abfold)   # merge phase, fused trip kernel vs k_select + k_merge_batch, corpus in HBM, alternating
     for rep in 1 2; do for f in 1 0; do
       BPE355_FOLD=$f timeout -k 10 300 python -u bench.py --no-file --no-encode --no-cpu-baseline --steps 3 --warmup 1 > $OUT/abfold_${f}_$rep.log 2>&1 || { echo "abfold failed"; tail -20 $OUT/abfold_${f}_$rep.log; exit 1; }
