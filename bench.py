@@ -66,7 +66,9 @@ def parse():
     ap.add_argument("--cpu-samples-mb", default="16,64", help="pure-Python training samples (MB)")
     ap.add_argument("--cpu-cap-s", type=float, default=20.0, help="wall cap of each sample's merge rounds")
     ap.add_argument("--cpu-encode-mb", type=float, default=64.0)
-    ap.add_argument("--cpu-procs", type=int, default=16, help="host cores for the encode pool / exact leg")
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="host cores for the encode pool / exact leg (0: the host's share, OMP_NUM_THREADS or "
+                         "the affinity mask)")
     ap.add_argument("--no-timing", action="store_true", help="skip per-launch HIP event timing")
     ap.add_argument("--no-file", action="store_true",
                     help="profiling runs: skip the file path (every k_count2 launch then covers the whole "
@@ -85,6 +87,16 @@ def write_corpus(L, path: pathlib.Path, n: int, seed: int, flavour: int):
             del buf
             assert rc == 0, rc
     os.replace(tmp, path)
+
+
+def golden_name(n, seed, flavour, vocab_size):
+    """the scale golden of (n, seed, flavour, vocab), e.g. "train_C3", or None"""
+    import gzip
+    for p in sorted((ROOT / "tests" / "golden" / "scale").glob("train_*.json.gz")):
+        g = json.load(gzip.open(p, "rt"))
+        if (g["n"], g["seed"], g["flavour"], g["vocab"]) == (n, seed, flavour, vocab_size):
+            return p.name[:-len(".json.gz")]
+    return None
 
 
 def golden_parity(n, seed, flavour, vocab_size, vocab, merges):
@@ -113,8 +125,9 @@ def cpu_baselines(args, path, vocab, merges, L):
     """The CPU legs (oracle/cpu_bench.py) in a child process that never touches the GPU: the
     pure-Python port on corpus.en in full and on 16 / 64 MB samples (one core each), the
     pure-Python encode port over 1 M-character pieces (a pool of cores), and the exact C oracle
-    on the full C2 corpus (one counting thread per core).  Returned as cpu_baseline; `value` is
-    the 64 MB training sample (one core, as the reference runs)."""
+    on the full bench corpus (C3; one counting thread per core of the host's share).  Returned as
+    cpu_baseline; `value` is the largest training sample whose extrapolation follows a cost curve
+    measured on that sample (one core, as the reference runs)."""
     import hashlib
     import struct
     import subprocess
@@ -123,9 +136,14 @@ def cpu_baselines(args, path, vocab, merges, L):
     mj, rj = tmp / "merges.json", tmp / "cpu.json"
     mj.write_text(json.dumps({"merges": [(a.hex(), b.hex()) for a, b in merges],
                               "vocab": [(i, b.hex()) for i, b in vocab.items()]}))
+    from oracle.cpu_bench import host_threads
+    procs = args.cpu_procs or host_threads()
     cmd = [sys.executable, "-m", "oracle.cpu_bench", "--corpus", str(path), "--vocab", str(args.vocab),
            "--samples-mb", args.cpu_samples_mb, "--cap-s", str(args.cpu_cap_s), "--merges-json", str(mj),
-           "--encode-mb", str(args.cpu_encode_mb), "--procs", str(args.cpu_procs), "--out", str(rj)]
+           "--encode-mb", str(args.cpu_encode_mb), "--procs", str(procs), "--out", str(rj)]
+    gname = golden_name(path.stat().st_size, args.seed, args.flavour, args.vocab)
+    if gname:   # the exact leg on the bench corpus itself (the headline config)
+        cmd += ["--exact-corpus", str(path), "--exact-golden", gname]
     subprocess.run(cmd, cwd=ROOT, check=True, timeout=600)
     r = json.loads(rj.read_text())
     for f in (mj, rj):
@@ -137,18 +155,24 @@ def cpu_baselines(args, path, vocab, merges, L):
     piece0 = head[:r["encode"]["piece0_chars"]]
     gpu_ids = Tokenizer(vocab, merges, [EOT]).encode(piece0)
     gpu_sha = hashlib.sha256(struct.pack(f"<{len(gpu_ids)}I", *gpu_ids)).hexdigest()
-    big = max(r["train"], key=lambda x: x["bytes"])
+    # the headline sample: the largest whose extrapolation is validated (complete, or corrected
+    # along a cost curve measured on those very bytes)
+    ok = [x for x in r["train"] if x.get("complete") or x.get("growth_validated")]
+    big = max(ok or r["train"], key=lambda x: x["bytes"])
     cores = os.cpu_count()
     enc = r["encode"]
     return {
-        "value": big["MBps"], "unit": "MB/s", "cores": 1, "kind": "port",
+        "value": big["MBps"], "unit": "MB/s", "cores": 1, "kind": "port", "host_cpus": cores,
+        "host_share_threads": r.get("threads"),
         "sample": (f"first {big['bytes'] / 1e6:.1f} MB of the same corpus at vocab {args.vocab}: "
                    f"oracle/cpu_ref.py (pure-Python port with the reference's structure) on 1 core "
                    f"(host shows {cores}); count {big['t_count_s']:.1f}s + build {big['t_build_s']:.1f}s "
                    f"measured, {big['rounds_done']}/{big['rounds_total']} merge rounds measured in "
                    f"{args.cpu_cap_s:.0f}s ({big['ms_per_round']:.1f} ms/round), the rest extrapolated along the "
                    f"port's measured cost curve (x{big.get('growth_factor') or 1:.2f} on the flat rate; "
-                   f"oracle/cpu_port_growth.json, a complete 16 MB run)"),
+                   f"oracle/cpu_port_growth.json, a complete run on these bytes). The port keeps the vocab's "
+                   f"byte strings in a set where the reference's vocab.py:29 scans dict values, so it is "
+                   f"faster than the reference itself (C1: see c1)"),
         "value_flat": big.get("MBps_flat"),
         "rounds_measured_frac": big["rounds_measured_frac"], "merges_per_s": big["merges_per_s"],
         "samples": r["train"],
@@ -158,8 +182,11 @@ def cpu_baselines(args, path, vocab, merges, L):
                        note="cpu_ref.Encoder (tokenizer.py:92-138) over 1 M-character pieces encoded on their "
                             "own (encode.py:31-36), a pool of processes"),
         "exact_cpu": dict(r.get("exact") or {}, kind="port (C oracle)",
-                          note="oracle/bpe_oracle.c on the full C2 corpus (BASELINE configs[1]): one counting "
-                               "thread per core, single-threaded exact merge loop; checked against train_C2"),
+                          note="oracle/bpe_oracle.c (exact incremental trainer, lazy max-heap argmax) on the full "
+                               "corpus of its config (the bench corpus itself when it is C3, BASELINE configs[2]): "
+                               f"one counting thread per core of this host's share ({procs} of the {cores} the host "
+                               "shows; OMP_NUM_THREADS / affinity), single-threaded exact merge loop; checked "
+                               "against the scale golden"),
     }
 
 

@@ -166,12 +166,12 @@ void bpe_result_free(bpe_result* r);
 
 /* Hands back the device memory the trainer keeps between calls so that a repeated train_bpe
  * does not pay for fresh allocations: the corpus buffer (drive.hip), the counter's record pool
- * and aggregation bins (count.hip; about 2 x 2 bytes per corpus byte) and the cached copy
- * streams, for `device` (< 0: every device).  The reference keeps nothing after train_bpe returns
- * (train.py:231) and its caller trains an LM on the same GPU next (train.py:230-232), so the
- * Python train_bpe calls this after every call unless keep_device_buffers=True.  Buffers held by
- * a call in flight are not touched; it must not run while another call of this library copies
- * a file on that device.  Tokenizer buffers: bpe_tok_release_buffers.  *freed_bytes (may be
+ * and aggregation bins (count.hip; about 2 x 2 bytes per corpus byte), for `device` (< 0: every
+ * device).  The reference keeps nothing after train_bpe returns (train.py:231) and its caller
+ * trains an LM on the same GPU next (train.py:230-232), so the Python train_bpe calls this after
+ * every call unless keep_device_buffers=True.  Buffers held by a call in flight are not touched,
+ * and the cached copy streams (no HBM to speak of) stay for the process, so a transfer of
+ * another thread is never cut off.  Tokenizer buffers: bpe_tok_release_buffers.  *freed_bytes (may be
  * NULL): device bytes handed back. */
 int bpe_release_device_memory(int device, size_t* freed_bytes);
 

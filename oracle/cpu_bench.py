@@ -20,10 +20,11 @@ Legs, all on this host's cores:
             the GPU-trained merges, in 1 M-character pieces each encoded on its own -- the
             reference's dataset encoder (encode.py:31-36) -- over a pool of processes (cores
             stated).  Piece 0's ids are returned for bench.py to compare with the GPU encoder.
-  exact     the C oracle (oracle/bpe_oracle.c: exact incremental trainer) on the full C2 corpus
-            (2 GB TinyStories-like, vocab 10 000; BASELINE configs[1]) with one counting thread
-            per core and its single-threaded merge loop; the result is checked against the
-            train_C2 scale golden.
+  exact     the C oracle (oracle/bpe_oracle.c: exact incremental trainer) on the full bench corpus
+            (C3: 11.9 GB OWT-like, vocab 32 000; BASELINE configs[2]; SURVEY.md §8d's "C++ exact
+            CPU trainer on all host cores") with one counting thread per core of the host's share
+            and its single-threaded merge loop; the result is checked against the train_C3 scale
+            golden (train_C2 when the bench corpus is not C3).
 """
 from __future__ import annotations
 
@@ -49,14 +50,18 @@ EOT = "<|endoftext|>"
 BLOCK = 4096
 
 
-def growth_factor(rounds_done: int, rounds_total: int):
+def growth_factor(rounds_done: int, rounds_total: int, nbytes: int, vocab: int):
     """(mean ms per round over the whole run) / (mean over the first rounds_done rounds), from the
-    complete run's cumulative cost curve (cpu_port_growth.json), or None without it"""
+    complete run's cumulative cost curve (cpu_port_growth.json), and whether that curve was
+    measured on this sample (same bytes and vocab: the correction is then validated; a larger
+    sample has more live pairs and its cost grows along a curve nobody measured), or (None, False)"""
     f = HERE / "cpu_port_growth.json"
     if not f.exists() or rounds_done <= 0:
-        return None
+        return None, False
     g = json.loads(f.read_text())
     pts = g["points"]
+    if rounds_total != g.get("rounds_total"):
+        return None, False
     r = min(rounds_done, pts[-1][0])
     if r <= pts[0][0]:   # before the first point: its mean
         t = pts[0][1] * r / pts[0][0]
@@ -67,7 +72,8 @@ def growth_factor(rounds_done: int, rounds_total: int):
                 t = t0 + (t1 - t0) * (r - r0) / max(1, r1 - r0)
                 break
     whole = pts[-1][1] / pts[-1][0]
-    return whole / (t / r) if t > 0 else None
+    validated = nbytes == g.get("bytes") and vocab == g.get("vocab")
+    return (whole / (t / r) if t > 0 else None), validated
 
 
 def _train_leg(args):
@@ -80,11 +86,12 @@ def _train_leg(args):
     t0 = time.perf_counter()
     _, merges, info = cpu_ref.train(text, vocab, [EOT], round_cap_s=cap_s)
     wall = time.perf_counter() - t0
-    nb = len(text.encode("utf-8"))
     # the rounds' mean excludes the one-time build of the words, pair counts and index
     per_round = (info["t_merge_s"] - info["t_build_s"]) / max(1, info["rounds_done"])
     flat = info["t_count_s"] + info["t_build_s"] + per_round * info["rounds_total"]
-    gf = None if info["complete"] else growth_factor(info["rounds_done"], info["rounds_total"])
+    nb = len(text.encode("utf-8"))
+    gf, gf_ok = (None, True) if info["complete"] else growth_factor(info["rounds_done"], info["rounds_total"], nb,
+                                                                     vocab)
     projected = flat if gf is None else info["t_count_s"] + info["t_build_s"] + per_round * info["rounds_total"] * gf
     return {"bytes": nb, "vocab": vocab, "wall_s": round(wall, 3), "t_count_s": round(info["t_count_s"], 3),
             "t_build_s": round(info["t_build_s"], 3),
@@ -94,6 +101,7 @@ def _train_leg(args):
             "MBps": round(nb / projected / 1e6, 5) if projected > 0 else None,
             "MBps_flat": round(nb / flat / 1e6, 5) if flat > 0 else None,
             "growth_factor": round(gf, 3) if gf else None,
+            "growth_validated": bool(gf_ok),
             "merges_per_s": round(info["rounds_total"] / max(1e-9, projected - info["t_count_s"] - info["t_build_s"]), 2)
                             if per_round > 0 else None,
             "complete": info["complete"],
@@ -142,19 +150,39 @@ def encode_leg(path, m, merges_json, procs, chars=1024 * 1024):
             "piece0_chars": len(pieces[0]) if pieces else 0}, (res[0][2] if res else [])
 
 
-def exact_leg(threads, piece=64 << 20):
-    """C oracle on the C2 corpus: generated into host memory first (untimed), then counted by
-    `threads` threads (safe-split pieces, one oracle counter each), summed, and trained"""
+def host_threads():
+    """threads for the CPU legs: the host's share of cores (OMP_NUM_THREADS where the job
+    scheduler sets it -- 16 on the GPU box, whose os.cpu_count() shows every core of the machine
+    -- else the cores this process may run on)"""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(int(env), aff) if env and env.isdigit() else aff)
+
+
+def exact_leg(threads, corpus=None, golden="train_C2", piece=64 << 20):
+    """The C oracle (exact incremental trainer, lazy max-heap argmax) on a full scale corpus:
+    `corpus` = the bench's own corpus file (memory-mapped, page-cache warm), else the golden's
+    corpus generated into host memory first (untimed).  Counted by `threads` threads (safe-split
+    pieces, one oracle counter each), summed, trained, and checked against the golden."""
     import numpy as np
     from bpe_amd import _lib   # the corpus generator's host twin only (no device call)
     from oracle import oracle
-    g = json.load(gzip.open(ROOT / "tests" / "golden" / "scale" / "train_C2.json.gz", "rt"))
+    g = json.load(gzip.open(ROOT / "tests" / "golden" / "scale" / f"{golden}.json.gz", "rt"))
     n, seed, flavour = g["n"], g["seed"], g["flavour"]
-    L = _lib.lib()
-    buf = np.empty(n, dtype=np.uint8)
-    tg = time.perf_counter()
-    assert L.bpe_synth_corpus_host(buf.ctypes.data, n, seed, flavour, 0, threads) == 0
-    t_gen = time.perf_counter() - tg
+    t_gen = 0.0
+    if corpus is not None:
+        assert os.path.getsize(corpus) == n, f"{corpus} is not the {golden} corpus"
+        buf = np.memmap(corpus, dtype=np.uint8, mode="r")
+    else:
+        L = _lib.lib()
+        buf = np.empty(n, dtype=np.uint8)
+        tg = time.perf_counter()
+        assert L.bpe_synth_corpus_host(buf.ctypes.data, n, seed, flavour, 0, threads) == 0
+        t_gen = time.perf_counter() - tg
+    base = buf.ctypes.data
     pieces = [(lo, min(piece, n - lo)) for lo in range(0, n, piece)]
     counters = [oracle.Counter([EOT]) for _ in range(threads)]
     t0 = time.perf_counter()
@@ -162,7 +190,7 @@ def exact_leg(threads, piece=64 << 20):
     def work(t):
         for i in range(t, len(pieces), threads):
             lo, m = pieces[i]
-            counters[t].feed(buf.ctypes.data + lo, m)
+            counters[t].feed(base + lo, m)
 
     th = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
     for x in th:
@@ -176,13 +204,16 @@ def exact_leg(threads, piece=64 << 20):
     vocab, merges = counters[0].train(g["vocab"])
     wall = time.perf_counter() - t0
     counters[0].close()
+    del buf
     h = hashlib.sha256()
     for i in range(len(vocab)):
         h.update(struct.pack("<I", len(vocab[i])) + vocab[i])
     want = [(bytes.fromhex(a), bytes.fromhex(b)) for a, b in g["merges"]]
-    return {"bytes": n, "vocab": g["vocab"], "threads": threads, "wall_s": round(wall, 3),
-            "t_count_s": round(t_count, 3), "t_merge_s": round(wall - t_count, 3), "t_generate_s": round(t_gen, 3),
-            "MBps": round(n / wall / 1e6, 2), "merges_per_s": round(len(merges) / max(1e-9, wall - t_count), 1),
+    return {"config": golden, "bytes": n, "vocab": g["vocab"], "threads": threads,
+            "source": "the bench's corpus file, memory-mapped" if corpus else "generated into host memory",
+            "wall_s": round(wall, 3), "t_count_s": round(t_count, 3), "t_merge_s": round(wall - t_count, 3),
+            "t_generate_s": round(t_gen, 3), "MBps": round(n / wall / 1e6, 2),
+            "merges_per_s": round(len(merges) / max(1e-9, wall - t_count), 1),
             "exact": merges == want and h.hexdigest() == g["vocab_sha256"]}
 
 
@@ -194,16 +225,19 @@ def main():
     ap.add_argument("--cap-s", type=float, default=20.0, help="wall cap of each sample's merge rounds")
     ap.add_argument("--merges-json", default=None)
     ap.add_argument("--encode-mb", type=float, default=64.0)
-    ap.add_argument("--procs", type=int, default=16, help="cores for the encode pool and the exact leg")
+    ap.add_argument("--procs", type=int, default=0, help="cores for the encode pool and the exact leg (0: host_threads())")
     ap.add_argument("--no-exact", action="store_true")
+    ap.add_argument("--exact-corpus", default=None, help="the corpus file of --exact-golden (else generated)")
+    ap.add_argument("--exact-golden", default="train_C2", help="scale golden of the exact leg")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
+    a.procs = a.procs or host_threads()
     c1 = ROOT / "tests" / "golden" / "fixtures" / "corpus.en"
     legs = [(str(c1), None, 500, None)]
     for s in a.samples_mb.split(","):
         m = int(float(s) * 1e6) // BLOCK * BLOCK
         legs.append((a.corpus, m, a.vocab, a.cap_s))
-    out = {"host_cpus": os.cpu_count()}
+    out = {"host_cpus": os.cpu_count(), "threads": host_threads()}
     ctx = mp.get_context("fork")
     with ctx.Pool(len(legs)) as pool:
         async_train = pool.map_async(_train_leg, legs)
@@ -215,7 +249,7 @@ def main():
     out["c1"] = res[0]
     out["train"] = res[1:]
     if not a.no_exact:
-        out["exact"] = exact_leg(a.procs)
+        out["exact"] = exact_leg(a.procs, a.exact_corpus, a.exact_golden)
     with open(a.out, "w") as f:
         json.dump(out, f)
 

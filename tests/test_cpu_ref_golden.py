@@ -39,8 +39,14 @@ def test_cpu_baseline_growth_curve():
     pts = g["points"]
     assert pts[-1][0] == g["rounds_total"] == 31743
     assert all(b[0] > a[0] and b[1] >= a[1] for a, b in zip(pts, pts[1:]))   # cumulative
-    assert abs(cpu_bench.growth_factor(g["rounds_total"], g["rounds_total"]) - 1.0) < 1e-9
+    n, v = g["bytes"], g["vocab"]
+    f, ok = cpu_bench.growth_factor(g["rounds_total"], g["rounds_total"], n, v)
+    assert ok and abs(f - 1.0) < 1e-9
     for r in (10, 199, 450, 1240, 5000):
-        assert cpu_bench.growth_factor(r, g["rounds_total"]) > 1.5
+        f, ok = cpu_bench.growth_factor(r, g["rounds_total"], n, v)
+        assert ok and f > 1.5
+    # the curve is validated only on the sample it was measured on
+    assert cpu_bench.growth_factor(450, g["rounds_total"], 4 * n, v)[1] is False
+    assert cpu_bench.growth_factor(450, g["rounds_total"], n, 10000)[1] is False
     # the flat rate of the first rounds under-estimated the complete run by ~86 %
     assert g["flat_projection_error"] < -0.5

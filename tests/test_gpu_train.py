@@ -92,3 +92,28 @@ def test_train_matches_oracle_tie_heavy(seed):
     got = bpe_amd.train_bpe_bytes(data, vocab, ["<|endoftext|>"])
     assert got[1] == want[1]
     assert got[0] == want[0]
+
+
+@pytest.mark.parametrize("knob", ["BPE355_FOLD=1", "BPE355_LDS_CELLS=0"])
+def test_train_runtime_variants(knob, monkeypatch):
+    """The merge loop's run-time variants against the same goldens: the fused trip
+    kernel k_trip (BPE355_FOLD=1: every workgroup decides the batch again while others already
+    rewrite) and the 64-bit global delta cells (BPE355_LDS_CELLS=0: the path a batch takes when
+    its P1 count reaches 2^32) -- each on the reference fixture, tie-heavy text and synthetic
+    text, bit-exact."""
+    import random
+    name, val = knob.split("=")
+    monkeypatch.setenv(name, val)
+    vocab, merges = bpe_amd.train_bpe(gpt2_files.FIXTURES / "corpus.en", 500, ["<|endoftext|>"])
+    ref_vocab, ref_merges = gpt2_files.load_reference_train_golden()
+    assert merges == ref_merges
+    assert set(vocab.values()) == set(ref_vocab.values())
+    for seed in (3, 7):
+        rng = random.Random(9000 + seed)
+        data = _tie_heavy_text(rng, 20000).encode("utf-8")
+        want = oracle.train_raw(data, 1000, ["<|endoftext|>"])
+        assert bpe_amd.train_bpe_bytes(data, 1000, ["<|endoftext|>"]) == want
+    import synth_text
+    data = synth_text.generate(11, 3_000_000, "mixed").encode("utf-8")
+    want = oracle.train_raw(data, 4000, ["<|endoftext|>"])
+    assert bpe_amd.train_bpe_bytes(data, 4000, ["<|endoftext|>"]) == want

@@ -41,7 +41,8 @@ def last_train_stats() -> dict:
 
 def release_device_memory(device: int = -1) -> int:
     """Hand back the device memory the trainer keeps between calls (the corpus buffer, the
-    counter's record pool and bins, the copy streams) on `device` (-1: every device); returns the
+    counter's record pool and bins) on `device` (-1: every device; buffers a call of another
+    thread is using are left alone, and the copy streams stay for the process); returns the
     bytes freed.  train_bpe calls it after every call unless keep_device_buffers=True."""
     L = _lib.lib()
     freed = ctypes.c_size_t(0)

@@ -190,7 +190,8 @@ int bpe_release_device_memory(int device, size_t* freed_bytes) {
         BPE_REQUIRE(device < n, BPE_E_ARG, "device " + std::to_string(device) + " is not visible");
         size_t b = bpe::corpus_release(device);
         b += bpe::scratch_release(device);
-        bpe::dma_release(device);
+        // the copy streams stay: they hold no HBM to speak of, and a transfer of another thread
+        // (encode_file, train_bpe) may be using them right now (drive.hip, DmaCache)
         if (freed_bytes) *freed_bytes = b;
     });
 }

@@ -50,8 +50,8 @@ void train_source(const Source& src, int vocab_size, const std::vector<std::stri
 void train_source_comm(const Source& src, bool split, int vocab_size, const std::vector<std::string>& specials,
                        Comm* comm, TrainOutput& out);
 // bpe_release_device_memory: the corpus buffers kept for `dev` (< 0: every device) go back to the
-// device allocator, and the device's cached copy streams are destroyed; returns the bytes freed
+// device allocator; returns the bytes freed.  Buffers a running call holds are not touched, and the
+// cached copy streams are kept for the process (a concurrent transfer may be using them)
 size_t corpus_release(int dev);
-void dma_release(int dev);
 
 }  // namespace bpe

@@ -293,20 +293,6 @@ const DmaStreams& cached_dma(int device, int dir) {
 }
 }  // namespace
 
-void dma_release(int dev) {
-    std::vector<DmaStreams*> drop;
-    {
-        DmaCache& c = dma_cache();
-        std::lock_guard<std::mutex> g(c.m);
-        for (size_t i = 0; i < c.made.size(); ++i)
-            if (c.made[i] && (dev < 0 || (int)(i / 4) == dev)) {
-                drop.push_back(c.made[i]);
-                c.made[i] = nullptr;
-            }
-    }
-    for (auto* d : drop) delete d;   // synchronises, then destroys each stream
-}
-
 // ------------------------------------------------------------------ sources
 Source Source::open_path(const char* path) {
     Source s;

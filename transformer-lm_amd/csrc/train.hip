@@ -88,6 +88,9 @@ struct RoundState {
     unsigned max_len;           // longest word (bytes): the most one new token adds to the pool
     int max_batch;              // merges allowed per trip (1: one merge per trip)
     unsigned long long pair_limit;   // ... or when the pair table could pass this many keys
+    long long narrow_limit;     // the merge sums a member's cells in 32-bit LDS words while count(P1) is
+                                // below this: 2^32 (a cell never exceeds count(P_j) <= count(P1)), 0 under
+                                // the test knob BPE355_LDS_CELLS=0 (every cell to the global 64-bit atomics)
 };
 
 struct Partial {
@@ -975,7 +978,7 @@ constexpr int kTopM = kMaxBatch + 1;
 // the select's clash check: candidates i < kClashI (a power of two >= kMaxBatch), kClashJ lanes each
 constexpr int kClashI = kMaxBatch <= 16 ? 16 : 32;
 constexpr int kClashJ = 64 / kClashI;
-#ifndef BPE355_LDS_CELLS
+#ifndef BPE355_LDS_CELLS   // build-time default of the run-time knob of the same name
 #define BPE355_LDS_CELLS 1
 #endif
 #ifndef BPE355_LDS_B
@@ -1235,6 +1238,7 @@ struct SelLds {
 
 // where the publishing workgroup records a batch decision for the host (round records, the
 // block's trip records)
+constexpr int kTI = 8;   // ints per trip record: round, k, full scan, list entries, ntok, |C|, listed keys, fresh
 struct SelOut {
     uint32_t *m_a, *m_b, *m_new, *m_mode;
     long long* m_cnt;
@@ -1296,7 +1300,7 @@ __device__ __forceinline__ void select_core(const RoundState* __restrict__ st, B
         if (tid == 0) {
             OB.stop = -1;
             if (pub && O.trip_info) {
-                int* ti = O.trip_info + 4 * O.trip_slot;
+                int* ti = O.trip_info + kTI * O.trip_slot;
                 ti[0] = -1; ti[1] = 0; ti[2] = 0; ti[3] = 0;
             }
         }
@@ -1458,7 +1462,7 @@ __device__ __forceinline__ void select_core(const RoundState* __restrict__ st, B
         if (lane == 0) {
             OB.stop = stop;
             if (pub && O.trip_info) {
-                int* ti = O.trip_info + 4 * O.trip_slot;
+                int* ti = O.trip_info + kTI * O.trip_slot;
                 ti[0] = -1; ti[1] = 0; ti[2] = 0; ti[3] = 0;
             }
         }
@@ -1692,8 +1696,10 @@ __device__ __forceinline__ void select_core(const RoundState* __restrict__ st, B
                 atomicAdd(&bs->k_hist[k], 1ull);
             }
             if (O.trip_info) {   // for the host: first round, members, scan mode, list entries
-                int* ti = O.trip_info + 4 * O.trip_slot;
+                int* ti = O.trip_info + kTI * O.trip_slot;
                 ti[0] = round; ti[1] = k; ti[2] = full; ti[3] = (int)tot_list;
+                // (the trip log's extra fields: tokens, C entries the apply scans, listed keys, fresh tokens)
+                ti[4] = ntok; ti[5] = (int)nC; ti[6] = (int)ln; ti[7] = (int)tot_fresh;
             }
             probe_stamp(st, ptrip, 3);
             probe_stamp(st, ptrip, 4);
@@ -1816,9 +1822,9 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
     // every field the prologue needs in one round trip (none depends on another)
     const int stop = B.stop, k = B.k, b_trip = B.trip, b_ntok = B.ntok, b_prev_k = B.prev_k;
     const unsigned idle_from = B.idle_from;
-    // 32-bit LDS cells hold every member's sums (test knob BPE355_LDS_CELLS=0: every cell global,
-    // the path of a batch whose P1 count reaches 2^32)
-    const bool narrow = BPE355_LDS_CELLS && B.m[0].cnt < (1ll << 32);
+    // 32-bit LDS cells hold every member's sums (run-time test knob BPE355_LDS_CELLS=0: every cell
+    // global, the path of a batch whose P1 count reaches 2^32)
+    const bool narrow = B.m[0].cnt < st->narrow_limit;
     unsigned ma = 0, mb = 0, mn = 0, mlb = 0, mpre = 0;
     if (tid < kMaxBatch) { ma = B.m[tid].a; mb = B.m[tid].b; mn = B.m[tid].nw; mlb = B.m[tid].list_beg; }
     if (tid <= kMaxBatch) mpre = B.list_pre[tid];
@@ -2975,6 +2981,7 @@ class MergeLoop {
     bool fused_ = false;         // k_trip (BPE355_FOLD=1), else k_select + k_merge_batch
     int max_batch_ = kMaxBatch;
     long long trips_launched_ = 0, trips_run_ = 0, rounds_batched_ = 0;
+    std::unique_ptr<std::vector<int>> trip_log_;   // analysis knob BPE355_TRIP_LOG=path: every trip's record
     DevBuf<BatchState> bs_;
     DevBuf<Batch> batch_;
     DevBuf<uint32_t> tags_;      // per slot word: the last batch that claimed it
@@ -3362,10 +3369,10 @@ void MergeLoop<TokT>::run() {
         BPE_HIP(hipMemsetAsync(bs_.p, 0, sizeof(BatchState), s_));
         batch_.alloc(1);
         BPE_HIP(hipMemsetAsync(batch_.p, 0, sizeof(Batch), s_));
-        trip_info_.alloc(2 * 4 * kTrips);
+        trip_info_.alloc(2 * kTI * kTrips);
         if (!snap_st_) {   // coherent pinned memory, written by k_snapshot
             BPE_HIP(hipHostMalloc(reinterpret_cast<void**>(&snap_st_), 2 * sizeof(RoundState), hipHostMallocCoherent));
-            BPE_HIP(hipHostMalloc(reinterpret_cast<void**>(&snap_ti_), 2 * 4 * kTrips * sizeof(int),
+            BPE_HIP(hipHostMalloc(reinterpret_cast<void**>(&snap_ti_), 2 * kTI * kTrips * sizeof(int),
                                   hipHostMallocCoherent));
             BPE_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&snap_st_dev_), snap_st_, 0));
             BPE_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&snap_ti_dev_), snap_ti_, 0));
@@ -3377,6 +3384,8 @@ void MergeLoop<TokT>::run() {
         const char* fe = std::getenv("BPE355_FOLD");
         fused_ = fe && fe[0] == '1';
     }
+    const char* trip_log_path = std::getenv("BPE355_TRIP_LOG");   // analysis knob: the trips' records
+    if (batched_ && trip_log_path) trip_log_.reset(new std::vector<int>());
     m_a_.alloc(n_rounds_); m_b_.alloc(n_rounds_); m_new_.alloc(n_rounds_); m_mode_.alloc(n_rounds_);
     const char* round_log = std::getenv("BPE355_ROUND_LOG");   // analysis knob: per-round records
     if (round_log) m_cnt_.alloc(n_rounds_);
@@ -3427,6 +3436,10 @@ void MergeLoop<TokT>::run() {
     hs_.halt = HALT_REBUILD;
     hs_.max_len = std::max(max_len_, 1u);
     hs_.max_batch = max_batch_;
+    {
+        const char* e = std::getenv("BPE355_LDS_CELLS");
+        hs_.narrow_limit = (e ? e[0] != '0' : BPE355_LDS_CELLS != 0) ? (1ll << 32) : 0;
+    }
     if (batched_ && std::getenv("BPE355_PROBE") && !BPE355_PROBE_CODE)
         std::fprintf(stderr, "[bpe355 probe] BPE355_PROBE needs a library built with -DBPE355_PROBE_CODE=1 "
                              "(tools/build_variant.sh): no stamps in this one\n");
@@ -3604,6 +3617,12 @@ void MergeLoop<TokT>::run() {
                 std::fwrite(&va[r], 4, 1, f); std::fwrite(&vb[r], 4, 1, f); std::fwrite(&vn[r], 4, 1, f);
                 std::fwrite(&vm[r], 4, 1, f); std::fwrite(&vc[r], 8, 1, f);
             }
+            std::fclose(f);
+        }
+    }
+    if (trip_log_ && !trip_log_->empty()) {   // kTI ints per trip (k > 0: the trips that ran)
+        if (FILE* f = std::fopen(trip_log_path, "wb")) {
+            std::fwrite(trip_log_->data(), sizeof(int), trip_log_->size(), f);
             std::fclose(f);
         }
     }
@@ -3831,7 +3850,7 @@ void MergeLoop<TokT>::launch_block(int slot, bool timing, std::vector<hipEvent_t
     const size_t lr_member = 2ull * tok_cap_, lr_parity = (size_t)kMaxBatch * lr_member;
     const unsigned ntb = tok_cap_;
     const unsigned apply_blocks = kApplyBatchBlocks;
-    int* ti = trip_info_.p + (size_t)slot * 4 * kTrips;
+    int* ti = trip_info_.p + (size_t)slot * kTI * kTrips;
     slot_base_[slot] = trips_launched_;
     for (int t = 0; t < trips_; ++t) {
         const bool timed = timing && (trips_launched_ + t) % kTimingStride == 0;
@@ -3858,8 +3877,8 @@ void MergeLoop<TokT>::launch_block(int slot, bool timing, std::vector<hipEvent_t
     // the block's snapshot: one small kernel stores the state and the trip records into pinned
     // host memory (two copy packets cost ~3x as much at every block boundary)
     hipLaunchKernelGGL(k_snapshot, dim3(1), dim3(256), 0, s_, (const uint32_t*)st_.p,
-                       (unsigned)(sizeof(RoundState) / 4), (const uint32_t*)ti, (unsigned)(4 * trips_),
-                       (uint32_t*)(snap_st_dev_ + slot), (uint32_t*)(snap_ti_dev_ + (size_t)slot * 4 * kTrips));
+                       (unsigned)(sizeof(RoundState) / 4), (const uint32_t*)ti, (unsigned)(kTI * trips_),
+                       (uint32_t*)(snap_st_dev_ + slot), (uint32_t*)(snap_ti_dev_ + (size_t)slot * kTI * kTrips));
     BPE_HIP(hipGetLastError());
     BPE_HIP(hipEventRecord(blk_ev_[slot], s_));
     trips_launched_ += trips_;
@@ -3870,34 +3889,35 @@ void MergeLoop<TokT>::finish_block(int slot, bool timing, std::vector<hipEvent_t
                                    double& k1_bytes, long long& k1_launches) {
     BPE_HIP(hipEventSynchronize(blk_ev_[slot]));
     hs_ = snap_st_[slot];
-    const int* ti = snap_ti_ + (size_t)slot * 4 * kTrips;
+    const int* ti = snap_ti_ + (size_t)slot * kTI * kTrips;
     for (int t = 0; t < trips_; ++t) {
-        trips_run_ += ti[4 * t + 1] > 0;
-        rounds_batched_ += ti[4 * t + 1] > 1 ? ti[4 * t + 1] : 0;
+        trips_run_ += ti[kTI * t + 1] > 0;
+        rounds_batched_ += ti[kTI * t + 1] > 1 ? ti[kTI * t + 1] : 0;
+        if (trip_log_) trip_log_->insert(trip_log_->end(), ti + kTI * t, ti + kTI * (t + 1));
     }
     {   // size the merge grid of the blocks launched from now on by this block's largest trip:
         // the members' list entries at one per thread, twice over for growth; a full scan (or
         // a single member without a list) wants the whole layout.  Any grid is correct.
         unsigned need = kMaxBatch;
         for (int t = 0; t < trips_; ++t) {
-            if (ti[4 * t + 1] <= 0) continue;
-            if (ti[4 * t + 2]) { need = merge_grid_; break; }
-            need = std::max(need, 2 * ceil_div((unsigned)ti[4 * t + 3], 256u));
+            if (ti[kTI * t + 1] <= 0) continue;
+            if (ti[kTI * t + 2]) { need = merge_grid_; break; }
+            need = std::max(need, 2 * ceil_div((unsigned)ti[kTI * t + 3], 256u));
         }
         merge_grid_cur_ = std::max<unsigned>(64, need);
     }
     if (!timing) return;
     const double slot_avg = scan_bytes_ / std::max(1u, idev_.n_slot_words + words_.ln);
     for (int t = 0; t < trips_; ++t) {
-        if ((slot_base_[slot] + t) % kTimingStride || ti[4 * t + 1] <= 0) continue;
+        if ((slot_base_[slot] + t) % kTimingStride || ti[kTI * t + 1] <= 0) continue;
         float ms = 0;
         const hipEvent_t* e = &ev[2 * ((size_t)slot * kTrips + t)];
         BPE_HIP(hipEventElapsedTime(&ms, e[0], e[1]));
         // algorithmic bytes: every slot on a full scan, else the members' list entries and their
         // slots (at the table's mean slot size); every long word once per trip
-        const bool full = ti[4 * t + 2] != 0;
+        const bool full = ti[kTI * t + 2] != 0;
         k1_ms += ms;
-        k1_bytes += full ? scan_bytes_ : long_bytes_ + (double)(unsigned)ti[4 * t + 3] * (4.0 + slot_avg);
+        k1_bytes += full ? scan_bytes_ : long_bytes_ + (double)(unsigned)ti[kTI * t + 3] * (4.0 + slot_avg);
         ++k1_launches;
     }
 }
