@@ -160,6 +160,9 @@ typedef struct {
     double t_gather_ms;       /* multi-GPU word exchange: the all-gather of the segments */
     double t_union_ms;        /* multi-GPU word exchange: the union-table inserts */
     int64_t exchange_seg_bytes; /* multi-GPU word exchange: one rank's segment (all ranks' equal) */
+    double t_alltoall_ms;     /* multi-GPU word exchange: the all-to-all of the words by owner */
+    double t_owner_ms;        /* multi-GPU word exchange: the owner-table inserts */
+    int64_t exchange_a2a_bytes; /* multi-GPU word exchange: the bytes this rank sent in the all-to-all */
 } bpe_train_stats;
 int bpe_result_stats(const bpe_result* r, bpe_train_stats* out);
 void bpe_result_free(bpe_result* r);

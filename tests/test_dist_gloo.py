@@ -2,8 +2,11 @@
 
 libbpe355 shards the corpus into slabs cut at safe points (one per rank) and has two ways to
 combine them (exchange.hip, train.hip):
-  words  (default)  each rank counts its slab's unique words; ONE all-gather of the word tables;
-                    every rank trains on the union (counts summed) with no further collective;
+  words  (default)  each rank counts its slab's unique words; ONE all-to-all sends every word to
+                    the rank its hash names (its owner sums the ranks' counts); ONE all-gather of
+                    the owners' tables (each word once); every rank trains on the union with no
+                    further collective ("words-gather": the local tables gathered as they are,
+                    counts summed by every rank; BPE355_EXCHANGE_OWNER=0);
   rounds            each rank keeps its unique words local and per merge round all-reduces one
                     fixed-layout int64 buffer of delta cells (L[x] for (x,a)-=c/(x,new)+=c and
                     R[y] for (b,y)-=c/(new,y)+=c); every rank applies the global deltas to a
@@ -48,7 +51,29 @@ def sharded_train(rank, world, slab: bytes, vocab_size, specials, mode="rounds")
     text = oracle.decode_text(slab)
     counts = oracle.word_counts(text, specials)
     if mode == "words":
-        # the one collective: gather every rank's table, sum the counts word by word
+        # the all-to-all by owner: rank r's words for owner o are o's share of r's table (the
+        # restatement ships every rank's per-owner tables and each keeps its column: gloo has no
+        # object all-to-all); the owner sums the counts of its words over the ranks
+        import zlib
+        mine = [dict() for _ in range(world)]
+        for w, c in counts.items():
+            mine[zlib.crc32(w) % world][w] = c
+        sent = [None] * world
+        dist.all_gather_object(sent, mine)
+        owned = {}
+        for src in sent:
+            for w, c in src[rank].items():
+                owned[w] = owned.get(w, 0) + c
+        # then one all-gather of the owners' tables: disjoint, so the union needs no sum
+        gathered = [None] * world
+        dist.all_gather_object(gathered, owned)
+        counts = {}
+        for table in gathered:
+            for w, c in table.items():
+                assert w not in counts, "a word with two owners"
+                counts[w] = c
+    elif mode == "words-gather":
+        # gather every rank's table as it is, sum the counts word by word
         gathered = [None] * world
         dist.all_gather_object(gathered, counts)
         counts = {}
@@ -71,7 +96,7 @@ def sharded_train(rank, world, slab: bytes, vocab_size, specials, mode="rounds")
     W = [[tid[c] for c in w] for w in words]
 
     def allreduce(vals):
-        if mode == "words":   # the union is global already: no per-round exchange
+        if mode != "rounds":   # the union is global already: no per-round exchange
             return vals
         t = torch.tensor(vals, dtype=torch.int64)
         dist.all_reduce(t)
@@ -162,7 +187,7 @@ def run_sharded(data: bytes, world: int, vocab_size: int, specials, mode="rounds
     return out
 
 
-@pytest.mark.parametrize("mode", ["words", "rounds"])
+@pytest.mark.parametrize("mode", ["words", "words-gather", "rounds"])
 @pytest.mark.parametrize("name,world", [("corpus_en_500", 2), ("tiny_1200", 2),
                                         ("synth_mixed_200k", 2), ("corpus_en_1000", 3)])
 def test_sharded_protocol_matches_reference(name, world, mode):

@@ -4,8 +4,10 @@ A one-GPU box cannot hold two RCCL ranks, so the ranks here are threads of this 
 share the device and exchange through the library's in-process communicator
 (BPE355_INPROC_RANKS=1, csrc/comm.hip InProcComm); the slab cutting, the collectives' call
 pattern and every kernel are the ones the RCCL path runs.  Both exchange modes are covered:
-  words  (default)  one all-gather of the slabs' unique-word tables, then rank 0 trains on the
-                    union (exchange.hip);
+  words  (default)  one all-to-all of the slabs' unique words by owner (the rank the word's hash
+                    names sums its counts), one all-gather of the owners' tables, then rank 0
+                    trains on the union (exchange.hip); "words-gather" skips the all-to-all
+                    (BPE355_EXCHANGE_OWNER=0: every rank's local table is gathered as it is);
   rounds            local word tables, one all-reduce of the delta cells per merge round, a
                     replicated pair table and argmax on every rank (the driver checks that all
                     ranks chose the same merges).
@@ -30,13 +32,16 @@ bpe_amd = pytest.importorskip("bpe_amd")
 def ranks(monkeypatch):
     def set_(n, mode):
         monkeypatch.setenv("BPE355_INPROC_RANKS", "1")
+        if mode == "words-gather":
+            monkeypatch.setenv("BPE355_EXCHANGE_OWNER", "0")
+            mode = "words"
         monkeypatch.setenv("BPE355_EXCHANGE", mode)
         bpe_amd.set_num_gpus(n)
     yield set_
     bpe_amd.set_num_gpus(None)
 
 
-@pytest.mark.parametrize("mode", ["words", "rounds"])
+@pytest.mark.parametrize("mode", ["words", "words-gather", "rounds"])
 @pytest.mark.parametrize("name", ["corpus_en_1000", "tiny_1200", "synth_mixed_200k"])
 def test_sharded_gpu_matches_reference(name, mode, ranks):
     o, vocab, merges = G.train_expect(name)
@@ -48,7 +53,7 @@ def test_sharded_gpu_matches_reference(name, mode, ranks):
     assert got_vocab == vocab
 
 
-@pytest.mark.parametrize("mode,n", [("words", 2), ("rounds", 2), ("rounds", 3)])
+@pytest.mark.parametrize("mode,n", [("words", 2), ("words", 5), ("words-gather", 3), ("rounds", 2), ("rounds", 3)])
 def test_sharded_gpu_synthetic_vs_oracle(mode, n, ranks):
     import synth_text
     data = synth_text.generate(31, 4_000_000, "ascii").encode("utf-8")
@@ -67,7 +72,8 @@ def _rccl_worker(port, q, force):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    os.environ[force] = "1"
+    for f in force.split("+"):
+        os.environ[f] = "1"
     if force == "BPE355_FORCE_COMM":
         os.environ["BPE355_EXCHANGE"] = "rounds"
     try:
@@ -85,7 +91,8 @@ def _rccl_worker(port, q, force):
         q.put(repr(e))
 
 
-@pytest.mark.parametrize("force", ["BPE355_FORCE_COMM", "BPE355_FORCE_EXCHANGE"])
+@pytest.mark.parametrize("force", ["BPE355_FORCE_COMM", "BPE355_FORCE_EXCHANGE",
+                                   "BPE355_FORCE_EXCHANGE+BPE355_EXCHANGE_OWNER"])
 def test_rccl_comm_single_rank_forced(force):
     import socket
     s = socket.socket()

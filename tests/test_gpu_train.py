@@ -94,16 +94,20 @@ def test_train_matches_oracle_tie_heavy(seed):
     assert got[0] == want[0]
 
 
-@pytest.mark.parametrize("knob", ["BPE355_FOLD=1", "BPE355_LDS_CELLS=0"])
+@pytest.mark.parametrize("knob", ["BPE355_FOLD=1", "BPE355_LDS_CELLS=0",
+                                  "BPE355_DENSE_TOK=128+BPE355_CHECK_MARKS=1", "BPE355_CELL_MARKS=0"])
 def test_train_runtime_variants(knob, monkeypatch):
     """The merge loop's run-time variants against the same goldens: the fused trip
     kernel k_trip (BPE355_FOLD=1: every workgroup decides the batch again while others already
     rewrite) and the 64-bit global delta cells (BPE355_LDS_CELLS=0: the path a batch takes when
-    its P1 count reaches 2^32) -- each on the reference fixture, tie-heavy text and synthetic
-    text, bit-exact."""
+    its P1 count reaches 2^32), the touched-block cells with a dense prefix of 128 tokens (every
+    later token's cells found through the merge's marks, as at the bench config past 2048 tokens)
+    and without marks (every cell scanned) -- each on the reference fixture, tie-heavy text and
+    synthetic text, bit-exact."""
     import random
-    name, val = knob.split("=")
-    monkeypatch.setenv(name, val)
+    for kv in knob.split("+"):   # (BPE355_CHECK_MARKS: the library fails the call if a delta cell
+        name, val = kv.split("=")  # escaped the marks or two apply workgroups listed other blocks)
+        monkeypatch.setenv(name, val)
     vocab, merges = bpe_amd.train_bpe(gpt2_files.FIXTURES / "corpus.en", 500, ["<|endoftext|>"])
     ref_vocab, ref_merges = gpt2_files.load_reference_train_golden()
     assert merges == ref_merges

@@ -45,6 +45,8 @@ class TrainStats(ctypes.Structure):
         ("count_partial_ms", ctypes.c_double), ("n_count_batches", ctypes.c_int64),
         ("t_gather_ms", ctypes.c_double), ("t_union_ms", ctypes.c_double),
         ("exchange_seg_bytes", ctypes.c_int64),
+        ("t_alltoall_ms", ctypes.c_double), ("t_owner_ms", ctypes.c_double),
+        ("exchange_a2a_bytes", ctypes.c_int64),
     ]
 
     def as_dict(self):

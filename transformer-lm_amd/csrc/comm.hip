@@ -5,6 +5,7 @@
 // exercised by several processes that share one GPU (tests).
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <condition_variable>
 #include <cstring>
 #include <mutex>
@@ -47,6 +48,21 @@ struct RcclComm final : Comm {
         if (bytes == 0) return;
         BPE_NCCL(ncclAllGather(d_send, d_recv, bytes, ncclUint8, comm, stream));
     }
+    // one grouped send/recv per peer over xGMI (the own share is a device copy)
+    void alltoallv_bytes(const void* d_send, const size_t* soff, const size_t* scnt, void* d_recv,
+                         const size_t* roff, const size_t* rcnt, hipStream_t stream) override {
+        const uint8_t* snd = static_cast<const uint8_t*>(d_send);
+        uint8_t* rcv = static_cast<uint8_t*>(d_recv);
+        if (scnt[rank])
+            BPE_HIP(hipMemcpyAsync(rcv + roff[rank], snd + soff[rank], scnt[rank], hipMemcpyDeviceToDevice, stream));
+        BPE_NCCL(ncclGroupStart());
+        for (int p = 0; p < nranks; ++p) {
+            if (p == rank) continue;
+            if (scnt[p]) BPE_NCCL(ncclSend(snd + soff[p], scnt[p], ncclUint8, p, comm, stream));
+            if (rcnt[p]) BPE_NCCL(ncclRecv(rcv + roff[p], rcnt[p], ncclUint8, p, comm, stream));
+        }
+        BPE_NCCL(ncclGroupEnd());
+    }
 };
 
 struct HostComm final : Comm {
@@ -81,6 +97,9 @@ struct InProcShared {
     std::vector<int64_t> acc, result;
     std::vector<uint8_t> gather;   // all-gather: rank r's segment at r * bytes
     int g_entered = 0, g_readers = 0;
+    // all-to-all: every rank's whole send buffer and its offsets / sizes per destination
+    std::vector<std::vector<uint8_t>> a2a;
+    std::vector<std::vector<size_t>> a2a_off, a2a_cnt;
     // a rank left a collective with an error: every rank waiting in (or later entering) one
     // throws instead of waiting for it forever
     bool failed = false;
@@ -172,6 +191,56 @@ struct InProcComm final : Comm {
             const uint8_t* all = sh->gather.data();
             lk.unlock();
             BPE_HIP(hipMemcpyAsync(d_recv, all, (size_t)nranks * bytes, hipMemcpyHostToDevice, stream));
+            BPE_HIP(hipStreamSynchronize(stream));
+            lk.lock();
+            --sh->g_readers;
+            sh->cv.notify_all();
+        });
+    }
+    // every rank stages its send buffer in host memory; after the last one arrives each copies
+    // its share of every rank's buffer (rank q's bytes for this rank) back to its device
+    void alltoallv_bytes(const void* d_send, const size_t* soff, const size_t* scnt, void* d_recv,
+                         const size_t* roff, const size_t* rcnt, hipStream_t stream) override {
+        guarded([&] {
+            size_t total = 0;
+            for (int p = 0; p < nranks; ++p) total = std::max(total, soff[p] + scnt[p]);
+            std::unique_lock<std::mutex> lk(sh->m);
+            sh->cv.wait(lk, [&] { return sh->g_readers == 0 || sh->failed; });
+            check_failed();
+            const uint64_t g = sh->gen;
+            if (sh->g_entered == 0) {
+                sh->a2a.assign(nranks, {});
+                sh->a2a_off.assign(nranks, {});
+                sh->a2a_cnt.assign(nranks, {});
+            }
+            ++sh->g_entered;
+            std::vector<uint8_t>& mine = sh->a2a[rank];
+            sh->a2a_off[rank].assign(soff, soff + nranks);
+            sh->a2a_cnt[rank].assign(scnt, scnt + nranks);
+            lk.unlock();
+            mine.resize(total);
+            if (total) BPE_HIP(hipMemcpyAsync(mine.data(), d_send, total, hipMemcpyDeviceToHost, stream));
+            BPE_HIP(hipStreamSynchronize(stream));
+            lk.lock();
+            check_failed();
+            if (++sh->arrived == nranks) {
+                sh->arrived = 0;
+                sh->g_entered = 0;
+                sh->g_readers = nranks;
+                ++sh->gen;
+                sh->cv.notify_all();
+            } else {
+                sh->cv.wait(lk, [&] { return sh->gen != g || sh->failed; });
+                check_failed();
+            }
+            lk.unlock();
+            for (int q = 0; q < nranks; ++q) {
+                const size_t c = sh->a2a_cnt[q][rank];
+                BPE_REQUIRE(c == rcnt[q], BPE_E_RCCL, "in-process all-to-all: ranks disagree on a size");
+                if (c)
+                    BPE_HIP(hipMemcpyAsync(static_cast<uint8_t*>(d_recv) + roff[q], sh->a2a[q].data() + sh->a2a_off[q][rank],
+                                           c, hipMemcpyHostToDevice, stream));
+            }
             BPE_HIP(hipStreamSynchronize(stream));
             lk.lock();
             --sh->g_readers;

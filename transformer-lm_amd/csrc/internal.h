@@ -22,6 +22,12 @@ struct Comm {
     // d_recv[r * bytes .. (r + 1) * bytes) = rank r's d_send[0 .. bytes) (default: through
     // allreduce_i64; RCCL overrides it with ncclAllGather)
     virtual void allgather_bytes(const void* d_send, size_t bytes, void* d_recv, hipStream_t stream);
+    // all-to-all of variable sizes: rank p receives scnt[p] bytes from d_send + soff[p] of this
+    // rank, and this rank's d_recv + roff[q] gets rcnt[q] bytes from rank q (default: through
+    // allgather_bytes, every rank's whole send buffer; RCCL and the in-process ranks override it
+    // with point-to-point copies)
+    virtual void alltoallv_bytes(const void* d_send, const size_t* soff, const size_t* scnt, void* d_recv,
+                                 const size_t* roff, const size_t* rcnt, hipStream_t stream);
 };
 
 // ---------------------------------------------------------------- small transfers (hostio.hip)

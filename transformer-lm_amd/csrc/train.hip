@@ -1018,6 +1018,11 @@ constexpr int kRegRewriteMaxW = BPE355_REG_REWRITE_MAXW;
 #endif
 constexpr int kPairFilterK = BPE355_PAIR_FILTER_K;
 constexpr unsigned kPairSlots = 4096;
+// list mode: a word's count is loaded only when the word holds a member (build knob)
+#ifndef BPE355_LATE_COUNT
+#define BPE355_LATE_COUNT 1
+#endif
+constexpr bool kLateCount = BPE355_LATE_COUNT != 0;
 __device__ __forceinline__ unsigned pair_h12(unsigned x, unsigned y) {
     return ((x * 0x9E3779B1u) ^ (y * 0x85EBCA77u)) >> 20;
 }
@@ -1098,15 +1103,37 @@ struct TokMetaS {
 // member's own count, count(P_j) <= count(P_1), so `narrow` = count(P_1) < 2^32 holds for the
 // whole batch; otherwise every add goes to the global cells), the rest by global atomics.
 typedef __attribute__((address_space(3))) unsigned LdsU32;   // an LDS word (explicit address space)
+// Touched blocks (the apply visits only the cells that can hold a delta): a member's cells
+// from `mark_from` on (2 x the densely scanned token prefix, >= 2 N) are grouped in blocks of 64
+// cells (32 tokens); every global add there sets its block's bit in the workgroup's LDS bitmap
+// (word = cell >> 11), which the flush ORs into one of kTBRep global replicas per trip parity
+// (fewer same-address atomics); the apply ORs the replicas and lists the touched blocks.
+constexpr unsigned kTBRep = 4;      // global bitmap replicas (a workgroup ORs into blockIdx % kTBRep)
+constexpr unsigned kTBMax = 64;     // bitmap words per member: tokens up to 65 536 (else every cell scanned)
+constexpr unsigned kTLCap = 4096;   // touched blocks the apply lists in LDS (more: every cell scanned)
+struct CellMarks {
+    unsigned* tb;        // [parity][kTBRep][kMaxBatch][tbw] touched-block bitmaps written by the merge
+    unsigned* tbc;       // [kMaxBatch][tbw]: the last apply's OR of its replicas (the next merge clears by it)
+    unsigned tbw;        // bitmap words per member (0: no marks, every cell scanned and cleared)
+    unsigned dense_tok;  // tokens below this are scanned densely for every member (a multiple of 32)
+    unsigned long long* sig;   // BPE355_CHECK_MARKS: each apply workgroup's view of the list (else null)
+};
 template <unsigned N>
 struct DeltaSinkN {
     unsigned long long* LR;     // this member's global cells
     LdsU32* lds;                // this member's LDS cells (ids below N)
+    LdsU32* bm;                 // this member's touched-block bitmap (LDS)
+    unsigned mark_from;         // cells from here on are marked (~0u: none)
     bool narrow;
     __device__ __forceinline__ void add(unsigned cell, unsigned long long c) const {
-        if (narrow && cell < 2 * N)
+        if (narrow && cell < 2 * N) {
             __hip_atomic_fetch_add(&lds[cell], (unsigned)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        else atomicAdd(&LR[cell], c);
+        } else {
+            atomicAdd(&LR[cell], c);
+            if (cell >= mark_from)
+                __hip_atomic_fetch_or(&bm[cell >> 11], 1u << ((cell >> 6) & 31), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
     }
 };
 
@@ -1715,6 +1742,45 @@ __global__ void __launch_bounds__(kSelThreads) k_select(const RoundState* __rest
     select_core<kSelThreads>(st, bs, K, X, part, lists, *bt, S, O, true);
 }
 
+// Test knob BPE355_CHECK_MARKS: after a trip's merge, the other parity (cleared by it from the
+// dense prefix and the previous apply's touched-block list) must be zero in every cell and bitmap:
+// a nonzero cell there is a delta the marks missed.  dbg[0] counts them, dbg[1..3] the first one
+// (trip, member, cell).
+__global__ void k_check_clear(const Batch* __restrict__ bt, const unsigned long long* __restrict__ LRbase,
+                              size_t lr_member, size_t lr_parity, const unsigned* __restrict__ tb, unsigned tbw,
+                              unsigned long long* __restrict__ dbg) {
+    const Batch& B = *bt;
+    if (B.stop) return;
+    const unsigned long long* LRo = LRbase + (size_t)((B.trip + 1) & 1) * lr_parity;
+    const size_t n = (size_t)kMaxBatch * lr_member;
+    for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (size_t)gridDim.x * blockDim.x)
+        if (LRo[q] != 0 && atomicAdd(&dbg[0], 1ull) == 0) {
+            dbg[1] = (unsigned long long)B.trip;
+            dbg[2] = q / lr_member;
+            dbg[3] = q % lr_member;
+        }
+    if (tbw) {
+        const unsigned* TBo = tb + (size_t)((B.trip + 1) & 1) * kTBRep * kMaxBatch * tbw;
+        for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < (size_t)kTBRep * kMaxBatch * tbw;
+             q += (size_t)gridDim.x * blockDim.x)
+            if (TBo[q]) atomicAdd(&dbg[4], 1ull);
+    }
+}
+
+// BPE355_CHECK_MARKS after an apply: every workgroup must have seen the same touched blocks
+__global__ void k_check_sig(const Batch* __restrict__ bt, unsigned long long* __restrict__ sig, unsigned n,
+                            unsigned long long* __restrict__ dbg) {
+    const Batch& B = *bt;
+    for (unsigned i = threadIdx.x; i < n; i += blockDim.x) {
+        if (!B.stop && sig[1 + i] != sig[1] && atomicAdd(&dbg[5], 1ull) == 0) {
+            dbg[6] = (unsigned long long)B.trip;
+            dbg[7] = i;
+        }
+    }
+    __syncthreads();
+    for (unsigned i = threadIdx.x; i < n; i += blockDim.x) sig[1 + i] = 0;
+}
+
 // end of a block of trips: the state and the trips' records -> pinned host memory (plain vector
 // stores; the block's event orders them before the host reads)
 __global__ void __launch_bounds__(256) k_snapshot(const uint32_t* __restrict__ st, unsigned n_st,
@@ -1733,14 +1799,19 @@ __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigne
                                                  unsigned long long* LRt, size_t lr_member,
                                                  unsigned* lds, bool narrow, const LdsU32* sm_a,
                                                  const LdsU32* sm_b, const LdsU32* sm_n, const LdsU8* pm, bool use_pm,
-                                                 unsigned& singles, uint32_t* tags = nullptr, unsigned f = 0) {
+                                                 unsigned& singles, LdsU32* bm, unsigned tbw, unsigned mark_from,
+                                                 uint32_t* tags = nullptr, unsigned f = 0) {
     constexpr int W = slot_w(C);
     constexpr int V = W * (int)sizeof(TokT) / 16;
     TokT* s = S.slot + (size_t)i * W;
     uint4 r[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) r[v] = reinterpret_cast<const uint4*>(s)[v];
-    const unsigned long long c = S.cnt[i];   // issued with the slot
+    // the count: issued with the slot in a full scan (most words hit early); in list mode, where
+    // most entries miss, only on a hit, beside the claim (one random line less per missing entry,
+    // and the claim's round trip covers the load)
+    unsigned long long c = 0;
+    if (!(kLateCount && tags)) c = S.cnt[i];
     TokT e[W];
     __builtin_memcpy(e, r, sizeof(e));
     // the members this word holds: no member's b is another's a and the new tokens are fresh, so
@@ -1783,10 +1854,13 @@ __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigne
     // claimed only on a hit (most list entries miss: no atomic for them).  A word rewritten under
     // another thread's claim was loaded after that claim, so its copy here, torn or not, ends in a
     // failed claim or in no hit: only the claimant ever writes it.
-    if (!hits || (tags && atomicMax(&tags[f], B.batch_id) >= B.batch_id)) return;
+    if (!hits) return;
+    if (kLateCount && tags) c = S.cnt[i];
+    if (tags && atomicMax(&tags[f], B.batch_id) >= B.batch_id) return;
     if (kRegRewrite && W <= kRegRewriteMaxW) {   // every member in registers, one compacting store
         const auto sink_of = [&](int j) {
-            return DeltaSinkN<kLdsB>{LRt + (size_t)j * lr_member, (LdsU32*)(lds + 2 * kLdsB * j), narrow};
+            return DeltaSinkN<kLdsB>{LRt + (size_t)j * lr_member, (LdsU32*)(lds + 2 * kLdsB * j), bm + j * tbw,
+                                     mark_from, narrow};
         };
         const uint32_t nl = rewrite_slot_members(e, s, hits, sm_a, sm_b, sm_n, c, sink_of);
         singles += nl < 2;
@@ -1802,7 +1876,8 @@ __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigne
             __builtin_memcpy(e, r, sizeof(e));
         }
         first = false;
-        const DeltaSinkN<kLdsB> D{LRt + (size_t)j * lr_member, (LdsU32*)(lds + 2 * kLdsB * j), narrow};
+        const DeltaSinkN<kLdsB> D{LRt + (size_t)j * lr_member, (LdsU32*)(lds + 2 * kLdsB * j), bm + j * tbw,
+                                  mark_from, narrow};
         const uint32_t nl = rewrite_slot(e, s, (TokT)sm_a[j], (TokT)sm_b[j], (TokT)sm_n[j], c, D);
         if (nl < 2) { ++singles; break; }
     }
@@ -1814,8 +1889,9 @@ template <class TokT>
 __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Batch& B, PairsDev P, ToksDev K,
                                            WordsDev<TokT> W, IndexDev X, unsigned long long* __restrict__ LRbase,
                                            size_t lr_member, size_t lr_parity, uint32_t* __restrict__ tags,
-                                           unsigned* l_lr) {
+                                           const CellMarks CM, unsigned* l_lr) {
     __shared__ unsigned s_ma[kMaxBatch], s_mb[kMaxBatch], s_mn[kMaxBatch];   // the members' tokens
+    __shared__ unsigned s_bm[kMaxBatch * kTBMax];   // the members' touched-block bitmaps (CellMarks)
     __shared__ unsigned s_pre[kMaxBatch + 1], s_lbeg[kMaxBatch];   // list prefix sums, list starts
     __shared__ unsigned s_pm[kPairSlots / 4];   // the batch's pair table (bytes; kPairFilterK)
     const int tid = threadIdx.x;
@@ -1829,15 +1905,36 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
     if (tid < kMaxBatch) { ma = B.m[tid].a; mb = B.m[tid].b; mn = B.m[tid].nw; mlb = B.m[tid].list_beg; }
     if (tid <= kMaxBatch) mpre = B.list_pre[tid];
     if (stop) return;
+    const unsigned tbw = CM.tbw;
+    const unsigned mark_from = tbw ? 2 * CM.dense_tok : ~0u;
     // the previous trip's cells (the other parity, read by its apply) are cleared here, spread
     // over the whole grid: workgroups without words do their share at once, the others after
-    // their flush, so the stores never wait in front of a rewrite's loads
+    // their flush, so the stores never wait in front of a rewrite's loads.  With marks: the dense
+    // token prefix, the blocks the previous apply listed (CM.tbc), and that parity's bitmaps
     auto clear_prev = [&]() {
         unsigned long long* LRo = LRbase + (size_t)((b_trip + 1) & 1) * lr_parity;
-        const unsigned nprev = 2 * (unsigned)b_ntok;
-        const unsigned S = gridDim.x * blockDim.x;
-        for (unsigned q = blockIdx.x * blockDim.x + tid; q < (unsigned)b_prev_k * nprev; q += S)
-            st_merge(&LRo[(size_t)(q / nprev) * lr_member + q % nprev], 0ull);
+        const unsigned S = gridDim.x * blockDim.x, g = blockIdx.x * blockDim.x + tid;
+        const unsigned pk = (unsigned)b_prev_k;
+        if (!tbw) {
+            const unsigned nprev = 2 * (unsigned)b_ntok;
+            for (unsigned q = g; q < pk * nprev; q += S)
+                st_merge(&LRo[(size_t)(q / nprev) * lr_member + q % nprev], 0ull);
+            return;
+        }
+        const unsigned nd2 = min(CM.dense_tok, (unsigned)b_ntok);   // 16-byte cell pairs per member
+        for (unsigned q = g; q < pk * nd2; q += S)
+            st_merge(reinterpret_cast<uint4*>(&LRo[(size_t)(q / nd2) * lr_member + 2 * (q % nd2)]), make_uint4(0, 0, 0, 0));
+        const unsigned nbk = 32 * tbw;   // blocks per member
+        for (unsigned q = g; q < pk * nbk; q += S) {
+            const unsigned j = q / nbk, blk = q % nbk;
+            if ((CM.tbc[j * tbw + (blk >> 5)] >> (blk & 31)) & 1u) {
+                uint4* c = reinterpret_cast<uint4*>(&LRo[(size_t)j * lr_member + 64 * (size_t)blk]);
+#pragma unroll 8
+                for (int u = 0; u < 32; ++u) st_merge(&c[u], make_uint4(0, 0, 0, 0));
+            }
+        }
+        unsigned* TBo = CM.tb + (size_t)((b_trip + 1) & 1) * kTBRep * kMaxBatch * tbw;
+        for (unsigned q = g; q < kTBRep * kMaxBatch * tbw; q += S) TBo[q] = 0u;
     };
     // Member j's pop and new-token registration (nothing in this launch reads them: the apply
     // and the next trip do) go to the first k workgroups without words when there are enough of
@@ -1886,6 +1983,8 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
     if (tid <= k) s_pre[tid] = mpre;
     if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 5);
     for (unsigned q = tid; q < 2 * kLdsB * (unsigned)k; q += blockDim.x) l_lr[q] = 0;
+    for (unsigned q = tid; q < tbw * (unsigned)k; q += blockDim.x) s_bm[q] = 0;
+    LdsU32* lbm = (LdsU32*)s_bm;
     unsigned long long* LRt = LRbase + (size_t)(B.trip & 1) * lr_parity;   // member j at + j * lr_member
     const bool use_pm = kPairFilterK > 0 && k >= kPairFilterK;   // (uniform)
     if (use_pm)
@@ -1918,7 +2017,7 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
         // one member: the per-round rewrite (index list or a scan of every slot)
         const BatchMember& M = B.m[0];
         const TokT ta = (TokT)M.a, tb = (TokT)M.b, tn = (TokT)M.nw;
-        const DeltaSinkN<kLdsB> D{LRt, (LdsU32*)l_lr, narrow};
+        const DeltaSinkN<kLdsB> D{LRt, (LdsU32*)l_lr, lbm, mark_from, narrow};
         if (M.use_list && bid < nb) {
             const uint32_t* L = X.list + M.list_beg;
             for (unsigned i = bid * blockDim.x + tid; i < M.list_len; i += nb * blockDim.x) {
@@ -1947,10 +2046,10 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
         if (B.full_scan) {
             const unsigned total = W.off[kNumCls];
             for (unsigned f = bid * blockDim.x + tid; f < total; f += nb * blockDim.x) {
-                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f,  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles);
-                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1],  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles);
-                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2],  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles);
-                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3],  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles);
+                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f,  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, lbm, tbw, mark_from);
+                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1],  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, lbm, tbw, mark_from);
+                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2],  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, lbm, tbw, mark_from);
+                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3],  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, lbm, tbw, mark_from);
             }
         } else {
             const unsigned total = B.list_pre[k];
@@ -1962,10 +2061,10 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
                     if (j + step < k && i >= s_pre[j + step]) j += step;
                 const unsigned f = X.list[s_lbeg[j] + (i - s_pre[j])];
                 // a word on several members' lists is rewritten by the first thread to claim it
-                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f,  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, tags, f);
-                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1],  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, tags, f);
-                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2],  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, tags, f);
-                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3],  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, tags, f);
+                if (f < W.off[1]) merge_word_batch<TokT, 0>(W.c[0], f,  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, lbm, tbw, mark_from, tags, f);
+                else if (f < W.off[2]) merge_word_batch<TokT, 1>(W.c[1], f - W.off[1],  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, lbm, tbw, mark_from, tags, f);
+                else if (f < W.off[3]) merge_word_batch<TokT, 2>(W.c[2], f - W.off[2],  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, lbm, tbw, mark_from, tags, f);
+                else merge_word_batch<TokT, 3>(W.c[3], f - W.off[3],  B, LRt, lr_member, l_lr, narrow, (const LdsU32*)s_ma, (const LdsU32*)s_mb, (const LdsU32*)s_mn, pmp, use_pm, singles, lbm, tbw, mark_from, tags, f);
             }
         }
     }
@@ -1979,7 +2078,8 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
                 bool hit = false;
                 for (uint32_t q = 0; q + 1 < len && !hit; ++q) hit = (t[q] == ta) & (t[q + 1] == tb);
                 if (!hit) continue;
-                const DeltaSinkN<kLdsB> D{LRt + (size_t)j * lr_member, (LdsU32*)(l_lr + 2 * kLdsB * j), narrow};
+                const DeltaSinkN<kLdsB> D{LRt + (size_t)j * lr_member, (LdsU32*)(l_lr + 2 * kLdsB * j), lbm + j * tbw,
+                                          mark_from, narrow};
                 len = rewrite_word(t, len, ta, tb, (TokT)B.m[j].nw, W.lcnt[i], D, false);
                 W.llen[i] = len;
                 singles += (len < 2);
@@ -1994,6 +2094,13 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
     for (unsigned q = tid; q < 2 * kLdsB * (unsigned)k; q += blockDim.x) {
         const unsigned v = l_lr[q];
         if (v) atomicAdd(&LRt[(size_t)(q / (2 * kLdsB)) * lr_member + q % (2 * kLdsB)], (unsigned long long)v);
+    }
+    if (tbw) {   // the touched blocks, into this workgroup's replica of this parity's bitmaps
+        unsigned* TBt = CM.tb + ((size_t)(B.trip & 1) * kTBRep + blockIdx.x % kTBRep) * kMaxBatch * tbw;
+        for (unsigned q = tid; q < tbw * (unsigned)k; q += blockDim.x) {
+            const unsigned v = s_bm[q];
+            if (v) atomicOr(&TBt[q], v);
+        }
     }
     if (blockIdx.x == 0 && tid == 0) probe_stamp(st, B.trip, 8);
     clear_prev();
@@ -2012,9 +2119,9 @@ template <class TokT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof(TokT) == 2 ? BPE355_MERGE_WAVES : 2))) k_merge_batch(RoundState* __restrict__ st, const Batch* __restrict__ bt,
                                                      PairsDev P, ToksDev K, WordsDev<TokT> W, IndexDev X,
                                                      unsigned long long* __restrict__ LRbase, size_t lr_member,
-                                                     size_t lr_parity, uint32_t* __restrict__ tags) {
+                                                     size_t lr_parity, uint32_t* __restrict__ tags, CellMarks CM) {
     __shared__ unsigned l_lr[2 * kLdsB * kMaxBatch];
-    merge_body<TokT>(st, *bt, P, K, W, X, LRbase, lr_member, lr_parity, tags, l_lr);
+    merge_body<TokT>(st, *bt, P, K, W, X, LRbase, lr_member, lr_parity, tags, CM, l_lr);
 }
 
 // One trip's select and merge in ONE launch.  Every workgroup decides the
@@ -2032,7 +2139,7 @@ __global__ void __launch_bounds__(kTripThreads) k_trip(RoundState* __restrict__ 
                                               Batch* __restrict__ bt, const Partial* __restrict__ part,
                                               const Partial* __restrict__ lists, SelOut O,
                                               unsigned long long* __restrict__ LRbase, size_t lr_member,
-                                              size_t lr_parity, uint32_t* __restrict__ tags) {
+                                              size_t lr_parity, uint32_t* __restrict__ tags, CellMarks CM) {
     __shared__ union TripLds {
         SelLds sel;
         unsigned lr[2 * kLdsB * kMaxBatch];
@@ -2047,7 +2154,7 @@ __global__ void __launch_bounds__(kTripThreads) k_trip(RoundState* __restrict__ 
         for (unsigned i = threadIdx.x; i < (unsigned)(sizeof(Batch) / 4); i += blockDim.x) dst[i] = src[i];
     }
     if (s_b.stop) return;
-    merge_body<TokT>(st, s_b, P, K, W, X, LRbase, lr_member, lr_parity, tags, u.lr);
+    merge_body<TokT>(st, s_b, P, K, W, X, LRbase, lr_member, lr_parity, tags, CM, u.lr);
 }
 
 // Apply the trip's deltas and list the next trip's candidates.  Items:
@@ -2077,8 +2184,12 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
                                                                     unsigned long long* __restrict__ LRbase,
                                                                     size_t lr_member, size_t lr_parity, unsigned ntb,
                                                                     Partial* __restrict__ part,
-                                                                    Partial* __restrict__ list, int scan_only) {
+                                                                    Partial* __restrict__ list, int scan_only,
+                                                                    CellMarks CM) {
     __shared__ unsigned s_tok[3 * kMaxBatch];
+    __shared__ unsigned s_tw[kMaxBatch * kTBMax];   // touched-block bitmaps (the replicas' OR)
+    __shared__ unsigned short s_tl[kTLCap];         // touched blocks past the dense prefix: j << 11 | block
+    __shared__ unsigned s_wsum[kApplyBatchThreads / 64];
     __shared__ unsigned s_role[3 * kMaxBatch];   // S entry: members' mask << 3 | role (1 a, 2 b, 4 new)
     __shared__ unsigned s_grp[2 * kMaxBatch];    // member j's a group (2j) and b group (2j + 1)
     __shared__ unsigned s_filt[kSFilterWords];   // bit (x mod 4096): x may be in S
@@ -2113,6 +2224,26 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     const int k = scan_only ? 0 : b_k;
     const bool pw0 = !scan_only && blockIdx.x == 0 && tid == 0;
     if (pw0) probe_stamp(st, b_trip, 9);
+    // touched blocks (CellMarks): the members' bitmaps, OR of the replicas, kTBW words per thread
+    // (issued before the S deduplication; used after its barrier)
+    constexpr unsigned kTBW = kMaxBatch * kTBMax / kApplyBatchThreads;
+    static_assert(kTBW * kApplyBatchThreads == kMaxBatch * kTBMax, "bitmap words per thread");
+    const unsigned tbw = CM.tbw;
+    const unsigned ntb_all = scan_only ? ntb : min(ntb, (unsigned)b_ntok + b_fresh);
+    const bool sparse = !scan_only && tbw != 0 && ntb_all > CM.dense_tok;   // (uniform)
+    unsigned tw[kTBW];
+    if (sparse) {
+        const unsigned* TBp = CM.tb + (size_t)(b_trip & 1) * kTBRep * kMaxBatch * tbw;
+#pragma unroll
+        for (unsigned u = 0; u < kTBW; ++u) {
+            const unsigned q = tid * kTBW + u;
+            unsigned v = 0;
+            if (q < (unsigned)k * tbw)
+#pragma unroll
+                for (unsigned r = 0; r < kTBRep; ++r) v |= TBp[(size_t)r * kMaxBatch * tbw + q];
+            tw[u] = v;
+        }
+    }
     if (tid < 64) {   // wave 0: S deduplicated (a == b is possible only when k == 1), lane i = entry i
         static_assert(3 * kMaxBatch <= 64, "S fits one wave");
         const int i = tid;
@@ -2149,9 +2280,109 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     __syncthreads();
     const int ns = s_ns;
     const unsigned long long* LRc = LRbase + (size_t)(b_trip & 1) * lr_parity;
-    if (!scan_only) ntb = min(ntb, (unsigned)b_ntok + b_fresh);   // token ids after this trip
+    ntb = ntb_all;   // token ids after this trip
     const unsigned per_member = 4 * ntb;
-    const unsigned n_cell = (unsigned)k * per_member;
+    // the cell items: every (member, token, op) densely, or (sparse) the dense token prefix of every
+    // member plus the touched blocks past it, 128 items (32 tokens x 4 ops) per block
+    const unsigned nD = CM.dense_tok / 32;   // dense-prefix blocks per member
+    unsigned n_cell = (unsigned)k * per_member;
+    bool listed = false;
+    if (sparse) {
+        // a token group's first member updates (x, a) / (b, y) for the whole group from the
+        // group's summed cells: its blocks must cover every group member's
+#pragma unroll
+        for (unsigned u = 0; u < kTBW; ++u) {
+            const unsigned q = tid * kTBW + u;
+            if (q < (unsigned)k * tbw) s_tw[q] = tw[u];
+        }
+        __syncthreads();
+        // (from the members' own bitmaps only: every workgroup must list exactly the same blocks,
+        // since the items are numbered across the grid -- a leader that is itself in another
+        // leader's group must not pass on bits in an order that depends on timing)
+        unsigned c = 0;
+#pragma unroll
+        for (unsigned u = 0; u < kTBW; ++u) {
+            const unsigned q = tid * kTBW + u;
+            if (q >= (unsigned)k * tbw) continue;
+            const unsigned j = q / tbw, w = q % tbw;
+            unsigned gm = (s_grp[2 * j] | s_grp[2 * j + 1]) & ~(1u << j);
+            while (gm) {
+                const unsigned m = (unsigned)__builtin_ctz(gm);
+                gm &= gm - 1;
+                tw[u] |= s_tw[m * tbw + w];
+            }
+            c += __popc(tw[u]);
+        }
+        // exclusive scan of the counts over the workgroup
+        unsigned inc = c;
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned t = __shfl_up(inc, d);
+            if ((tid & 63) >= d) inc += t;
+        }
+        if ((tid & 63) == 63) s_wsum[tid >> 6] = inc;
+        __syncthreads();
+        unsigned base = 0, T = 0;
+        for (int w = 0; w < (int)(kApplyBatchThreads / 64); ++w) {
+            const unsigned ws = s_wsum[w];
+            base += w < (tid >> 6) ? ws : 0u;
+            T += ws;
+        }
+        base += inc - c;
+        if (T <= kTLCap) {
+            listed = true;
+#pragma unroll
+            for (unsigned u = 0; u < kTBW; ++u) {
+                unsigned v = tw[u];
+                const unsigned q = tid * kTBW + u;
+                while (v) {
+                    const unsigned bit = (unsigned)__builtin_ctz(v);
+                    v &= v - 1;
+                    s_tl[base++] = (unsigned short)((q / tbw) << 11 | ((q % tbw) * 32 + bit));
+                }
+            }
+            n_cell = ((unsigned)k * nD + T) * 128;
+        }
+        if (CM.sig) {   // (test knob) this workgroup's view: T and a hash of its bitmaps
+            unsigned long long hsh = 0;
+#pragma unroll
+            for (unsigned u = 0; u < kTBW; ++u) hsh += (unsigned long long)tw[u] * (0x9E3779B97F4A7C15ull * (tid * kTBW + u + 1));
+            for (int o = 32; o > 0; o >>= 1) hsh += __shfl_xor(hsh, o);
+            if ((tid & 63) == 0) atomicAdd(&CM.sig[1 + blockIdx.x], hsh + ((unsigned long long)T << 48));
+        }
+        if (blockIdx.x == 0)   // for the next merge's clear
+#pragma unroll
+            for (unsigned u = 0; u < kTBW; ++u) {
+                const unsigned q = tid * kTBW + u;
+                if (q < (unsigned)k * tbw) CM.tbc[q] = tw[u];
+            }
+        __syncthreads();
+    } else if (!scan_only && tbw != 0 && blockIdx.x == 0) {
+        // nothing past the dense prefix can be marked yet: the next merge clears no block
+        for (unsigned q = tid; q < (unsigned)k * tbw; q += blockDim.x) CM.tbc[q] = 0u;
+    }
+    // cell item v -> member j, token x, op (false: no such cell)
+    auto cell_of = [&](unsigned v, unsigned& j, unsigned& x, unsigned& op) -> bool {
+        if (!listed) {
+            j = v / per_member;
+            const unsigned r = v % per_member;
+            x = r >> 2;
+            op = r & 3;
+            return true;
+        }
+        const unsigned slot = v >> 7, r = v & 127;
+        unsigned blk;
+        if (slot < (unsigned)k * nD) {
+            j = slot / nD;
+            blk = slot % nD;
+        } else {
+            const unsigned e = s_tl[slot - (unsigned)k * nD];
+            j = e >> 11;
+            blk = e & 2047u;
+        }
+        x = blk * 32 + (r >> 2);
+        op = r & 3;
+        return x < ntb;
+    };
     const unsigned n_sp = (unsigned)(ns * ns);
     const unsigned nC0 = scan_only ? st_nC : b_nC;
     const unsigned n_items = n_cell + n_sp + nC0;
@@ -2233,8 +2464,9 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
             dv[u] = 0;
             dw[u] = 0;
             ce[u] = make_uint4(0, 0, 0, 0);
+            unsigned j, x, op;
             if (v < n_cell) {
-                const unsigned j = v / per_member, r = v % per_member, x = r >> 2, op = r & 3;
+                if (!cell_of(v, j, x, op)) continue;
                 const size_t ci = 2 * (size_t)x + (op >> 1);
                 dv[u] = LRc[(size_t)j * lr_member + ci];
                 if (kShareTok && !(op & 1)) {   // (x, a_j) or (b_j, x): one updater per token group
@@ -2262,9 +2494,9 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
             const unsigned v = item(base + u * S + g);
             how[u] = 0; ip[u] = 0; iq[u] = 0; delta[u] = 0; touched[u] = false;
             hk[u] = 0; hc[u] = 0; hf[u] = 0; kp[u] = 0; kq[u] = 0;
+            unsigned j, x, op;
             if (v < n_cell) {
-                const unsigned j = v / per_member, r = v % per_member, x = r >> 2, op = r & 3;
-                const long long d = (long long)dv[u];
+                const long long d = cell_of(v, j, x, op) ? (long long)dv[u] : 0ll;
                 if (d && !in_S(x)) {
                     const BatchMember& M = B.m[j];
                     ip[u] = op <= 1 ? x : (op == 2 ? M.b : M.nw);
@@ -2969,6 +3201,9 @@ class MergeLoop {
     DevBuf<uint4> C_;
     // tokens
     unsigned tok_cap_ = 0;
+    size_t lr_member_ = 0;        // cells per member: 2 x tok_cap_, rounded up to whole 64-cell blocks
+    DevBuf<unsigned> tb_, tbc_;   // touched-block bitmaps (CellMarks)
+    CellMarks cm_{};
     DevBuf<uint8_t> pool_;
     DevBuf<uint32_t> toff_, tlen_;
     DevBuf<unsigned long long> tmap_;
@@ -2984,6 +3219,7 @@ class MergeLoop {
     std::unique_ptr<std::vector<int>> trip_log_;   // analysis knob BPE355_TRIP_LOG=path: every trip's record
     DevBuf<BatchState> bs_;
     DevBuf<Batch> batch_;
+    DevBuf<unsigned long long> dbg_, sig_;   // BPE355_CHECK_MARKS
     DevBuf<uint32_t> tags_;      // per slot word: the last batch that claimed it
     DevBuf<int> trip_info_;      // per trip of a block: first round, members, scan mode, list entries (2 slots)
     RoundState* snap_st_ = nullptr;   // pinned: the state at the end of each in-flight block
@@ -3321,8 +3557,8 @@ int MergeLoop<TokT>::rebuild() {
     if (batched_) {   // the rebuilt C's best (partials) and candidate list
         BPE_HIP(hipMemsetAsync(&bs_.p->list_n[0], 0, sizeof(bs_.p->list_n), s_));
         hipLaunchKernelGGL(k_apply_batch, dim3(kApplyBatchBlocks), dim3(kApplyBatchThreads), 0, s_, st_.p, bs_.p,
-                           (const Batch*)batch_.p, pairs(), toks(), LR_.p, 2ull * tok_cap_,
-                           (size_t)kMaxBatch * 2ull * tok_cap_, tok_cap_, part_.p, list_.p, 1);
+                           (const Batch*)batch_.p, pairs(), toks(), LR_.p, lr_member_,
+                           (size_t)kMaxBatch * lr_member_, tok_cap_, part_.p, list_.p, 1, cm_);
     }
     else
         hipLaunchKernelGGL(k_argmax, dim3(kArgBlocks), dim3(256), 0, s_, st_.p, pairs(), toks(), part_.p);
@@ -3362,8 +3598,27 @@ void MergeLoop<TokT>::run() {
         batched_ = !sharded() && max_batch_ >= 1;
     }
     // cells: two buffers by round (trip) parity; batched: kMaxBatch members each
-    LR_.alloc(2 * (batched_ ? (size_t)kMaxBatch : 1) * 2ull * tok_cap_);
+    lr_member_ = (2ull * tok_cap_ + 63) / 64 * 64;
+    LR_.alloc(2 * (batched_ ? (size_t)kMaxBatch : 1) * lr_member_);
     BPE_HIP(hipMemsetAsync(LR_.p, 0, LR_.bytes(), s_));
+    if (batched_) {   // touched blocks: the apply visits the dense token prefix and the marked blocks
+        const unsigned dense_tok = [] {   // test knob BPE355_DENSE_TOK (>= 128, a multiple of 32; per call)
+            const char* e = std::getenv("BPE355_DENSE_TOK");
+            const unsigned v = e ? (unsigned)std::max(0, std::atoi(e)) : 2048u;
+            return std::max(128u, v / 32 * 32);
+        }();
+        const unsigned tbw = ceil_div(tok_cap_, 1024u);
+        const bool marks = tbw <= kTBMax && !(std::getenv("BPE355_CELL_MARKS") && std::getenv("BPE355_CELL_MARKS")[0] == '0');
+        cm_ = CellMarks{nullptr, nullptr, marks ? tbw : 0u, dense_tok};
+        if (marks) {
+            tb_.alloc(2ull * kTBRep * kMaxBatch * tbw);
+            tbc_.alloc((size_t)kMaxBatch * tbw);
+            BPE_HIP(hipMemsetAsync(tb_.p, 0, tb_.bytes(), s_));
+            BPE_HIP(hipMemsetAsync(tbc_.p, 0, tbc_.bytes(), s_));
+            cm_.tb = tb_.p;
+            cm_.tbc = tbc_.p;
+        }
+    }
     if (batched_) {
         bs_.alloc(1);
         BPE_HIP(hipMemsetAsync(bs_.p, 0, sizeof(BatchState), s_));
@@ -3383,6 +3638,13 @@ void MergeLoop<TokT>::run() {
         // select and merge of a trip in one launch (k_trip), or k_select + k_merge_batch
         const char* fe = std::getenv("BPE355_FOLD");
         fused_ = fe && fe[0] == '1';
+    }
+    if (batched_ && std::getenv("BPE355_CHECK_MARKS")) {
+        dbg_.alloc(8);
+        BPE_HIP(hipMemsetAsync(dbg_.p, 0, dbg_.bytes(), s_));
+        sig_.alloc(1 + kApplyBatchBlocks);
+        BPE_HIP(hipMemsetAsync(sig_.p, 0, sig_.bytes(), s_));
+        cm_.sig = sig_.p;
     }
     const char* trip_log_path = std::getenv("BPE355_TRIP_LOG");   // analysis knob: the trips' records
     if (batched_ && trip_log_path) trip_log_.reset(new std::vector<int>());
@@ -3620,6 +3882,14 @@ void MergeLoop<TokT>::run() {
             std::fclose(f);
         }
     }
+    if (dbg_.p) {
+        unsigned long long d[8];
+        BPE_HIP(hipMemcpy(d, dbg_.p, sizeof(d), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "[bpe355 check-marks] nonzero cells left after the clear: %llu (first: trip %llu member %llu "
+                             "cell %llu); bitmap words left: %llu; apply workgroups with another view: %llu (first: "
+                             "trip %llu workgroup %llu)\n", d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
+        BPE_REQUIRE(d[0] == 0 && d[4] == 0, BPE_E_HIP, "cell marks: a delta outside the marked blocks");
+    }
     if (trip_log_ && !trip_log_->empty()) {   // kTI ints per trip (k > 0: the trips that ran)
         if (FILE* f = std::fopen(trip_log_path, "wb")) {
             std::fwrite(trip_log_->data(), sizeof(int), trip_log_->size(), f);
@@ -3847,7 +4117,7 @@ unsigned MergeLoop<TokT>::merge_grid() const {
 
 template <class TokT>
 void MergeLoop<TokT>::launch_block(int slot, bool timing, std::vector<hipEvent_t>& ev) {
-    const size_t lr_member = 2ull * tok_cap_, lr_parity = (size_t)kMaxBatch * lr_member;
+    const size_t lr_member = lr_member_, lr_parity = (size_t)kMaxBatch * lr_member;
     const unsigned ntb = tok_cap_;
     const unsigned apply_blocks = kApplyBatchBlocks;
     int* ti = trip_info_.p + (size_t)slot * kTI * kTrips;
@@ -3860,18 +4130,24 @@ void MergeLoop<TokT>::launch_block(int slot, bool timing, std::vector<hipEvent_t
             hipExtLaunchKernelGGL(k_trip<TokT>, dim3(trip_grid_), dim3(kTripThreads), 0, s_,
                                   timed ? e[0] : nullptr, timed ? e[1] : nullptr, 0,
                                   st_.p, bs_.p, pairs(), toks(), wdev_trip_, idev_, batch_.p, (const Partial*)part_.p,
-                                  (const Partial*)list_.p, so, LR_.p, lr_member, lr_parity, tags_.p);
+                                  (const Partial*)list_.p, so, LR_.p, lr_member, lr_parity, tags_.p, cm_);
         } else {
             hipLaunchKernelGGL(k_select, dim3(1), dim3(kSelThreads), 0, s_, (const RoundState*)st_.p, bs_.p, toks(),
                                idev_, batch_.p, (const Partial*)part_.p, (const Partial*)list_.p, so);
             hipExtLaunchKernelGGL(k_merge_batch<TokT>, dim3(merge_grid()), dim3(256), 0, s_,
                                   timed ? e[0] : nullptr, timed ? e[1] : nullptr, 0,
                                   st_.p, (const Batch*)batch_.p, pairs(), toks(), wdev_, idev_, LR_.p, lr_member,
-                                  lr_parity, tags_.p);
+                                  lr_parity, tags_.p, cm_);
         }
+        if (dbg_.p)
+            hipLaunchKernelGGL(k_check_clear, dim3(256), dim3(256), 0, s_, (const Batch*)batch_.p, (const unsigned long long*)LR_.p,
+                               lr_member, lr_parity, (const unsigned*)cm_.tb, cm_.tbw, dbg_.p);
         hipLaunchKernelGGL(k_apply_batch, dim3(apply_blocks), dim3(kApplyBatchThreads), 0, s_, st_.p, bs_.p,
                            (const Batch*)batch_.p, pairs(), toks(), LR_.p, lr_member, lr_parity, ntb, part_.p,
-                           list_.p, 0);
+                           list_.p, 0, cm_);
+        if (sig_.p)
+            hipLaunchKernelGGL(k_check_sig, dim3(1), dim3(256), 0, s_, (const Batch*)batch_.p, sig_.p,
+                               (unsigned)kApplyBatchBlocks, dbg_.p);
     }
     static_assert(sizeof(RoundState) % 4 == 0, "k_snapshot copies words");
     // the block's snapshot: one small kernel stores the state and the trip records into pinned
