@@ -95,7 +95,7 @@ def test_train_matches_oracle_tie_heavy(seed):
 
 
 @pytest.mark.parametrize("knob", ["BPE355_FOLD=1", "BPE355_LDS_CELLS=0",
-                                  "BPE355_DENSE_TOK=128+BPE355_CHECK_MARKS=1", "BPE355_CELL_MARKS=0"])
+                                  "BPE355_DENSE_TOK=128+BPE355_SPARSE_FROM=128+BPE355_CHECK_MARKS=1", "BPE355_CELL_MARKS=0"])
 def test_train_runtime_variants(knob, monkeypatch):
     """The merge loop's run-time variants against the same goldens: the fused trip
     kernel k_trip (BPE355_FOLD=1: every workgroup decides the batch again while others already

@@ -111,6 +111,14 @@ for step in "$@"; do
   trace|trace_host)   # the host's halts and clock (BPE355_TRACE) of the HBM-resident training
     BPE355_TRACE=1 timeout -k 10 200 python -u bench.py --no-file --steps 1 --warmup 0 --no-encode --no-cpu-baseline --no-timing --keep-corpus > $OUT/trace_host.log 2> $OUT/trace_host_err.log || { echo "trace failed"; tail -5 $OUT/trace_host_err.log; exit 1; }
     grep -E "host clock|trips:|batch ended" $OUT/trace_host_err.log; grep -c "halt" $OUT/trace_host_err.log ;;
+  abenvs:*)   # merge phase under env settings (abenvs:default,A=1,B=2+C=3), corpus in HBM, alternating, 2 reps
+    SPECS=${step#abenvs:}; SPECS=${SPECS//,/ }
+    for rep in 1 2; do for sp in $SPECS; do
+      if [ "$sp" = default ]; then ENVS=""; else ENVS=${sp//+/ }; fi
+      tag=${sp//[=+]/_}
+      env $ENVS timeout -k 10 300 python -u bench.py --no-file --no-encode --no-cpu-baseline --steps 3 --warmup 1 > $OUT/abe_${tag}_$rep.log 2>&1 || { echo "abenvs failed"; tail -20 $OUT/abe_${tag}_$rep.log; exit 1; }
+      python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().split(chr(10))[-1]); m=d['merge_loop']; print('$sp rep $rep merge_ms', m['ms'], 'us_per_trip', m['us_per_trip'], 'k_us', m['k_merge_batch_us'], 'trips', m['trips'], 'parity', d['parity']['parity'])" $OUT/abe_${tag}_$rep.log
+    done; done ;;
   c4)
     BPE355_STATS_OUT=$OUT/c4_exchange.json timeout -k 10 600 python -u -m pytest tests/test_gpu_c4.py -x -q --timeout 380 --timeout-method thread -k "words_full or rounds" > $OUT/c4.log 2>&1 || { echo "c4 failed"; tail -20 $OUT/c4.log; exit 1; }
     cat $OUT/c4_exchange*.json ;;

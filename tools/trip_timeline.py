@@ -41,7 +41,7 @@ def main():
         raw = np.fromfile(sys.argv[3], dtype=np.int32).reshape(-1, 8)
         log = raw[raw[:, 1] > 0]
     T = trainings[pick]
-    ran = [t for t in T if t["merge"] > 6.0]   # a trip queued behind a halt: every kernel returns at once (~4.8 us each under the tracer)
+    ran = [t for t in T if t["merge"] > 6.0 and t["apply"] > 6.0]   # a trip queued behind a halt: every kernel returns at once (~5-6 us each under the tracer)
     halted = len(T) - len(ran)
     keys = ["g_sel", "sel", "g_merge", "merge", "g_apply", "apply"]
     A = np.array([[t[k] for k in keys] for t in ran])

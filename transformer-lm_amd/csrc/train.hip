@@ -1043,6 +1043,7 @@ struct Batch {
     int k;               // members
     int round, ntok;     // round of member 0, token count before the batch
     int trip, prev_k;    // trip number (cell parity), members of the previous trip
+    int prev_sparse;     // the previous trip's apply listed touched blocks (its merge clears by them)
     unsigned batch_id;   // word claims of this batch
     unsigned full_scan;  // a member has no usable posting list: scan every word once
     unsigned n_fresh;    // members that create a token
@@ -1062,6 +1063,7 @@ struct BatchState {
     unsigned batch_seq;      // last batch_id handed out
     int trip;                // trips completed
     int prev_k;              // members of the last trip (its cells are cleared by the next apply)
+    int prev_sparse;         // the last trip's apply listed touched blocks (CellMarks)
     unsigned long long rounds_batched;   // statistics: rounds taken in batches of k > 1
     unsigned long long trips_batched;
     long long T2;            // candidate-list threshold (>= T): every present key >= T2 is listed
@@ -1108,7 +1110,7 @@ typedef __attribute__((address_space(3))) unsigned LdsU32;   // an LDS word (exp
 // cells (32 tokens); every global add there sets its block's bit in the workgroup's LDS bitmap
 // (word = cell >> 11), which the flush ORs into one of kTBRep global replicas per trip parity
 // (fewer same-address atomics); the apply ORs the replicas and lists the touched blocks.
-constexpr unsigned kTBRep = 4;      // global bitmap replicas (a workgroup ORs into blockIdx % kTBRep)
+constexpr unsigned kTBRep = 2;      // global bitmap replicas (a workgroup ORs into blockIdx % kTBRep)
 constexpr unsigned kTBMax = 64;     // bitmap words per member: tokens up to 65 536 (else every cell scanned)
 constexpr unsigned kTLCap = 4096;   // touched blocks the apply lists in LDS (more: every cell scanned)
 struct CellMarks {
@@ -1116,6 +1118,7 @@ struct CellMarks {
     unsigned* tbc;       // [kMaxBatch][tbw]: the last apply's OR of its replicas (the next merge clears by it)
     unsigned tbw;        // bitmap words per member (0: no marks, every cell scanned and cleared)
     unsigned dense_tok;  // tokens below this are scanned densely for every member (a multiple of 32)
+    unsigned sparse_from;   // an apply lists touched blocks once the tokens pass this (below: every cell)
     unsigned long long* sig;   // BPE355_CHECK_MARKS: each apply workgroup's view of the list (else null)
 };
 template <unsigned N>
@@ -1342,7 +1345,7 @@ __device__ __forceinline__ void select_core(const RoundState* __restrict__ st, B
     const unsigned pool_used = st->pool_used, pool_cap = st->pool_cap;
     const unsigned max_len = st->max_len;
     const int ntok = st->ntok, max_batch = st->max_batch;
-    const int prev_k = bs->prev_k;
+    const int prev_k = bs->prev_k, prev_sparse = bs->prev_sparse;
     const unsigned bid = bs->batch_seq + 1;
     const long long T2old = bs->T2;
     if (pub && tid == 0) probe_stamp(st, ptrip, 1);
@@ -1692,6 +1695,7 @@ __device__ __forceinline__ void select_core(const RoundState* __restrict__ st, B
         OB.ntok = ntok;
         OB.trip = ptrip;
         OB.prev_k = prev_k;
+        OB.prev_sparse = prev_sparse;
         OB.batch_id = bid;
         OB.nC_base = nC;
         OB.full_scan = full;
@@ -1896,7 +1900,8 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
     __shared__ unsigned s_pm[kPairSlots / 4];   // the batch's pair table (bytes; kPairFilterK)
     const int tid = threadIdx.x;
     // every field the prologue needs in one round trip (none depends on another)
-    const int stop = B.stop, k = B.k, b_trip = B.trip, b_ntok = B.ntok, b_prev_k = B.prev_k;
+    const int stop = B.stop, k = B.k, b_trip = B.trip, b_ntok = B.ntok, b_prev_k = B.prev_k,
+              b_prev_sparse = B.prev_sparse;
     const unsigned idle_from = B.idle_from;
     // 32-bit LDS cells hold every member's sums (run-time test knob BPE355_LDS_CELLS=0: every cell
     // global, the path of a batch whose P1 count reaches 2^32)
@@ -1915,10 +1920,14 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
         unsigned long long* LRo = LRbase + (size_t)((b_trip + 1) & 1) * lr_parity;
         const unsigned S = gridDim.x * blockDim.x, g = blockIdx.x * blockDim.x + tid;
         const unsigned pk = (unsigned)b_prev_k;
-        if (!tbw) {
-            const unsigned nprev = 2 * (unsigned)b_ntok;
+        unsigned* TBo = CM.tb + (size_t)((b_trip + 1) & 1) * kTBRep * kMaxBatch * tbw;
+        if (tbw)   // that parity's bitmaps (the marks its merge made, whatever its apply did with them)
+            for (unsigned q = g; q < kTBRep * kMaxBatch * tbw; q += S) TBo[q] = 0u;
+        if (!tbw || !b_prev_sparse) {   // the previous apply scanned every cell: clear every cell
+            const unsigned nprev = (unsigned)b_ntok;   // 16-byte cell pairs per member
             for (unsigned q = g; q < pk * nprev; q += S)
-                st_merge(&LRo[(size_t)(q / nprev) * lr_member + q % nprev], 0ull);
+                st_merge(reinterpret_cast<uint4*>(&LRo[(size_t)(q / nprev) * lr_member + 2 * (q % nprev)]),
+                         make_uint4(0, 0, 0, 0));
             return;
         }
         const unsigned nd2 = min(CM.dense_tok, (unsigned)b_ntok);   // 16-byte cell pairs per member
@@ -1933,8 +1942,6 @@ __device__ __forceinline__ void merge_body(RoundState* __restrict__ st, const Ba
                 for (int u = 0; u < 32; ++u) st_merge(&c[u], make_uint4(0, 0, 0, 0));
             }
         }
-        unsigned* TBo = CM.tb + (size_t)((b_trip + 1) & 1) * kTBRep * kMaxBatch * tbw;
-        for (unsigned q = g; q < kTBRep * kMaxBatch * tbw; q += S) TBo[q] = 0u;
     };
     // Member j's pop and new-token registration (nothing in this launch reads them: the apply
     // and the next trip do) go to the first k workgroups without words when there are enough of
@@ -2185,7 +2192,7 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
                                                                     size_t lr_member, size_t lr_parity, unsigned ntb,
                                                                     Partial* __restrict__ part,
                                                                     Partial* __restrict__ list, int scan_only,
-                                                                    CellMarks CM) {
+                                                                    CellMarks CM, int sparse_hint) {
     __shared__ unsigned s_tok[3 * kMaxBatch];
     __shared__ unsigned s_tw[kMaxBatch * kTBMax];   // touched-block bitmaps (the replicas' OR)
     __shared__ unsigned short s_tl[kTLCap];         // touched blocks past the dense prefix: j << 11 | block
@@ -2212,6 +2219,25 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     const unsigned t_raw = tid < 3 * kMaxBatch ? reinterpret_cast<const unsigned*>(&B.m[tid / 3])[tid % 3] : ~0u;
     static_assert(offsetof(BatchMember, gb) == offsetof(BatchMember, ga) + 4, "ga, gb adjacent");
     const unsigned g_raw = tid < 3 * kMaxBatch && tid % 3 < 2 ? (&B.m[tid / 3].ga)[tid % 3] : 0u;
+    // touched-block bitmaps of both parities (CellMarks), issued with the batch record's loads
+    // rather than behind them (the parity is the batch's); kTBW words per thread
+    constexpr unsigned kTBW = (kMaxBatch * kTBMax + kApplyBatchThreads - 1) / kApplyBatchThreads;
+    unsigned t2[2][kTBW];
+    {
+        const bool want = sparse_hint && !scan_only && CM.tbw != 0;
+#pragma unroll
+        for (unsigned pty = 0; pty < 2; ++pty)
+#pragma unroll
+            for (unsigned u = 0; u < kTBW; ++u) {
+                const unsigned q = tid * kTBW + u;
+                unsigned v = 0;
+                if (want && q < kMaxBatch * CM.tbw)
+#pragma unroll
+                    for (unsigned r = 0; r < kTBRep; ++r)
+                        v |= CM.tb[((size_t)pty * kTBRep + r) * kMaxBatch * CM.tbw + q];
+                t2[pty][u] = v;
+            }
+    }
     if (!scan_only && b_stop) {   // no trip: part[] and the list keep what the next select reads
         if (b_stop > 0 && blockIdx.x == 0 && tid == 0) st->halt = b_stop;   // the select's halt
         return;
@@ -2224,26 +2250,15 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
     const int k = scan_only ? 0 : b_k;
     const bool pw0 = !scan_only && blockIdx.x == 0 && tid == 0;
     if (pw0) probe_stamp(st, b_trip, 9);
-    // touched blocks (CellMarks): the members' bitmaps, OR of the replicas, kTBW words per thread
-    // (issued before the S deduplication; used after its barrier)
-    constexpr unsigned kTBW = kMaxBatch * kTBMax / kApplyBatchThreads;
-    static_assert(kTBW * kApplyBatchThreads == kMaxBatch * kTBMax, "bitmap words per thread");
+    // touched blocks (CellMarks): listed from cm.sparse_from tokens on (below, the dense scan of
+    // every cell is cheaper than building the list)
     const unsigned tbw = CM.tbw;
     const unsigned ntb_all = scan_only ? ntb : min(ntb, (unsigned)b_ntok + b_fresh);
-    const bool sparse = !scan_only && tbw != 0 && ntb_all > CM.dense_tok;   // (uniform)
+    const bool sparse = sparse_hint && !scan_only && tbw != 0 && ntb_all > CM.sparse_from;   // (uniform)
     unsigned tw[kTBW];
-    if (sparse) {
-        const unsigned* TBp = CM.tb + (size_t)(b_trip & 1) * kTBRep * kMaxBatch * tbw;
 #pragma unroll
-        for (unsigned u = 0; u < kTBW; ++u) {
-            const unsigned q = tid * kTBW + u;
-            unsigned v = 0;
-            if (q < (unsigned)k * tbw)
-#pragma unroll
-                for (unsigned r = 0; r < kTBRep; ++r) v |= TBp[(size_t)r * kMaxBatch * tbw + q];
-            tw[u] = v;
-        }
-    }
+    for (unsigned u = 0; u < kTBW; ++u)
+        tw[u] = sparse && tid * kTBW + u < (unsigned)k * tbw ? t2[b_trip & 1][u] : 0u;
     if (tid < 64) {   // wave 0: S deduplicated (a == b is possible only when k == 1), lane i = entry i
         static_assert(3 * kMaxBatch <= 64, "S fits one wave");
         const int i = tid;
@@ -2356,9 +2371,6 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
                 if (q < (unsigned)k * tbw) CM.tbc[q] = tw[u];
             }
         __syncthreads();
-    } else if (!scan_only && tbw != 0 && blockIdx.x == 0) {
-        // nothing past the dense prefix can be marked yet: the next merge clears no block
-        for (unsigned q = tid; q < (unsigned)k * tbw; q += blockDim.x) CM.tbc[q] = 0u;
     }
     // cell item v -> member j, token x, op (false: no such cell)
     auto cell_of = [&](unsigned v, unsigned& j, unsigned& x, unsigned& op) -> bool {
@@ -2599,6 +2611,7 @@ __global__ void __launch_bounds__(kApplyBatchThreads) k_apply_batch(RoundState* 
             st->ntok = B.ntok + (int)B.n_fresh;
             bs->trip = B.trip + 1;
             bs->prev_k = k;
+            bs->prev_sparse = sparse;
             st->pool_used = B.pool_after;
             bs->batch_seq = B.batch_id;
             bs->T2 = b_T2;
@@ -3558,7 +3571,7 @@ int MergeLoop<TokT>::rebuild() {
         BPE_HIP(hipMemsetAsync(&bs_.p->list_n[0], 0, sizeof(bs_.p->list_n), s_));
         hipLaunchKernelGGL(k_apply_batch, dim3(kApplyBatchBlocks), dim3(kApplyBatchThreads), 0, s_, st_.p, bs_.p,
                            (const Batch*)batch_.p, pairs(), toks(), LR_.p, lr_member_,
-                           (size_t)kMaxBatch * lr_member_, tok_cap_, part_.p, list_.p, 1, cm_);
+                           (size_t)kMaxBatch * lr_member_, tok_cap_, part_.p, list_.p, 1, cm_, 0);
     }
     else
         hipLaunchKernelGGL(k_argmax, dim3(kArgBlocks), dim3(256), 0, s_, st_.p, pairs(), toks(), part_.p);
@@ -3609,7 +3622,15 @@ void MergeLoop<TokT>::run() {
         }();
         const unsigned tbw = ceil_div(tok_cap_, 1024u);
         const bool marks = tbw <= kTBMax && !(std::getenv("BPE355_CELL_MARKS") && std::getenv("BPE355_CELL_MARKS")[0] == '0');
-        cm_ = CellMarks{nullptr, nullptr, marks ? tbw : 0u, dense_tok};
+        // the apply lists touched blocks once the tokens pass sparse_from (test knob
+        // BPE355_SPARSE_FROM; below, scanning every cell costs less than building the list)
+        const unsigned sparse_from = [&] {
+            const char* e = std::getenv("BPE355_SPARSE_FROM");
+            // 16384 (r06h, merge phase at the bench config, two reps: 181.3-181.9 ms, against 182.6-182.8
+            // at 8192, 185.6-186.3 at 2048 and 184.5 with no marks)
+            return std::max(dense_tok, e ? (unsigned)std::max(0, std::atoi(e)) : 16384u);
+        }();
+        cm_ = CellMarks{nullptr, nullptr, marks ? tbw : 0u, dense_tok, sparse_from, nullptr};
         if (marks) {
             tb_.alloc(2ull * kTBRep * kMaxBatch * tbw);
             tbc_.alloc((size_t)kMaxBatch * tbw);
@@ -4120,6 +4141,9 @@ void MergeLoop<TokT>::launch_block(int slot, bool timing, std::vector<hipEvent_t
     const size_t lr_member = lr_member_, lr_parity = (size_t)kMaxBatch * lr_member;
     const unsigned ntb = tok_cap_;
     const unsigned apply_blocks = kApplyBatchBlocks;
+    // whether this block's applies may list touched blocks: the tokens may pass cm_.sparse_from
+    // within the two blocks in flight (the apply decides from the batch's own count)
+    const int sparse_hint = cm_.tbw && (long long)hs_.ntok + 2ll * trips_ * kMaxBatch >= (long long)cm_.sparse_from;
     int* ti = trip_info_.p + (size_t)slot * kTI * kTrips;
     slot_base_[slot] = trips_launched_;
     for (int t = 0; t < trips_; ++t) {
@@ -4144,7 +4168,7 @@ void MergeLoop<TokT>::launch_block(int slot, bool timing, std::vector<hipEvent_t
                                lr_member, lr_parity, (const unsigned*)cm_.tb, cm_.tbw, dbg_.p);
         hipLaunchKernelGGL(k_apply_batch, dim3(apply_blocks), dim3(kApplyBatchThreads), 0, s_, st_.p, bs_.p,
                            (const Batch*)batch_.p, pairs(), toks(), LR_.p, lr_member, lr_parity, ntb, part_.p,
-                           list_.p, 0, cm_);
+                           list_.p, 0, cm_, sparse_hint);
         if (sig_.p)
             hipLaunchKernelGGL(k_check_sig, dim3(1), dim3(256), 0, s_, (const Batch*)batch_.p, sig_.p,
                                (unsigned)kApplyBatchBlocks, dbg_.p);
