@@ -240,6 +240,10 @@ def main():
               file=sys.stderr, flush=True)
     barrier()
 
+    def note(msg):   # progress on stderr (a long run stays visibly alive)
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
     def train_file():   # steps repeat, so the corpus buffer and the counter's scratch are kept
         if multiproc:
             return train_bpe(path, args.vocab, [EOT], comm=comm, split_file=True, keep_device_buffers=True)
@@ -263,6 +267,7 @@ def main():
         barrier()
         elapsed = max_over_ranks(time.perf_counter() - t0)
         L.bpe_set_timing(0)
+        note(f"{args.steps} timed file steps: {elapsed / args.steps * 1e3:.1f} ms per step")
 
     def traffic_of(kernel):
         """HBM bytes per launch from the committed PMC passes (tools/gpu_pmc_all.sh): the newest
@@ -445,7 +450,10 @@ def main():
     # ---------------------------------------------------------------- CPU baseline (rank 0, N=1)
     cpu = None
     if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
+        note("GPU legs done; CPU baselines (oracle/cpu_bench.py)")
+        t_cpu = time.perf_counter()
         cpu = cpu_baselines(args, path, vocab, merges, L)
+        note(f"CPU baselines: {time.perf_counter() - t_cpu:.1f} s")
 
     if rank == 0:
         s0 = stats[-1]

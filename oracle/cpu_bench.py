@@ -201,6 +201,8 @@ def exact_leg(threads, corpus=None, golden="train_C2", piece=64 << 20):
         counters[0].absorb(c)
         c.close()
     t_count = time.perf_counter() - t0
+    print(f"[cpu_bench] exact leg: counted {n / 1e9:.2f} GB on {threads} threads in {t_count:.1f} s; training",
+          file=sys.stderr, flush=True)
     vocab, merges = counters[0].train(g["vocab"])
     wall = time.perf_counter() - t0
     counters[0].close()
@@ -238,6 +240,11 @@ def main():
         m = int(float(s) * 1e6) // BLOCK * BLOCK
         legs.append((a.corpus, m, a.vocab, a.cap_s))
     out = {"host_cpus": os.cpu_count(), "threads": host_threads()}
+    t_all = time.perf_counter()
+
+    def note(msg):   # progress on stderr (bench.py's log shows the run is alive)
+        print(f"[cpu_bench {time.perf_counter() - t_all:6.1f}s] {msg}", file=sys.stderr, flush=True)
+    note(f"legs: c1, training samples {a.samples_mb} MB, encode {a.encode_mb} MB; {a.procs} threads")
     ctx = mp.get_context("fork")
     with ctx.Pool(len(legs)) as pool:
         async_train = pool.map_async(_train_leg, legs)
@@ -245,11 +252,15 @@ def main():
             m = int(a.encode_mb * 1e6) // BLOCK * BLOCK
             out["encode"], piece0 = encode_leg(a.corpus, m, a.merges_json, max(1, a.procs - len(legs)))
             out["encode_piece0_ids_sha256"] = hashlib.sha256(struct.pack(f"<{len(piece0)}I", *piece0)).hexdigest()
+        note("encode leg done")
         res = async_train.get()
+    note("training legs done")
     out["c1"] = res[0]
     out["train"] = res[1:]
     if not a.no_exact:
+        note(f"exact leg ({a.exact_golden})")
         out["exact"] = exact_leg(a.procs, a.exact_corpus, a.exact_golden)
+        note(f"exact leg done: {out['exact']['wall_s']} s, exact {out['exact']['exact']}")
     with open(a.out, "w") as f:
         json.dump(out, f)
 
