@@ -119,6 +119,14 @@ for step in "$@"; do
       env $ENVS timeout -k 10 300 python -u bench.py --no-file --no-encode --no-cpu-baseline --steps 3 --warmup 1 > $OUT/abe_${tag}_$rep.log 2>&1 || { echo "abenvs failed"; tail -20 $OUT/abe_${tag}_$rep.log; exit 1; }
       python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().split(chr(10))[-1]); m=d['merge_loop']; print('$sp rep $rep merge_ms', m['ms'], 'us_per_trip', m['us_per_trip'], 'k_us', m['k_merge_batch_us'], 'trips', m['trips'], 'parity', d['parity']['parity'])" $OUT/abe_${tag}_$rep.log
     done; done ;;
+  abenc:*)   # device encode of the bench corpus under env settings (abenc:default,A=1), corpus in HBM, 2 reps
+    SPECS=${step#abenc:}; SPECS=${SPECS//,/ }
+    for rep in 1 2; do for sp in $SPECS; do
+      if [ "$sp" = default ]; then ENVS=""; else ENVS=${sp//+/ }; fi
+      tag=${sp//[=+]/_}
+      env $ENVS timeout -k 10 300 python -u bench.py --no-file --no-cpu-baseline --steps 1 --warmup 0 > $OUT/abenc_${tag}_$rep.log 2>&1 || { echo "abenc failed"; tail -20 $OUT/abenc_${tag}_$rep.log; exit 1; }
+      python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().split(chr(10))[-1]); e=d['encode']; print('$sp rep $rep encode MB/s', e['value'], 's', e['seconds'], 'ids', e['ids_rank0'])" $OUT/abenc_${tag}_$rep.log
+    done; done ;;
   c4)
     BPE355_STATS_OUT=$OUT/c4_exchange.json timeout -k 10 600 python -u -m pytest tests/test_gpu_c4.py -x -q --timeout 380 --timeout-method thread -k "words_full or rounds" > $OUT/c4.log 2>&1 || { echo "c4 failed"; tail -20 $OUT/c4.log; exit 1; }
     cat $OUT/c4_exchange*.json ;;
