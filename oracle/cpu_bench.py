@@ -203,7 +203,21 @@ def exact_leg(threads, corpus=None, golden="train_C2", piece=64 << 20):
     t_count = time.perf_counter() - t0
     print(f"[cpu_bench] exact leg: counted {n / 1e9:.2f} GB on {threads} threads in {t_count:.1f} s; training",
           file=sys.stderr, flush=True)
-    vocab, merges = counters[0].train(g["vocab"])
+    # a heartbeat while the merge loop runs (one C call that prints nothing): a run that writes
+    # nothing for minutes reads as hung
+    done = threading.Event()
+
+    def beat():
+        while not done.wait(30.0):
+            print(f"[cpu_bench] exact leg: training, {time.perf_counter() - t0 - t_count:.0f} s", file=sys.stderr,
+                  flush=True)
+    hb = threading.Thread(target=beat, daemon=True)
+    hb.start()
+    try:
+        vocab, merges = counters[0].train(g["vocab"])
+    finally:
+        done.set()
+        hb.join()
     wall = time.perf_counter() - t0
     counters[0].close()
     del buf

@@ -127,6 +127,13 @@ for step in "$@"; do
       env $ENVS timeout -k 10 300 python -u bench.py --no-file --no-cpu-baseline --steps 1 --warmup 0 > $OUT/abenc_${tag}_$rep.log 2>&1 || { echo "abenc failed"; tail -20 $OUT/abenc_${tag}_$rep.log; exit 1; }
       python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().split(chr(10))[-1]); e=d['encode']; print('$sp rep $rep encode MB/s', e['value'], 's', e['seconds'], 'ids', e['ids_rank0'])" $OUT/abenc_${tag}_$rep.log
     done; done ;;
+  exactc3)   # the exact C oracle on the full C3 corpus (generated into host memory), host's share of cores
+    timeout -k 10 900 python -u -c "
+import json, sys; sys.path[:0] = ['transformer-lm_amd', '.']
+from oracle.cpu_bench import exact_leg, host_threads
+r = exact_leg(host_threads(), None, 'train_C3')
+json.dump(r, open('$OUT/exact_cpu_C3.json', 'w'), indent=1); print(r)" > $OUT/exact_c3.log 2>&1 || { echo "exact C3 failed"; tail -5 $OUT/exact_c3.log; exit 1; }
+    tail -1 $OUT/exact_c3.log ;;
   c4)
     BPE355_STATS_OUT=$OUT/c4_exchange.json timeout -k 10 600 python -u -m pytest tests/test_gpu_c4.py -x -q --timeout 380 --timeout-method thread -k "words_full or rounds" > $OUT/c4.log 2>&1 || { echo "c4 failed"; tail -20 $OUT/c4.log; exit 1; }
     cat $OUT/c4_exchange*.json ;;
