@@ -1023,11 +1023,6 @@ constexpr unsigned kPairSlots = 4096;
 #define BPE355_LATE_COUNT 1
 #endif
 constexpr bool kLateCount = BPE355_LATE_COUNT != 0;
-// ... and in a full scan too (build knob; 0: a full scan loads every word's count with its slot)
-#ifndef BPE355_LATE_COUNT_FULL
-#define BPE355_LATE_COUNT_FULL 0
-#endif
-constexpr bool kLateCountFull = BPE355_LATE_COUNT_FULL != 0;
 __device__ __forceinline__ unsigned pair_h12(unsigned x, unsigned y) {
     return ((x * 0x9E3779B1u) ^ (y * 0x85EBCA77u)) >> 20;
 }
@@ -1820,8 +1815,7 @@ __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigne
     // most entries miss, only on a hit, beside the claim (one random line less per missing entry,
     // and the claim's round trip covers the load)
     unsigned long long c = 0;
-    const bool late = kLateCount && (tags || kLateCountFull);
-    if (!late) c = S.cnt[i];
+    if (!(kLateCount && tags)) c = S.cnt[i];
     TokT e[W];
     __builtin_memcpy(e, r, sizeof(e));
     // the members this word holds: no member's b is another's a and the new tokens are fresh, so
@@ -1865,7 +1859,7 @@ __device__ __forceinline__ void merge_word_batch(const SlotCls<TokT>& S, unsigne
     // another thread's claim was loaded after that claim, so its copy here, torn or not, ends in a
     // failed claim or in no hit: only the claimant ever writes it.
     if (!hits) return;
-    if (late) c = S.cnt[i];
+    if (kLateCount && tags) c = S.cnt[i];
     if (tags && atomicMax(&tags[f], B.batch_id) >= B.batch_id) return;
     if (kRegRewrite && W <= kRegRewriteMaxW) {   // every member in registers, one compacting store
         const auto sink_of = [&](int j) {
