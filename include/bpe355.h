@@ -126,6 +126,11 @@ size_t bpe_result_vocab_blob(const bpe_result* r, const uint8_t** data);
  * (Host-side plumbing for the Python shim: one buffer sliced, not one parse per record.) */
 size_t bpe_result_flat(const bpe_result* r, int which, const uint32_t** lens, const uint8_t** bytes,
                        size_t* n_bytes);
+/* The merges as vocab ids: *ids gets (a0, b0, a1, b1, ...), the ids of flat record order 1 whose
+ * bytes each merge joins; returns the merge count (0: not available, use bpe_result_flat 0).  The
+ * Python shim then builds merges from the vocab's own bytes objects, as the reference does when it
+ * appends (vocab[a], vocab[b]) (train.py:191-196), instead of one new bytes object per part. */
+size_t bpe_result_merge_ids(const bpe_result* r, const uint32_t** ids);
 
 typedef struct {
     double t_total_ms;        /* whole call, host wall clock */

@@ -31,6 +31,32 @@ def test_reference_fixture_corpus_en_500():
     assert set(vocab.values()) == set(ref_vocab.values())
 
 
+def test_merges_are_vocab_objects_and_match_the_flat_view():
+    """The result's merges come from bpe_result_merge_ids: each part is the vocab's own bytes
+    object (as the reference appends (vocab[a], vocab[b]), train.py:191-196), and the pairs equal
+    the byte records of bpe_result_flat(0) (the view the shim falls back to)."""
+    import ctypes
+    from bpe_amd import _lib
+    L = _lib.lib()
+    arr, n, _keep = _lib.c_strings(["<|endoftext|>"])
+    data = (gpt2_files.FIXTURES / "corpus.en").read_bytes()
+    res = ctypes.c_void_p()
+    _lib.check(L.bpe_train_buffer(data, len(data), 500, arr, n, None, ctypes.byref(res)), "train")
+    lens, buf, nb = ctypes.POINTER(ctypes.c_uint32)(), ctypes.c_void_p(), ctypes.c_size_t(0)
+    k = L.bpe_result_flat(res, 0, ctypes.byref(lens), ctypes.byref(buf), ctypes.byref(nb))
+    raw = ctypes.string_at(buf, nb.value)
+    parts, o = [], 0
+    for i in range(k):
+        parts.append(raw[o:o + lens[i]])
+        o += lens[i]
+    ids = ctypes.POINTER(ctypes.c_uint32)()
+    assert L.bpe_result_merge_ids(res, ctypes.byref(ids)) == k // 2 > 0
+    vocab, merges, _ = _lib.take_result(res)   # (frees res)
+    assert merges == list(zip(parts[0::2], parts[1::2]))
+    objs = {id(b) for b in vocab.values()}
+    assert all(id(a) in objs and id(b) in objs for a, b in merges)
+
+
 @pytest.mark.parametrize("name", G.names("train"))
 def test_train_matches_reference_golden(name):
     o, vocab, merges = G.train_expect(name)

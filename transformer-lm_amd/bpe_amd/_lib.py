@@ -96,6 +96,7 @@ _SIGS = [
     ("bpe_result_vocab_blob", _SZ, [_P, ctypes.POINTER(_P)]),
     ("bpe_result_flat", ctypes.c_size_t, [_P, ctypes.c_int, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32)),
                                            ctypes.POINTER(_P), ctypes.POINTER(_SZ)]),
+    ("bpe_result_merge_ids", ctypes.c_size_t, [_P, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32))]),
     ("bpe_result_stats", ctypes.c_int, [_P, ctypes.POINTER(TrainStats)]),
     ("bpe_result_free", None, [_P]),
     ("bpe_release_device_memory", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_SZ)]),
@@ -228,13 +229,23 @@ def take_result(res: ctypes.c_void_p):
         buf = ctypes.string_at(data, nb.value)
         return [buf[a:b] for a, b in zip(off, off[1:])]
     try:
-        m = flat(0)
         v = flat(1)
+        # the merges as vocab ids: each part is the vocab's own bytes object (the reference appends
+        # (vocab[a], vocab[b]), train.py:191-196), not one new object per part
+        ids = ctypes.POINTER(ctypes.c_uint32)()
+        nm = L.bpe_result_merge_ids(res, ctypes.byref(ids))
+        if nm:
+            iv = memoryview((ctypes.c_uint32 * (2 * nm)).from_address(ctypes.addressof(ids.contents)))
+            iv = iv.cast("B").cast("I").tolist()
+            g = v.__getitem__
+            merges = list(zip(map(g, iv[0::2]), map(g, iv[1::2])))
+        else:
+            m = flat(0)
+            merges = list(zip(m[0::2], m[1::2]))
         st = TrainStats()
         check(L.bpe_result_stats(res, ctypes.byref(st)), "stats")
     finally:
         L.bpe_result_free(res)
-    merges = list(zip(m[0::2], m[1::2]))
     vocab = dict(enumerate(v))
     return vocab, merges, st.as_dict()
 

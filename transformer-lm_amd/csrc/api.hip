@@ -8,6 +8,8 @@
 #include <cstring>
 #include <fstream>
 #include <memory>
+#include <string_view>
+#include <unordered_map>
 #include <unordered_set>
 #include <string>
 #include <vector>
@@ -94,6 +96,7 @@ struct bpe_result {
     // the same records as (lengths, concatenated bytes): the Python shim slices one buffer
     std::vector<uint32_t> flat_len[2];   // 0: merges (a, b, a, b, ...), 1: vocab in id order
     std::string flat_bytes[2];
+    std::vector<uint32_t> merge_ids;     // (a, b, a, b, ...) as vocab ids (empty: unavailable)
     int64_t n_merges = 0, n_vocab = 0;
     bpe_train_stats stats{};
 };
@@ -112,18 +115,33 @@ namespace {
 
 // Vocab(special_tokens) + add_token per merge (reference models/tokenizer/vocab.py:2-34)
 void finish_result(bpe::TrainOutput& out, const std::vector<std::string>& specials, bpe_result* r) {
-    std::vector<const std::string*> ids;
-    std::unordered_set<std::string> seen;
-    std::vector<std::string> extra;
-    extra.reserve(out.merges.size());
-    auto add = [&](const std::string& s) {
-        if (seen.insert(s).second) ids.push_back(&*seen.find(s));
+    // the vocab in id order: a token whose bytes are already there is not added again
+    // (vocab.py:29); every container sized up front (no rehash, and the vector never moves, so
+    // the views the index keeps into its strings stay valid)
+    const size_t cap = specials.size() + 256 + out.merges.size();
+    std::vector<std::string> toks;
+    toks.reserve(cap);
+    std::unordered_map<std::string_view, uint32_t> id_of;
+    id_of.reserve(2 * cap);
+    auto add = [&](std::string s) {
+        if (id_of.count(s)) return;
+        toks.push_back(std::move(s));
+        id_of.emplace(toks.back(), (uint32_t)(toks.size() - 1));
     };
     for (const auto& s : specials) add(s);
     for (int b = 0; b < 256; ++b) add(std::string(1, (char)b));
-    for (const auto& m : out.merges) add(m.first + m.second);
+    size_t mb = 0;
+    for (const auto& m : out.merges) {
+        add(m.first + m.second);
+        mb += m.first.size() + m.second.size();
+    }
     r->n_merges = (int64_t)out.merges.size();
-    r->n_vocab = (int64_t)ids.size();
+    r->n_vocab = (int64_t)toks.size();
+    r->merges_blob.reserve(mb + 8 * out.merges.size());
+    r->flat_bytes[0].reserve(mb);
+    r->flat_len[0].reserve(2 * out.merges.size());
+    r->merge_ids.reserve(2 * out.merges.size());
+    bool ids_ok = true;
     for (const auto& m : out.merges) {
         bpe::put_u32(r->merges_blob, (uint32_t)m.first.size());
         r->merges_blob += m.first;
@@ -133,12 +151,22 @@ void finish_result(bpe::TrainOutput& out, const std::vector<std::string>& specia
         r->flat_len[0].push_back((uint32_t)m.second.size());
         r->flat_bytes[0] += m.first;
         r->flat_bytes[0] += m.second;
+        const auto ia = id_of.find(m.first), ib = id_of.find(m.second);   // (a part is always a token)
+        if (ia == id_of.end() || ib == id_of.end()) { ids_ok = false; continue; }
+        r->merge_ids.push_back(ia->second);
+        r->merge_ids.push_back(ib->second);
     }
-    for (const auto* s : ids) {
-        bpe::put_u32(r->vocab_blob, (uint32_t)s->size());
-        r->vocab_blob += *s;
-        r->flat_len[1].push_back((uint32_t)s->size());
-        r->flat_bytes[1] += *s;
+    if (!ids_ok) r->merge_ids.clear();
+    size_t vb = 0;
+    for (const auto& s : toks) vb += s.size();
+    r->vocab_blob.reserve(vb + 4 * toks.size());
+    r->flat_bytes[1].reserve(vb);
+    r->flat_len[1].reserve(toks.size());
+    for (const auto& s : toks) {
+        bpe::put_u32(r->vocab_blob, (uint32_t)s.size());
+        r->vocab_blob += s;
+        r->flat_len[1].push_back((uint32_t)s.size());
+        r->flat_bytes[1] += s;
     }
     r->stats = out.stats;
 }
@@ -337,6 +365,12 @@ size_t bpe_result_flat(const bpe_result* r, int which, const uint32_t** lens, co
     *bytes = reinterpret_cast<const uint8_t*>(r->flat_bytes[which].data());
     *n_bytes = r->flat_bytes[which].size();
     return r->flat_len[which].size();
+}
+
+size_t bpe_result_merge_ids(const bpe_result* r, const uint32_t** ids) {
+    if (!r || !ids || r->merge_ids.size() != 2 * (size_t)r->n_merges) return 0;
+    *ids = r->merge_ids.data();
+    return (size_t)r->n_merges;
 }
 
 int64_t bpe_result_n_merges(const bpe_result* r) { return r ? r->n_merges : -1; }
