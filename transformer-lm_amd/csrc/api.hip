@@ -8,6 +8,7 @@
 #include <cstring>
 #include <fstream>
 #include <memory>
+#include <mutex>
 #include <string_view>
 #include <unordered_map>
 #include <unordered_set>
@@ -92,13 +93,17 @@ bool timing_enabled() { return g_timing; }
 }  // namespace bpe
 
 struct bpe_result {
-    std::string merges_blob, vocab_blob;
-    // the same records as (lengths, concatenated bytes): the Python shim slices one buffer
-    std::vector<uint32_t> flat_len[2];   // 0: merges (a, b, a, b, ...), 1: vocab in id order
-    std::string flat_bytes[2];
+    std::vector<std::pair<std::string, std::string>> merges;   // byte pairs, in order
+    std::vector<std::string> vocab;                            // id order
     std::vector<uint32_t> merge_ids;     // (a, b, a, b, ...) as vocab ids (empty: unavailable)
     int64_t n_merges = 0, n_vocab = 0;
     bpe_train_stats stats{};
+    // the byte views, built on first request (the Python shim asks only for the vocab's flat
+    // records and the merge ids): blobs, and (lengths, concatenated bytes) records to slice
+    mutable std::once_flag once_mblob, once_vblob, once_flat[2];
+    mutable std::string merges_blob, vocab_blob;
+    mutable std::vector<uint32_t> flat_len[2];   // 0: merges (a, b, a, b, ...), 1: vocab in id order
+    mutable std::string flat_bytes[2];
 };
 
 struct bpe_comm {
@@ -130,44 +135,19 @@ void finish_result(bpe::TrainOutput& out, const std::vector<std::string>& specia
     };
     for (const auto& s : specials) add(s);
     for (int b = 0; b < 256; ++b) add(std::string(1, (char)b));
-    size_t mb = 0;
-    for (const auto& m : out.merges) {
-        add(m.first + m.second);
-        mb += m.first.size() + m.second.size();
-    }
+    for (const auto& m : out.merges) add(m.first + m.second);
     r->n_merges = (int64_t)out.merges.size();
     r->n_vocab = (int64_t)toks.size();
-    r->merges_blob.reserve(mb + 8 * out.merges.size());
-    r->flat_bytes[0].reserve(mb);
-    r->flat_len[0].reserve(2 * out.merges.size());
     r->merge_ids.reserve(2 * out.merges.size());
-    bool ids_ok = true;
     for (const auto& m : out.merges) {
-        bpe::put_u32(r->merges_blob, (uint32_t)m.first.size());
-        r->merges_blob += m.first;
-        bpe::put_u32(r->merges_blob, (uint32_t)m.second.size());
-        r->merges_blob += m.second;
-        r->flat_len[0].push_back((uint32_t)m.first.size());
-        r->flat_len[0].push_back((uint32_t)m.second.size());
-        r->flat_bytes[0] += m.first;
-        r->flat_bytes[0] += m.second;
         const auto ia = id_of.find(m.first), ib = id_of.find(m.second);   // (a part is always a token)
-        if (ia == id_of.end() || ib == id_of.end()) { ids_ok = false; continue; }
+        if (ia == id_of.end() || ib == id_of.end()) { r->merge_ids.clear(); break; }
         r->merge_ids.push_back(ia->second);
         r->merge_ids.push_back(ib->second);
     }
-    if (!ids_ok) r->merge_ids.clear();
-    size_t vb = 0;
-    for (const auto& s : toks) vb += s.size();
-    r->vocab_blob.reserve(vb + 4 * toks.size());
-    r->flat_bytes[1].reserve(vb);
-    r->flat_len[1].reserve(toks.size());
-    for (const auto& s : toks) {
-        bpe::put_u32(r->vocab_blob, (uint32_t)s.size());
-        r->vocab_blob += s;
-        r->flat_len[1].push_back((uint32_t)s.size());
-        r->flat_bytes[1] += s;
-    }
+    id_of.clear();   // (views into toks: dropped before toks moves)
+    r->merges = std::move(out.merges);
+    r->vocab = std::move(toks);
     r->stats = out.stats;
 }
 
@@ -361,6 +341,30 @@ void bpe_blob_free(uint8_t* blob) { std::free(blob); }
 size_t bpe_result_flat(const bpe_result* r, int which, const uint32_t** lens, const uint8_t** bytes,
                        size_t* n_bytes) {
     if (!r || which < 0 || which > 1 || !lens || !bytes || !n_bytes) return 0;
+    std::call_once(r->once_flat[which], [&] {
+        std::vector<uint32_t>& L = r->flat_len[which];
+        std::string& B = r->flat_bytes[which];
+        size_t nb = 0;
+        if (which == 0) {
+            for (const auto& m : r->merges) nb += m.first.size() + m.second.size();
+            L.reserve(2 * r->merges.size());
+            B.reserve(nb);
+            for (const auto& m : r->merges) {
+                L.push_back((uint32_t)m.first.size());
+                L.push_back((uint32_t)m.second.size());
+                B += m.first;
+                B += m.second;
+            }
+        } else {
+            for (const auto& t : r->vocab) nb += t.size();
+            L.reserve(r->vocab.size());
+            B.reserve(nb);
+            for (const auto& t : r->vocab) {
+                L.push_back((uint32_t)t.size());
+                B += t;
+            }
+        }
+    });
     *lens = r->flat_len[which].data();
     *bytes = reinterpret_cast<const uint8_t*>(r->flat_bytes[which].data());
     *n_bytes = r->flat_bytes[which].size();
@@ -377,11 +381,25 @@ int64_t bpe_result_n_merges(const bpe_result* r) { return r ? r->n_merges : -1; 
 int64_t bpe_result_n_vocab(const bpe_result* r) { return r ? r->n_vocab : -1; }
 size_t bpe_result_merges_blob(const bpe_result* r, const uint8_t** data) {
     if (!r || !data) return 0;
+    std::call_once(r->once_mblob, [&] {
+        for (const auto& m : r->merges) {
+            bpe::put_u32(r->merges_blob, (uint32_t)m.first.size());
+            r->merges_blob += m.first;
+            bpe::put_u32(r->merges_blob, (uint32_t)m.second.size());
+            r->merges_blob += m.second;
+        }
+    });
     *data = reinterpret_cast<const uint8_t*>(r->merges_blob.data());
     return r->merges_blob.size();
 }
 size_t bpe_result_vocab_blob(const bpe_result* r, const uint8_t** data) {
     if (!r || !data) return 0;
+    std::call_once(r->once_vblob, [&] {
+        for (const auto& t : r->vocab) {
+            bpe::put_u32(r->vocab_blob, (uint32_t)t.size());
+            r->vocab_blob += t;
+        }
+    });
     *data = reinterpret_cast<const uint8_t*>(r->vocab_blob.data());
     return r->vocab_blob.size();
 }
