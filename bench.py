@@ -166,9 +166,11 @@ def cpu_baselines(args, path, vocab, merges, L):
     big = max(ok or r["train"], key=lambda x: x["bytes"])
     cores = os.cpu_count()
     enc = r["encode"]
-    c3 = None   # the committed run of the exact leg at C3 (tools/exact_c3.sh on the GPU box's host)
-    c3f = ROOT / "profiles" / "r06" / "exact_cpu_C3.json"
-    if c3f.exists() and not (r.get("exact") or {}).get("config") == "train_C3":
+    c3 = None   # the newest committed run of the exact leg at C3 (tools/gpu_r06.sh exactc3, the box's host)
+    c3s = sorted((p for p in (ROOT / "profiles").glob("r[0-9]*") if (p / "exact_cpu_C3.json").exists()),
+                 key=lambda p: int(p.name[1:]) if p.name[1:].isdigit() else -1)
+    c3f = c3s[-1] / "exact_cpu_C3.json" if c3s else None
+    if c3f is not None and not (r.get("exact") or {}).get("config") == "train_C3":
         c3 = dict(json.loads(c3f.read_text()), source_file=str(c3f.relative_to(ROOT)),
                   note="committed run of this leg on the full C3 corpus (BASELINE configs[2]), not measured in "
                        "this bench run: python bench.py --exact-c3 measures it (~5 min of CPU legs)")
