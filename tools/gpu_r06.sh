@@ -2,7 +2,9 @@
 # Round-6 GPU call.  usage: tools/gpu_r06.sh TAG [tests|quick|bench|prof|c4] ...
 #   quick: the tests this round added or changed; tests: the whole -m gpu suite + smoke;
 #   bench: the default bench line (CPU baselines included); prof: rocprofv3 kernel summary of the
-#   HBM-resident bench; c4: the 8-rank words exchange stats + rounds-mode stats.
+#   HBM-resident bench; c4: the 8-rank words exchange stats + rounds-mode stats; pmc: the HBM traffic
+#   passes; exactc3: the exact C oracle on the full C3 corpus; ab*/abenc*/trainpar:*: A/Bs and the
+#   train parity tests of build/variants/NAME.
 set -o pipefail
 TAG=${1:-r06}
 shift
